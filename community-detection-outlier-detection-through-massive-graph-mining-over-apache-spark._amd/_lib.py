@@ -1,0 +1,142 @@
+"""ctypes binding of liblpa_hip.so (C ABI in include/lpa.h).
+
+The library is the product: there is no CPU fallback.  If the shared object
+is missing, loading fails loudly with instructions to build it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblpa_hip.so")
+
+LPA_OK = 0
+LPA_EINVAL = -22
+LPA_ENOMEM = -12
+LPA_ENODEV = -19
+LPA_EHIP = -1000
+LPA_ERCCL = -2000
+LPA_INPUT_DEVICE = 0x1
+LPA_NBINS = 8
+LPA_STATS_MAX_ITERS = 64
+BIN_NAMES = ("seg", "wave", "g16", "g8", "g4", "g2", "g1", "isolated")
+
+
+class LpaStats(ctypes.Structure):
+    _fields_ = [
+        ("iters", ctypes.c_int32),
+        ("n_iter_ms", ctypes.c_int32),
+        ("iter_ms", ctypes.c_float * LPA_STATS_MAX_ITERS),
+        ("bin_ms", ctypes.c_float * LPA_NBINS),
+        ("exchange_ms", ctypes.c_float),
+        ("total_ms", ctypes.c_double),
+    ]
+
+    def to_dict(self):
+        return dict(iters=self.iters, iter_ms=list(self.iter_ms[: self.n_iter_ms]),
+                    bin_ms={BIN_NAMES[b]: self.bin_ms[b] for b in range(LPA_NBINS)},
+                    exchange_ms=self.exchange_ms, total_ms=self.total_ms)
+
+
+class LpaGraphInfo(ctypes.Structure):
+    _fields_ = [
+        ("V", ctypes.c_int64), ("m", ctypes.c_int64), ("arcs", ctypes.c_int64),
+        ("slice", ctypes.c_int64), ("own_begin", ctypes.c_int64),
+        ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("device", ctypes.c_int32),
+        ("max_degree", ctypes.c_int32),
+        ("bin_vertices", ctypes.c_int64 * LPA_NBINS), ("bin_arcs", ctypes.c_int64 * LPA_NBINS),
+        ("hub_vertices", ctypes.c_int64), ("segments", ctypes.c_int64),
+        ("device_bytes", ctypes.c_int64),
+    ]
+
+    def to_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("bin_vertices", "bin_arcs")}
+        d["bin_vertices"] = {BIN_NAMES[b]: self.bin_vertices[b] for b in range(LPA_NBINS)}
+        d["bin_arcs"] = {BIN_NAMES[b]: self.bin_arcs[b] for b in range(LPA_NBINS)}
+        return d
+
+
+class LpaOutlierSummary(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in (
+        "n_groups", "k", "threshold", "n_flagged", "n_communities", "n_communities_flagged",
+        "distinct_edges")]
+
+    def to_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# every symbol include/lpa.h declares, with its ctypes signature
+_vp = ctypes.c_void_p
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+SIGNATURES = {
+    "lpa_graph_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "lpa_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "lpa_graph_create_dist": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "lpa_set_stream": (ctypes.c_int, [_vp, _vp]),
+    "lpa_reset": (ctypes.c_int, [_vp]),
+    "lpa_step": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(LpaStats)]),
+    "lpa_get_labels": (ctypes.c_int, [_vp, _vp, ctypes.c_int32]),
+    "lpa_run": (ctypes.c_int, [_vp, ctypes.c_int32, _vp, ctypes.c_int32, ctypes.POINTER(LpaStats)]),
+    "lpa_outlier": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                   _i64p, _i64p, _i32p, _u8p, ctypes.POINTER(LpaOutlierSummary)]),
+    "lpa_degrees": (ctypes.c_int, [_vp, _i32p]),
+    "lpa_exchange_get": (ctypes.c_int, [_vp, _i32p]),
+    "lpa_exchange_put": (ctypes.c_int, [_vp, _i32p]),
+    "lpa_graph_get_info": (ctypes.c_int, [_vp, ctypes.POINTER(LpaGraphInfo)]),
+    "lpa_graph_destroy": (None, [_vp]),
+    "lpa_last_error": (ctypes.c_char_p, []),
+    "lpa_gen_rmat": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32,
+                                    _vp, _vp, ctypes.c_int32, _vp]),
+    "lpa_gen_sbm": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                                   ctypes.c_uint64, _vp, _vp, ctypes.c_int32, _vp]),
+}
+
+_lib = None
+
+
+class LpaError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (lpa error {code})")
+        self.code = code
+
+
+def load():
+    """Load liblpa_hip.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: the HIP library has not been built. "
+            "Run `python -c 'import __graft_entry__ as g; g.build()'` (or `make -C <pkg>/csrc`).")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().lpa_last_error()
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(rc: int):
+    """Map a C-ABI return code onto a Python exception (ValueError for bad arguments,
+    as GraphFrames raises for a bad schema / IllegalArgumentException for maxIter)."""
+    if rc == LPA_OK:
+        return
+    msg = last_error()
+    if rc == LPA_EINVAL:
+        raise ValueError(msg)
+    if rc == LPA_ENOMEM:
+        raise MemoryError(msg)
+    raise LpaError(rc, msg)

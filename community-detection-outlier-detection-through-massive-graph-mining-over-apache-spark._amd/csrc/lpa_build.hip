@@ -1,0 +1,365 @@
+// Graph construction on the GPU (replaces GraphFrames
+// indexedVertices/indexedEdges/cachedTopologyGraphX and the GraphX EdgePartition
+// build).
+//
+//   1. symmetrised degree of every vertex (each directed edge = one arc each way)
+//   2. degree-ranked vertex order: sort by (degree desc, id asc) -> internal slots.
+//      Rank r of P owns the vertices of degree rank k with k % P == r, at slot
+//      r*slice + k/P: every rank's slice is itself degree-sorted, slices are equal
+//      length (a plain allgather needs no padding) and carry ~A/P arcs each.
+//      Labels keep the ORIGINAL dense ids as values, so the smallest-label
+//      tie-break and the output are unaffected by the renumbering.
+//   3. owned arcs emitted as 64-bit keys (row << 32 | col), LSD radix sorted
+//      (rows sorted, neighbours ascending inside a row; hubs have the smallest
+//      slots, so their labels sit densely in a few cache lines).
+//   4. row_ptr = exclusive scan of owned degrees (int64: >2^31 arcs at scale 26).
+//   5. degree bins = contiguous slot ranges (binary search on the sorted degrees),
+//      hub segments and their global merge tables.
+#include "lpa_internal.h"
+
+namespace lpa {
+
+namespace {
+
+__global__ void k_degree(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                         int64_t m, int32_t V, int32_t* __restrict__ deg, int32_t* err) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int32_t s = src[e], d = dst[e];
+    if ((u32)s >= (u32)V || (u32)d >= (u32)V) {
+      atomicOr(err, 1);
+      continue;
+    }
+    atomicAdd(&deg[s], 1);
+    atomicAdd(&deg[d], 1);
+  }
+}
+
+__global__ void k_maxdeg(const int32_t* __restrict__ deg, int64_t V, int32_t* out) {
+  int32_t mx = 0;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x)
+    mx = max(mx, deg[v]);
+  for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, mx);
+}
+
+__global__ void k_vertex_keys(const int32_t* __restrict__ deg, int64_t V, int32_t maxdeg,
+                              u64* __restrict__ keys) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x)
+    keys[v] = ((u64)(u32)(maxdeg - deg[v]) << 32) | (u64)v;
+}
+
+__global__ void k_vertex_order(const u64* __restrict__ keys, int64_t V, int32_t P, int64_t S,
+                               int32_t* __restrict__ new_of, int32_t* __restrict__ old_of) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < V;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    int32_t old = (int32_t)(u32)keys[k];
+    int64_t slot = (k % P) * S + k / P;
+    new_of[old] = (int32_t)slot;
+    old_of[slot] = old;
+  }
+}
+
+__global__ void k_owned_degree(const int32_t* __restrict__ old_of_own,
+                               const int32_t* __restrict__ deg, int64_t S,
+                               int32_t* __restrict__ deg_own) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int32_t o = old_of_own[i];
+    deg_own[i] = o >= 0 ? deg[o] : 0;
+  }
+}
+
+// P == 1: every edge gives two arcs at fixed positions (no atomics)
+__global__ void k_emit_arcs_single(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                   int64_t m, const int32_t* __restrict__ new_of,
+                                   u64* __restrict__ keys) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    u64 s = (u32)new_of[src[e]], d = (u32)new_of[dst[e]];
+    keys[2 * e] = (s << 32) | d;
+    keys[2 * e + 1] = (d << 32) | s;
+  }
+}
+
+// P > 1: keep the arcs whose row is owned; row stored slice-local
+__global__ void k_emit_arcs_owned(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                  int64_t m, const int32_t* __restrict__ new_of, int64_t lo,
+                                  int64_t hi, u64* __restrict__ keys,
+                                  unsigned long long* cursor) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t s = new_of[src[e]], d = new_of[dst[e]];
+    if (s >= lo && s < hi) keys[atomicAdd(cursor, 1ull)] = ((u64)(s - lo) << 32) | (u64)d;
+    if (d >= lo && d < hi) keys[atomicAdd(cursor, 1ull)] = ((u64)(d - lo) << 32) | (u64)s;
+  }
+}
+
+__global__ void k_keys_to_col(const u64* __restrict__ keys, int64_t n, int32_t* __restrict__ col) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x)
+    col[j] = (int32_t)(u32)keys[j];
+}
+
+// first index in the non-increasing deg_own[0, S) with deg <= t, for each threshold
+__global__ void k_bin_bounds(const int32_t* __restrict__ deg_own, int64_t S,
+                             const int32_t* __restrict__ thr, int nthr, int64_t* __restrict__ out) {
+  int i = threadIdx.x;
+  if (i >= nthr) return;
+  int32_t t = thr[i];
+  int64_t lo = 0, hi = S;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (deg_own[mid] > t) lo = mid + 1; else hi = mid;
+  }
+  out[i] = lo;
+}
+
+__global__ void k_seg_counts(const int32_t* __restrict__ deg_own, int64_t n0,
+                             int32_t* __restrict__ nseg, int32_t* __restrict__ hubcap, int64_t n_hub) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n0;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    int32_t d = deg_own[v];
+    nseg[v] = (d + kSegArcs - 1) / kSegArcs;
+    if (v < n_hub) {
+      // global table: next power of two >= 2d
+      u32 c = 1u;
+      while (c < 2u * (u32)d) c <<= 1;
+      hubcap[v] = (int32_t)c;
+    }
+  }
+}
+
+__global__ void k_fill_segs(const int64_t* __restrict__ rp, const int32_t* __restrict__ deg_own,
+                            const int64_t* __restrict__ seg_off, int64_t n0, int64_t n_hub,
+                            Segment* __restrict__ segs) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n0;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    int32_t d = deg_own[v];
+    int64_t o = seg_off[v];
+    int32_t ns = (d + kSegArcs - 1) / kSegArcs;
+    for (int32_t j = 0; j < ns; ++j) {
+      Segment sg;
+      sg.begin = rp[v] + (int64_t)j * kSegArcs;
+      sg.len = min(kSegArcs, d - j * kSegArcs);
+      sg.v = v < n_hub ? -(int32_t)(v + 1) : (int32_t)v;
+      segs[o + j] = sg;
+    }
+  }
+}
+
+__global__ void k_init_labels(const int32_t* __restrict__ old_of, int64_t n, int32_t* __restrict__ a,
+                              int32_t* __restrict__ b) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int32_t o = old_of[i];
+    int32_t l = o >= 0 ? o : 0;
+    a[i] = l;
+    b[i] = l;
+  }
+}
+
+inline unsigned grid_for(int64_t n, int threads = 256) {
+  int64_t b = (n + threads - 1) / threads;
+  if (b < 1) b = 1;
+  if (b > 65536) b = 65536;
+  return (unsigned)b;
+}
+
+}  // namespace
+
+int init_labels(lpa_graph* g) {
+  hipLaunchKernelGGL(k_init_labels, dim3(grid_for(g->vpad)), dim3(256), 0, g->stream, g->old_of,
+                     g->vpad, g->lab[0], g->lab[1]);
+  LPA_HIP(hipGetLastError());
+  g->cur = 0;
+  return LPA_OK;
+}
+
+int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                uint32_t flags) {
+  hipStream_t s = g->stream;
+  const int32_t P = g->nranks, r = g->rank;
+  g->V = V;
+  g->m = m;
+  g->slice = ((int64_t)V + P - 1) / P;
+  if (g->slice == 0) g->slice = 1;
+  g->vpad = g->slice * P;
+  g->own_begin = (int64_t)r * g->slice;
+  const int64_t S = g->slice;
+
+  // ---- keep the edge list on the device (outlier stage needs it) ----
+  LPA_TRY(dev_alloc(g, (void**)&g->e_src, sizeof(int32_t) * (m > 0 ? m : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->e_dst, sizeof(int32_t) * (m > 0 ? m : 1)));
+  if (m > 0) {
+    hipMemcpyKind kind = (flags & LPA_INPUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    LPA_HIP(hipMemcpyAsync(g->e_src, src, sizeof(int32_t) * m, kind, s));
+    LPA_HIP(hipMemcpyAsync(g->e_dst, dst, sizeof(int32_t) * m, kind, s));
+  }
+
+  // ---- 1. degrees ----
+  int32_t* d_err = nullptr;
+  int32_t* d_max = nullptr;
+  LPA_HIP(hipMallocAsync((void**)&d_err, 2 * sizeof(int32_t), s));
+  d_max = d_err + 1;
+  LPA_HIP(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), s));
+  LPA_TRY(dev_alloc(g, (void**)&g->deg, sizeof(int32_t) * (V > 0 ? V : 1)));
+  LPA_HIP(hipMemsetAsync(g->deg, 0, sizeof(int32_t) * (V > 0 ? V : 1), s));
+  if (m > 0) {
+    hipLaunchKernelGGL(k_degree, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, V,
+                       g->deg, d_err);
+    LPA_HIP(hipGetLastError());
+  }
+  if (V > 0) {
+    hipLaunchKernelGGL(k_maxdeg, dim3(grid_for(V)), dim3(256), 0, s, g->deg, (int64_t)V, d_max);
+    LPA_HIP(hipGetLastError());
+  }
+  int32_t h_err[2] = {0, 0};
+  LPA_HIP(hipMemcpyAsync(h_err, d_err, sizeof(h_err), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  LPA_HIP(hipFreeAsync(d_err, s));
+  if (h_err[0]) {
+    set_error("edge endpoint outside [0, V=%d)", V);
+    return LPA_EINVAL;
+  }
+  g->max_degree = h_err[1];
+
+  // ---- 2. degree-ranked vertex order ----
+  LPA_TRY(dev_alloc(g, (void**)&g->new_of, sizeof(int32_t) * (V > 0 ? V : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->old_of, sizeof(int32_t) * g->vpad));
+  LPA_HIP(hipMemsetAsync(g->old_of, 0xFF, sizeof(int32_t) * g->vpad, s));
+  if (V > 0) {
+    u64* vk = nullptr;
+    LPA_HIP(hipMallocAsync((void**)&vk, sizeof(u64) * 2 * V, s));
+    hipLaunchKernelGGL(k_vertex_keys, dim3(grid_for(V)), dim3(256), 0, s, g->deg, (int64_t)V,
+                       g->max_degree, vk);
+    LPA_HIP(hipGetLastError());
+    int shifts[16], ns = 0;
+    int blo = bits_for((uint64_t)(V - 1)), bhi = bits_for((uint64_t)g->max_degree);
+    for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
+    for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
+    LPA_TRY(radix_sort_u64(vk, vk + V, V, shifts, ns, s));
+    hipLaunchKernelGGL(k_vertex_order, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, P, S,
+                       g->new_of, g->old_of);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipFreeAsync(vk, s));
+  }
+
+  // ---- owned degrees, row_ptr ----
+  int32_t* deg_own = nullptr;
+  LPA_HIP(hipMallocAsync((void**)&deg_own, sizeof(int32_t) * S, s));
+  hipLaunchKernelGGL(k_owned_degree, dim3(grid_for(S)), dim3(256), 0, s, g->old_of + g->own_begin,
+                     g->deg, S, deg_own);
+  LPA_HIP(hipGetLastError());
+  LPA_TRY(dev_alloc(g, (void**)&g->rp, sizeof(int64_t) * (S + 1)));
+  LPA_TRY(exclusive_scan_i32_i64(deg_own, g->rp, S, s));
+  int64_t arcs = 0;
+  LPA_HIP(hipMemcpyAsync(&arcs, g->rp + S, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  g->arcs = arcs;
+
+  // ---- 3. owned arcs, sorted ----
+  LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
+  if (arcs > 0) {
+    u64* keys = nullptr;
+    if (hipMallocAsync((void**)&keys, sizeof(u64) * 2 * arcs, s) != hipSuccess) {
+      set_error("out of device memory for %lld arc keys", (long long)(2 * arcs));
+      return LPA_ENOMEM;
+    }
+    if (P == 1) {
+      hipLaunchKernelGGL(k_emit_arcs_single, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
+                         g->e_dst, m, g->new_of, keys);
+    } else {
+      unsigned long long* cursor = nullptr;
+      LPA_HIP(hipMallocAsync((void**)&cursor, sizeof(unsigned long long), s));
+      LPA_HIP(hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
+      hipLaunchKernelGGL(k_emit_arcs_owned, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
+                         g->e_dst, m, g->new_of, g->own_begin, g->own_begin + S, keys, cursor);
+      LPA_HIP(hipFreeAsync(cursor, s));
+    }
+    LPA_HIP(hipGetLastError());
+    int shifts[16], ns = 0;
+    int blo = bits_for((uint64_t)(g->vpad - 1)), bhi = bits_for((uint64_t)(S - 1));
+    for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
+    for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
+    LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
+    hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipFreeAsync(keys, s));
+  }
+
+  // ---- 4. degree bins (contiguous slot ranges) ----
+  {
+    const int32_t thr_h[8] = {kWaveMaxDeg, 16, 8, 4, 2, 1, 0, kSegArcs};
+    int32_t* d_thr = nullptr;
+    int64_t* d_bb = nullptr;
+    LPA_HIP(hipMallocAsync((void**)&d_thr, sizeof(thr_h), s));
+    LPA_HIP(hipMallocAsync((void**)&d_bb, sizeof(int64_t) * 8, s));
+    LPA_HIP(hipMemcpyAsync(d_thr, thr_h, sizeof(thr_h), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_bin_bounds, dim3(1), dim3(64), 0, s, deg_own, S, d_thr, 8, d_bb);
+    LPA_HIP(hipGetLastError());
+    int64_t bb[8];
+    LPA_HIP(hipMemcpyAsync(bb, d_bb, sizeof(bb), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    LPA_HIP(hipFreeAsync(d_thr, s));
+    LPA_HIP(hipFreeAsync(d_bb, s));
+    g->bin_begin[0] = 0;
+    for (int b = 1; b < LPA_NBINS; ++b) g->bin_begin[b] = bb[b - 1];
+    g->bin_begin[LPA_NBINS] = S;
+    g->n_hub = bb[7];
+    int64_t rpb[LPA_NBINS + 1];
+    for (int b = 0; b <= LPA_NBINS; ++b)
+      LPA_HIP(hipMemcpyAsync(&rpb[b], g->rp + g->bin_begin[b], sizeof(int64_t),
+                             hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    for (int b = 0; b < LPA_NBINS; ++b) g->bin_arcs[b] = rpb[b + 1] - rpb[b];
+  }
+
+  // ---- 5. hub segments + global merge tables ----
+  const int64_t n0 = g->bin_begin[1];
+  if (n0 > 0) {
+    int32_t* nseg = nullptr;
+    int32_t* hubcap = nullptr;
+    int64_t* seg_off = nullptr;
+    LPA_HIP(hipMallocAsync((void**)&nseg, sizeof(int32_t) * n0, s));
+    LPA_HIP(hipMallocAsync((void**)&hubcap, sizeof(int32_t) * (g->n_hub > 0 ? g->n_hub : 1), s));
+    LPA_HIP(hipMallocAsync((void**)&seg_off, sizeof(int64_t) * (n0 + 1), s));
+    hipLaunchKernelGGL(k_seg_counts, dim3(grid_for(n0)), dim3(256), 0, s, deg_own, n0, nseg,
+                       hubcap, g->n_hub);
+    LPA_HIP(hipGetLastError());
+    LPA_TRY(exclusive_scan_i32_i64(nseg, seg_off, n0, s));
+    LPA_HIP(hipMemcpyAsync(&g->n_segs, seg_off + n0, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    LPA_TRY(dev_alloc(g, (void**)&g->segs, sizeof(Segment) * g->n_segs));
+    hipLaunchKernelGGL(k_fill_segs, dim3(grid_for(n0)), dim3(256), 0, s, g->rp, deg_own, seg_off,
+                       n0, g->n_hub, g->segs);
+    LPA_HIP(hipGetLastError());
+    if (g->n_hub > 0) {
+      LPA_TRY(dev_alloc(g, (void**)&g->hub_off, sizeof(int64_t) * (g->n_hub + 1)));
+      LPA_TRY(exclusive_scan_i32_i64(hubcap, g->hub_off, g->n_hub, s));
+      int64_t tot = 0;
+      LPA_HIP(hipMemcpyAsync(&tot, g->hub_off + g->n_hub, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      LPA_HIP(hipStreamSynchronize(s));
+      LPA_TRY(dev_alloc(g, (void**)&g->gtab, sizeof(u64) * tot));
+      LPA_TRY(dev_alloc(g, (void**)&g->glist, sizeof(int32_t) * tot));
+      LPA_TRY(dev_alloc(g, (void**)&g->gcnt, sizeof(int32_t) * g->n_hub));
+      LPA_HIP(hipMemsetAsync(g->gtab, 0, sizeof(u64) * tot, s));
+      LPA_HIP(hipMemsetAsync(g->gcnt, 0, sizeof(int32_t) * g->n_hub, s));
+    }
+    LPA_HIP(hipFreeAsync(nseg, s));
+    LPA_HIP(hipFreeAsync(hubcap, s));
+    LPA_HIP(hipFreeAsync(seg_off, s));
+  }
+  LPA_HIP(hipFreeAsync(deg_own, s));
+
+  // ---- labels (replicated, ping-pong) ----
+  LPA_TRY(dev_alloc(g, (void**)&g->lab[0], sizeof(int32_t) * g->vpad));
+  LPA_TRY(dev_alloc(g, (void**)&g->lab[1], sizeof(int32_t) * g->vpad));
+  LPA_TRY(init_labels(g));
+  LPA_HIP(hipStreamSynchronize(s));
+  return LPA_OK;
+}
+
+}  // namespace lpa

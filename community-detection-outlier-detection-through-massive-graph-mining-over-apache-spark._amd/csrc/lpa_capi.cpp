@@ -1,0 +1,372 @@
+// C ABI of liblpa_hip.so (include/lpa.h).  Handle lifetime, argument checks,
+// error reporting, RCCL communicator setup.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+
+#include "lpa_internal.h"
+
+namespace lpa {
+
+namespace {
+thread_local char g_err[1024] = "";
+}
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int dev_alloc(lpa_graph* g, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 1;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    (void)hipGetLastError();
+    set_error("hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+    return LPA_ENOMEM;
+  }
+  g->device_bytes += (int64_t)bytes;
+  return LPA_OK;
+}
+
+void dev_free(lpa_graph* g, void* p) {
+  (void)g;
+  if (p) (void)hipFree(p);
+}
+
+int gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t do_scramble, int32_t* d_src,
+             int32_t* d_dst, hipStream_t s);
+int gen_sbm(int32_t V, int32_t blocks, int64_t m, uint32_t p_in_q32, uint64_t seed, int32_t* d_src,
+            int32_t* d_dst, hipStream_t s);
+
+void destroy(lpa_graph* g) {
+  if (!g) return;
+  (void)hipSetDevice(g->device);
+  if (g->stream) (void)hipStreamSynchronize(g->stream);
+  void* bufs[] = {g->rp,   g->col,   g->new_of, g->old_of, g->deg,   g->lab[0], g->lab[1],
+                  g->segs, g->hub_off, g->gtab, g->glist,  g->gcnt, g->e_src,  g->e_dst};
+  for (void* p : bufs) dev_free(g, p);
+  for (auto& e : g->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : g->bin_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (g->comm) (void)ncclCommDestroy(g->comm);
+  if (g->own_stream) (void)hipStreamDestroy(g->own_stream);
+  delete g;
+}
+
+static int check_device(int32_t device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) {
+    (void)hipGetLastError();
+    set_error("no HIP device available (%s)", e != hipSuccess ? hipGetErrorString(e) : "0 devices");
+    return LPA_ENODEV;
+  }
+  if (device < 0 || device >= n) {
+    set_error("device %d out of range [0, %d)", device, n);
+    return LPA_ENODEV;
+  }
+  return LPA_OK;
+}
+
+static int check_edges(const int32_t* src, const int32_t* dst, int64_t m, int32_t V) {
+  if (V < 0 || m < 0) {
+    set_error("V and m must be non-negative (V=%d, m=%lld)", V, (long long)m);
+    return LPA_EINVAL;
+  }
+  if (m > 0 && (!src || !dst)) {
+    set_error("src/dst must be non-null when m > 0");
+    return LPA_EINVAL;
+  }
+  if (m > ((int64_t)1 << 32) - 2) {
+    set_error("m=%lld exceeds the supported edge count", (long long)m);
+    return LPA_EINVAL;
+  }
+  return LPA_OK;
+}
+
+int create_common(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
+                  int64_t m, int32_t V, uint32_t flags, int32_t rank, int32_t nranks,
+                  const uint8_t* comm_id, lpa_graph** out) {
+  if (!out) {
+    set_error("out must be non-null");
+    return LPA_EINVAL;
+  }
+  *out = nullptr;
+  LPA_TRY(check_edges(src, dst, m, V));
+  if (nranks < 1 || rank < 0 || rank >= nranks) {
+    set_error("bad rank %d / nranks %d", rank, nranks);
+    return LPA_EINVAL;
+  }
+  LPA_TRY(check_device(device));
+  LPA_HIP(hipSetDevice(device));
+  lpa_graph* g = new (std::nothrow) lpa_graph();
+  if (!g) {
+    set_error("host allocation failed");
+    return LPA_ENOMEM;
+  }
+  g->device = device;
+  g->rank = rank;
+  g->nranks = nranks;
+  if (stream) {
+    g->stream = stream;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&g->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      set_error("hipStreamCreate: %s", hipGetErrorString(e));
+      delete g;
+      return LPA_EHIP;
+    }
+    g->stream = g->own_stream;
+  }
+  if (nranks > 1 && comm_id) {
+    ncclUniqueId id;
+    memcpy(&id, comm_id, sizeof(id));
+    ncclResult_t r = ncclCommInitRank(&g->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+      set_error("ncclCommInitRank(rank %d of %d): %s", rank, nranks, ncclGetErrorString(r));
+      g->comm = nullptr;
+      destroy(g);
+      return LPA_ERCCL;
+    }
+  }
+  int rc = build_graph(g, src, dst, m, V, flags);
+  if (rc != LPA_OK) {
+    destroy(g);
+    return rc;
+  }
+  *out = g;
+  return LPA_OK;
+}
+
+int create_local(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
+                 int64_t m, int32_t V, uint32_t flags, lpa_graph** out) {
+  return create_common(device, stream, src, dst, m, V, flags, 0, 1, nullptr, out);
+}
+
+}  // namespace lpa
+
+using namespace lpa;
+
+extern "C" {
+
+const char* lpa_last_error(void) { return g_err; }
+
+int lpa_graph_create(const int32_t* src, const int32_t* dst, int64_t m, int32_t V, int32_t device,
+                     uint32_t flags, lpa_graph** out) {
+  return create_common(device, nullptr, src, dst, m, V, flags, 0, 1, nullptr, out);
+}
+
+int lpa_comm_unique_id(uint8_t id_out[128]) {
+  if (!id_out) {
+    set_error("id_out must be non-null");
+    return LPA_EINVAL;
+  }
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    set_error("ncclGetUniqueId: %s", ncclGetErrorString(r));
+    return LPA_ERCCL;
+  }
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  memcpy(id_out, &id, 128);
+  return LPA_OK;
+}
+
+int lpa_graph_create_dist(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                          int32_t device, uint32_t flags, int32_t rank, int32_t nranks,
+                          const uint8_t comm_id[128], lpa_graph** out) {
+  return create_common(device, nullptr, src, dst, m, V, flags, rank, nranks, comm_id, out);
+}
+
+int lpa_exchange_get(lpa_graph* g, int32_t* slice_out) {
+  if (!g || !slice_out) {
+    set_error("null handle or output");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  LPA_HIP(hipMemcpyAsync(slice_out, g->lab[g->cur] + g->own_begin, sizeof(int32_t) * g->slice,
+                         hipMemcpyDeviceToHost, g->stream));
+  LPA_HIP(hipStreamSynchronize(g->stream));
+  return LPA_OK;
+}
+
+int lpa_exchange_put(lpa_graph* g, const int32_t* full_in) {
+  if (!g || !full_in) {
+    set_error("null handle or input");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  LPA_HIP(hipMemcpyAsync(g->lab[g->cur], full_in, sizeof(int32_t) * g->vpad, hipMemcpyHostToDevice,
+                         g->stream));
+  LPA_HIP(hipStreamSynchronize(g->stream));
+  return LPA_OK;
+}
+
+int lpa_set_stream(lpa_graph* g, void* hip_stream) {
+  if (!g) {
+    set_error("null handle");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  LPA_HIP(hipStreamSynchronize(g->stream));
+  g->stream = hip_stream ? (hipStream_t)hip_stream : g->own_stream;
+  if (!g->stream) {
+    LPA_HIP(hipStreamCreateWithFlags(&g->own_stream, hipStreamNonBlocking));
+    g->stream = g->own_stream;
+  }
+  return LPA_OK;
+}
+
+int lpa_reset(lpa_graph* g) {
+  if (!g) {
+    set_error("null handle");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  LPA_TRY(init_labels(g));
+  LPA_HIP(hipStreamSynchronize(g->stream));
+  return LPA_OK;
+}
+
+int lpa_step(lpa_graph* g, int32_t n_supersteps, lpa_stats* stats) {
+  if (!g) {
+    set_error("null handle");
+    return LPA_EINVAL;
+  }
+  if (n_supersteps < 0) {
+    set_error("n_supersteps must be >= 0, got %d", n_supersteps);
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  return run_supersteps(g, n_supersteps, stats);
+}
+
+int lpa_get_labels(lpa_graph* g, int32_t* labels_out, int32_t out_is_device) {
+  if (!g || (!labels_out && g->V > 0)) {
+    set_error("null handle or output");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  if (g->V == 0) return LPA_OK;
+  if (out_is_device) {
+    LPA_TRY(gather_labels(g, labels_out));
+  } else {
+    int32_t* tmp = nullptr;
+    LPA_HIP(hipMallocAsync((void**)&tmp, sizeof(int32_t) * g->V, g->stream));
+    int rc = gather_labels(g, tmp);
+    if (rc == LPA_OK)
+      LPA_HIP(hipMemcpyAsync(labels_out, tmp, sizeof(int32_t) * g->V, hipMemcpyDeviceToHost, g->stream));
+    LPA_HIP(hipFreeAsync(tmp, g->stream));
+    if (rc != LPA_OK) return rc;
+  }
+  LPA_HIP(hipStreamSynchronize(g->stream));
+  return LPA_OK;
+}
+
+int lpa_run(lpa_graph* g, int32_t max_iter, int32_t* labels_out, int32_t out_is_device,
+            lpa_stats* stats) {
+  if (!g) {
+    set_error("null handle");
+    return LPA_EINVAL;
+  }
+  if (max_iter <= 0) {
+    set_error("requirement failed: Maximum of steps must be greater than 0, but got %d", max_iter);
+    return LPA_EINVAL;
+  }
+  LPA_TRY(lpa_reset(g));
+  LPA_TRY(lpa_step(g, max_iter, stats));
+  if (labels_out) LPA_TRY(lpa_get_labels(g, labels_out, out_is_device));
+  return LPA_OK;
+}
+
+int lpa_outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
+                int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
+                uint8_t* flags, lpa_outlier_summary* summary) {
+  if (!g || (!labels && g->V > 0)) {
+    set_error("null handle or labels");
+    return LPA_EINVAL;
+  }
+  if (g->nranks > 1) {
+    set_error("lpa_outlier runs on a single-GPU handle");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  return outlier(g, labels, labels_on_device, mode, sub_iter, size_hist, incident, sub_labels, flags,
+                 summary);
+}
+
+int lpa_degrees(lpa_graph* g, int32_t* deg_out) {
+  if (!g || (!deg_out && g->V > 0)) {
+    set_error("null handle or output");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  if (g->V > 0)
+    LPA_HIP(hipMemcpyAsync(deg_out, g->deg, sizeof(int32_t) * g->V, hipMemcpyDeviceToHost, g->stream));
+  LPA_HIP(hipStreamSynchronize(g->stream));
+  return LPA_OK;
+}
+
+int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
+  if (!g || !info) {
+    set_error("null handle or info");
+    return LPA_EINVAL;
+  }
+  memset(info, 0, sizeof(*info));
+  info->V = g->V;
+  info->m = g->m;
+  info->arcs = g->arcs;
+  info->slice = g->slice;
+  info->own_begin = g->own_begin;
+  info->rank = g->rank;
+  info->nranks = g->nranks;
+  info->device = g->device;
+  info->max_degree = g->max_degree;
+  for (int b = 0; b < LPA_NBINS; ++b) {
+    info->bin_vertices[b] = g->bin_begin[b + 1] - g->bin_begin[b];
+    info->bin_arcs[b] = g->bin_arcs[b];
+  }
+  info->hub_vertices = g->n_hub;
+  info->segments = g->n_segs;
+  info->device_bytes = g->device_bytes;
+  return LPA_OK;
+}
+
+void lpa_graph_destroy(lpa_graph* g) { destroy(g); }
+
+int lpa_gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t scramble, int32_t* d_src,
+                 int32_t* d_dst, int32_t device, void* hip_stream) {
+  LPA_TRY(check_device(device));
+  LPA_HIP(hipSetDevice(device));
+  if (m > 0 && (!d_src || !d_dst)) {
+    set_error("d_src/d_dst must be non-null");
+    return LPA_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)hip_stream;
+  LPA_TRY(gen_rmat(scale, m, seed, scramble, d_src, d_dst, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  return LPA_OK;
+}
+
+int lpa_gen_sbm(int32_t V, int32_t blocks, int64_t m, uint32_t p_in_q32, uint64_t seed,
+                int32_t* d_src, int32_t* d_dst, int32_t device, void* hip_stream) {
+  LPA_TRY(check_device(device));
+  LPA_HIP(hipSetDevice(device));
+  if (m > 0 && (!d_src || !d_dst)) {
+    set_error("d_src/d_dst must be non-null");
+    return LPA_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)hip_stream;
+  LPA_TRY(gen_sbm(V, blocks, m, p_in_q32, seed, d_src, d_dst, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  return LPA_OK;
+}
+
+}  // extern "C"

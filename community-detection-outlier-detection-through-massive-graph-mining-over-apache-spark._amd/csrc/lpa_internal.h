@@ -1,0 +1,141 @@
+// Internal declarations shared by the HIP translation units of liblpa_hip.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/lpa.h"
+
+namespace lpa {
+
+typedef unsigned long long u64;
+typedef uint32_t u32;
+
+// ---------------------------------------------------------------------------
+// Degree bins (SURVEY.md §7 kernel inventory).  Vertices of a rank's slice are
+// sorted by degree (descending), so every bin is one contiguous range.
+// ---------------------------------------------------------------------------
+enum Bin { BIN_SEG = 0, BIN_WAVE = 1, BIN_G16 = 2, BIN_G8 = 3, BIN_G4 = 4, BIN_G2 = 5, BIN_G1 = 6,
+           BIN_ISO = 7 };
+
+constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 16 < deg <= 512
+constexpr int kWaveCap = 1024;        // per-wave LDS table entries (>= 2 * kWaveMaxDeg)
+constexpr int kSegArcs = 2048;        // arcs per block segment (hub path)
+constexpr int kSegCap = 4096;         // per-block LDS table entries (>= 2 * kSegArcs)
+constexpr int kBinEvents = LPA_NBINS + 1;  // event marks per timed superstep
+
+struct Segment {
+  int64_t begin;  // first arc (local CSR index)
+  int32_t len;    // arcs in the segment (<= kSegArcs)
+  int32_t v;      // local vertex index; negative-encoded when the vertex spans >1 segment: -(hub+1)
+};
+
+// thread-local last error
+void set_error(const char* fmt, ...);
+
+#define LPA_HIP(call)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess) {                                                                \
+      ::lpa::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                       __LINE__);                                                          \
+      return LPA_EHIP;                                                                     \
+    }                                                                                      \
+  } while (0)
+
+#define LPA_TRY(call)        \
+  do {                       \
+    int rc_ = (call);        \
+    if (rc_ != LPA_OK) return rc_; \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Device memory held by a handle.
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace lpa
+
+struct lpa_graph {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  int32_t rank = 0, nranks = 1;
+  ncclComm_t comm = nullptr;
+
+  int64_t V = 0, m = 0;
+  int64_t slice = 0;      // vertex slots per rank
+  int64_t vpad = 0;       // nranks * slice
+  int64_t own_begin = 0;  // rank * slice
+  int64_t n_own = 0;      // real (non-padding) vertices owned
+  int64_t arcs = 0;       // local arcs
+  int32_t max_degree = 0;
+
+  // CSR of the owned slice, internal (degree-ranked) numbering
+  int64_t* rp = nullptr;    // [slice + 1]
+  int32_t* col = nullptr;   // [arcs] global internal ids
+  int32_t* new_of = nullptr;  // [V] dense id -> internal slot
+  int32_t* old_of = nullptr;  // [vpad] internal slot -> dense id (-1 padding)
+  int32_t* deg = nullptr;     // [V] symmetrised degree by dense id
+  int32_t* lab[2] = {nullptr, nullptr};  // [vpad] ping-pong label vectors (replicated)
+  int cur = 0;                // index of the current label vector
+
+  // degree bins over the owned slice
+  int64_t bin_begin[LPA_NBINS + 1] = {0};
+  int64_t bin_arcs[LPA_NBINS] = {0};
+
+  // hub path
+  lpa::Segment* segs = nullptr;
+  int64_t n_segs = 0;
+  int64_t n_hub = 0;        // vertices with > kSegArcs arcs (global merge)
+  int64_t* hub_off = nullptr;     // [n_hub + 1] table offsets
+  lpa::u64* gtab = nullptr;       // global hash tables
+  int32_t* glist = nullptr;       // touched-slot lists
+  int32_t* gcnt = nullptr;        // [n_hub] list lengths
+
+  // original edge list kept for the outlier stage (device, dense ids)
+  int32_t* e_src = nullptr;
+  int32_t* e_dst = nullptr;
+
+  int64_t device_bytes = 0;
+  hipEvent_t ev[2 * LPA_STATS_MAX_ITERS + 2] = {};
+  hipEvent_t bin_ev[LPA_STATS_MAX_ITERS * lpa::kBinEvents] = {};
+};
+
+namespace lpa {
+
+// allocation helpers (track bytes on the handle)
+int dev_alloc(lpa_graph* g, void** p, size_t bytes);
+void dev_free(lpa_graph* g, void* p);
+
+// primitives (lpa_prims.hip)
+// LSD radix sort of u64 keys in place (tmp: same length); sorts digits at the
+// given bit shifts (8-bit digits), in order.  Result ends in `keys`.
+int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshifts,
+                   hipStream_t s);
+// exclusive scan of int32 input into int64 output (n + 1 entries: out[n] = total)
+int exclusive_scan_i32_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s);
+int exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
+int bits_for(uint64_t maxval);  // bits needed to represent maxval (0 -> 0)
+
+// build (lpa_build.hip)
+int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                uint32_t flags);
+int init_labels(lpa_graph* g);
+
+// iteration (lpa_iter.hip)
+int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st);
+int gather_labels(lpa_graph* g, int32_t* out_dense_dev);
+
+// outlier (lpa_outlier.hip)
+int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
+            int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
+            uint8_t* flags, lpa_outlier_summary* summary);
+
+}  // namespace lpa

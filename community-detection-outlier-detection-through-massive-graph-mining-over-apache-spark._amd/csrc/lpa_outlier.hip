@@ -1,0 +1,406 @@
+// Outlier stage on the GPU (/root/reference/
+// CommunityDetection/Graphframes.py:92-137).
+//
+// L1  size[l]   = |{v : L[v] = l}|                               (:100-104, :120)
+//     inc[l]    = |{distinct (s,d) : L[s] = l or L[d] = l}|      (:107-118)
+//     threshold rule over the community sizes, flag members of small communities
+// L2  E' = distinct (s,d) with L[s] = L[d]; L' = LPA-DET(E', sub_iter)   (:121-128)
+//     per community: threshold rule over its sub-label sizes     (:130-137)
+//
+// Threshold rule (App. B a13): groups sorted by (size desc, label asc),
+// k = n // 10, thr = sorted[-k].size if k > 0 else sorted[0].size, i.e. the
+// k-th smallest size (k > 0) or the largest; a group is an outlier iff size < thr.
+// Per segment (community) it is computed by one radix sort of (segment << 32 | size)
+// keys, after which the k-th smallest sits at segment_start + k - 1.
+//
+// A sub-label L'[v] is the id of a vertex of v's own community (E' never
+// crosses communities), so the group (L[v], L'[v]) is identified by L'[v] alone
+// and its community is L[L'[v]].
+#include "lpa_internal.h"
+
+namespace lpa {
+
+int create_local(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
+                 int64_t m, int32_t V, uint32_t flags, lpa_graph** out);
+void destroy(lpa_graph* g);
+
+namespace {
+
+inline unsigned grid_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 65536) b = 65536;
+  return (unsigned)b;
+}
+
+#define GRID_STRIDE(i, n) \
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+__global__ void k_edge_keys(const int32_t* __restrict__ s, const int32_t* __restrict__ d, int64_t m,
+                            u64* __restrict__ k) {
+  GRID_STRIDE(e, m) k[e] = ((u64)(u32)s[e] << 32) | (u32)d[e];
+}
+
+// compact the distinct keys of a sorted array (first occurrence kept)
+__global__ void k_mark_first(const u64* __restrict__ k, int64_t n, int32_t* __restrict__ mark) {
+  GRID_STRIDE(i, n) mark[i] = (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
+}
+
+__global__ void k_scatter_marked(const u64* __restrict__ k, const int32_t* __restrict__ mark,
+                                 const int64_t* __restrict__ pos, int64_t n, u64* __restrict__ out) {
+  GRID_STRIDE(i, n) if (mark[i]) out[pos[i]] = k[i];
+}
+
+__global__ void k_histogram(const int32_t* __restrict__ lab, int64_t V, int32_t* __restrict__ hist) {
+  GRID_STRIDE(v, V) atomicAdd(&hist[lab[v]], 1);
+}
+
+__global__ void k_incident(const u64* __restrict__ ek, int64_t n, const int32_t* __restrict__ L,
+                           int32_t* __restrict__ inc) {
+  GRID_STRIDE(i, n) {
+    const int32_t ls = L[(int32_t)(ek[i] >> 32)], ld = L[(int32_t)(u32)ek[i]];
+    atomicAdd(&inc[ls], 1);
+    if (ld != ls) atomicAdd(&inc[ld], 1);
+  }
+}
+
+// E' edges: distinct keys whose endpoints share a label
+__global__ void k_mark_intra(const u64* __restrict__ ek, int64_t n, const int32_t* __restrict__ L,
+                             int32_t* __restrict__ mark) {
+  GRID_STRIDE(i, n) mark[i] = L[(int32_t)(ek[i] >> 32)] == L[(int32_t)(u32)ek[i]] ? 1 : 0;
+}
+
+__global__ void k_split_marked(const u64* __restrict__ ek, const int32_t* __restrict__ mark,
+                               const int64_t* __restrict__ pos, int64_t n, int32_t* __restrict__ s,
+                               int32_t* __restrict__ d) {
+  GRID_STRIDE(i, n) if (mark[i]) {
+    s[pos[i]] = (int32_t)(ek[i] >> 32);
+    d[pos[i]] = (int32_t)(u32)ek[i];
+  }
+}
+
+// group keys (segment << 32 | size) for every label l with size[l] > 0
+__global__ void k_group_flags(const int32_t* __restrict__ size, int64_t V, int32_t* __restrict__ mark) {
+  GRID_STRIDE(l, V) mark[l] = size[l] > 0 ? 1 : 0;
+}
+
+__global__ void k_group_keys(const int32_t* __restrict__ size, const int32_t* __restrict__ seg_of,
+                             const int32_t* __restrict__ mark, const int64_t* __restrict__ pos,
+                             int64_t V, u64* __restrict__ keys) {
+  GRID_STRIDE(l, V) if (mark[l]) {
+    const u32 sg = seg_of ? (u32)seg_of[l] : 0u;
+    keys[pos[l]] = ((u64)sg << 32) | (u32)size[l];
+  }
+}
+
+// per segment: first / last index in the sorted group keys
+__global__ void k_seg_bounds(const u64* __restrict__ keys, int64_t n, int32_t* __restrict__ first,
+                             int32_t* __restrict__ last) {
+  GRID_STRIDE(i, n) {
+    const u32 sg = (u32)(keys[i] >> 32);
+    if (i == 0 || (u32)(keys[i - 1] >> 32) != sg) first[sg] = (int32_t)i;
+    if (i == n - 1 || (u32)(keys[i + 1] >> 32) != sg) last[sg] = (int32_t)i;
+  }
+}
+
+// threshold per segment present in the keys
+__global__ void k_seg_threshold(const u64* __restrict__ keys, int64_t n, const int32_t* __restrict__ first,
+                                const int32_t* __restrict__ last, int32_t* __restrict__ thr,
+                                int32_t* __restrict__ ngroups) {
+  GRID_STRIDE(i, n) {
+    const u32 sg = (u32)(keys[i] >> 32);
+    if (first[sg] != (int32_t)i) continue;
+    const int64_t cnt = (int64_t)last[sg] - first[sg] + 1;
+    const int64_t k = cnt / 10;
+    const int64_t at = k > 0 ? first[sg] + k - 1 : last[sg];
+    thr[sg] = (int32_t)(u32)keys[at];
+    ngroups[sg] = (int32_t)cnt;
+  }
+}
+
+// flags[v] = size(group of v) < thr(segment of v); counts
+__global__ void k_flag(const int32_t* __restrict__ group_of, const int32_t* __restrict__ size,
+                       const int32_t* __restrict__ seg_of_v, const int32_t* __restrict__ thr,
+                       int64_t V, uint8_t* __restrict__ flags, int32_t* __restrict__ seg_flagged,
+                       unsigned long long* __restrict__ nflag) {
+  GRID_STRIDE(v, V) {
+    const int32_t gph = group_of[v];
+    const u32 sg = seg_of_v ? (u32)seg_of_v[v] : 0u;
+    const uint8_t f = size[gph] < thr[sg] ? 1 : 0;
+    flags[v] = f;
+    if (f) {
+      atomicAdd(nflag, 1ull);
+      seg_flagged[sg] = 1;
+    }
+  }
+}
+
+__global__ void k_count_nonzero(const int32_t* __restrict__ a, int64_t n, unsigned long long* out) {
+  unsigned long long c = 0;
+  GRID_STRIDE(i, n) c += a[i] != 0;
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+__global__ void k_check_range(const int32_t* __restrict__ a, int64_t n, unsigned long long* bad) {
+  GRID_STRIDE(i, n) if ((u32)a[i] >= (u32)n) atomicAdd(bad, 1ull);
+}
+
+__global__ void k_widen(const int32_t* __restrict__ a, int64_t n, int64_t* __restrict__ out) {
+  GRID_STRIDE(i, n) out[i] = a[i];
+}
+
+struct Scratch {
+  hipStream_t s;
+  void* ptrs[32];
+  int n = 0;
+  explicit Scratch(hipStream_t st) : s(st) {}
+  template <typename T>
+  int get(T** p, int64_t count) {
+    if (count < 1) count = 1;
+    if (hipMallocAsync((void**)p, sizeof(T) * count, s) != hipSuccess) {
+      set_error("outlier: out of device memory (%lld x %zu B)", (long long)count, sizeof(T));
+      return LPA_ENOMEM;
+    }
+    ptrs[n++] = *p;
+    return LPA_OK;
+  }
+  ~Scratch() {
+    for (int i = 0; i < n; ++i) (void)hipFreeAsync(ptrs[i], s);
+  }
+};
+
+// stable compaction helper: mark -> positions (exclusive scan) -> count
+int compact_positions(const int32_t* mark, int64_t n, int64_t* pos, int64_t* total, hipStream_t s) {
+  LPA_TRY(exclusive_scan_i32_i64(mark, pos, n, s));
+  LPA_HIP(hipMemcpyAsync(total, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  return LPA_OK;
+}
+
+int sort_keys(u64* keys, u64* tmp, int64_t n, int bits_lo, int bits_hi, hipStream_t s) {
+  int shifts[16], ns = 0;
+  for (int b = 0; b < bits_lo; b += 8) shifts[ns++] = b;
+  for (int b = 0; b < bits_hi; b += 8) shifts[ns++] = 32 + b;
+  return radix_sort_u64(keys, tmp, n, shifts, ns, s);
+}
+
+// distinct directed edges of the handle as sorted (s << 32 | d) keys
+int distinct_edges(lpa_graph* g, Scratch& sc, u64** out, int64_t* nd) {
+  hipStream_t s = g->stream;
+  const int64_t m = g->m;
+  u64* k = nullptr;
+  int32_t* mark = nullptr;
+  int64_t* pos = nullptr;
+  u64* dk = nullptr;
+  LPA_TRY(sc.get(&k, 2 * m));
+  LPA_TRY(sc.get(&mark, m));
+  LPA_TRY(sc.get(&pos, m + 1));
+  if (m > 0) {
+    hipLaunchKernelGGL(k_edge_keys, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, k);
+    LPA_HIP(hipGetLastError());
+    const int b = bits_for((uint64_t)(g->V > 0 ? g->V - 1 : 0));
+    LPA_TRY(sort_keys(k, k + m, m, b, b, s));
+    hipLaunchKernelGGL(k_mark_first, dim3(grid_for(m)), dim3(256), 0, s, k, m, mark);
+    LPA_HIP(hipGetLastError());
+  }
+  LPA_TRY(compact_positions(mark, m, pos, nd, s));
+  LPA_TRY(sc.get(&dk, *nd));
+  if (m > 0) {
+    hipLaunchKernelGGL(k_scatter_marked, dim3(grid_for(m)), dim3(256), 0, s, k, mark, pos, m, dk);
+    LPA_HIP(hipGetLastError());
+  }
+  *out = dk;
+  return LPA_OK;
+}
+
+// groups = labels l with size[l] > 0, segment seg_of[l] (nullptr: one segment).
+// Returns per-segment thresholds (thr[V]) and group counts (ngroups[V]).
+int segmented_threshold(lpa_graph* g, Scratch& sc, const int32_t* size, const int32_t* seg_of,
+                        int64_t V, int32_t* thr, int32_t* ngroups, int64_t* n_groups_total) {
+  hipStream_t s = g->stream;
+  int32_t* mark = nullptr;
+  int64_t* pos = nullptr;
+  LPA_TRY(sc.get(&mark, V));
+  LPA_TRY(sc.get(&pos, V + 1));
+  hipLaunchKernelGGL(k_group_flags, dim3(grid_for(V)), dim3(256), 0, s, size, V, mark);
+  LPA_HIP(hipGetLastError());
+  int64_t ng = 0;
+  LPA_TRY(compact_positions(mark, V, pos, &ng, s));
+  *n_groups_total = ng;
+  if (ng == 0) return LPA_OK;
+  u64* keys = nullptr;
+  int32_t *first = nullptr, *last = nullptr;
+  LPA_TRY(sc.get(&keys, 2 * ng));
+  LPA_TRY(sc.get(&first, V));
+  LPA_TRY(sc.get(&last, V));
+  hipLaunchKernelGGL(k_group_keys, dim3(grid_for(V)), dim3(256), 0, s, size, seg_of, mark, pos, V,
+                     keys);
+  LPA_HIP(hipGetLastError());
+  const int b = bits_for((uint64_t)(V > 0 ? V : 0));
+  LPA_TRY(sort_keys(keys, keys + ng, ng, b, seg_of ? b : 0, s));
+  hipLaunchKernelGGL(k_seg_bounds, dim3(grid_for(ng)), dim3(256), 0, s, keys, ng, first, last);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_seg_threshold, dim3(grid_for(ng)), dim3(256), 0, s, keys, ng, first, last,
+                     thr, ngroups);
+  LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
+
+}  // namespace
+
+int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
+            int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
+            uint8_t* flags, lpa_outlier_summary* summary) {
+  if (mode != 1 && mode != 2) {
+    set_error("outlier mode must be 1 (L1) or 2 (L2), got %d", mode);
+    return LPA_EINVAL;
+  }
+  if (mode == 2 && sub_iter <= 0) {
+    set_error("requirement failed: Maximum of steps must be greater than 0, but got %d", sub_iter);
+    return LPA_EINVAL;
+  }
+  hipStream_t s = g->stream;
+  const int64_t V = g->V;
+  Scratch sc(s);
+  lpa_outlier_summary sum = {};
+  int32_t *L = nullptr, *size = nullptr, *inc = nullptr, *thr = nullptr, *ngr = nullptr,
+          *segflag = nullptr;
+  uint8_t* fl = nullptr;
+  int64_t* wide = nullptr;
+  unsigned long long* cnt = nullptr;
+  LPA_TRY(sc.get(&L, V));
+  LPA_TRY(sc.get(&size, V));
+  LPA_TRY(sc.get(&inc, V));
+  LPA_TRY(sc.get(&thr, V));
+  LPA_TRY(sc.get(&ngr, V));
+  LPA_TRY(sc.get(&segflag, V));
+  LPA_TRY(sc.get(&fl, V));
+  LPA_TRY(sc.get(&wide, V));
+  LPA_TRY(sc.get(&cnt, 4));
+  if (V == 0) {
+    if (summary) *summary = sum;
+    return LPA_OK;
+  }
+  LPA_HIP(hipMemcpyAsync(L, labels, sizeof(int32_t) * V,
+                         labels_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  LPA_HIP(hipMemsetAsync(size, 0, sizeof(int32_t) * V, s));
+  LPA_HIP(hipMemsetAsync(inc, 0, sizeof(int32_t) * V, s));
+  LPA_HIP(hipMemsetAsync(segflag, 0, sizeof(int32_t) * V, s));
+  LPA_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 4, s));
+
+  // labels must be dense ids: a label outside [0, V) would index out of bounds
+  hipLaunchKernelGGL(k_check_range, dim3(grid_for(V)), dim3(256), 0, s, L, V, cnt + 3);
+  LPA_HIP(hipGetLastError());
+  {
+    unsigned long long bad = 0;
+    LPA_HIP(hipMemcpyAsync(&bad, cnt + 3, sizeof(bad), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    if (bad) {
+      set_error("outlier: %llu labels outside [0, V=%lld)", bad, (long long)V);
+      return LPA_EINVAL;
+    }
+  }
+  hipLaunchKernelGGL(k_histogram, dim3(grid_for(V)), dim3(256), 0, s, L, V, size);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(V)), dim3(256), 0, s, size, V, cnt);
+  LPA_HIP(hipGetLastError());
+
+  u64* ek = nullptr;
+  int64_t nd = 0;
+  LPA_TRY(distinct_edges(g, sc, &ek, &nd));
+  sum.distinct_edges = nd;
+  if (nd > 0) {
+    hipLaunchKernelGGL(k_incident, dim3(grid_for(nd)), dim3(256), 0, s, ek, nd, L, inc);
+    LPA_HIP(hipGetLastError());
+  }
+
+  if (mode == 1) {
+    int64_t ng = 0;
+    LPA_TRY(segmented_threshold(g, sc, size, nullptr, V, thr, ngr, &ng));
+    hipLaunchKernelGGL(k_flag, dim3(grid_for(V)), dim3(256), 0, s, L, size, (const int32_t*)nullptr,
+                       thr, V, fl, segflag, cnt + 1);
+    LPA_HIP(hipGetLastError());
+    int32_t h_thr = 0;
+    LPA_HIP(hipMemcpyAsync(&h_thr, thr, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    unsigned long long h_cnt[4];
+    LPA_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    sum.n_groups = ng;
+    sum.k = ng / 10;
+    sum.threshold = h_thr;
+    sum.n_flagged = (int64_t)h_cnt[1];
+    sum.n_communities = (int64_t)h_cnt[0];
+    sum.n_communities_flagged = sum.n_flagged > 0 ? 1 : 0;
+  } else {
+    // E' = distinct intra-community edges
+    int32_t* mark = nullptr;
+    int64_t* pos = nullptr;
+    int32_t *s2 = nullptr, *d2 = nullptr, *sub = nullptr, *subsize = nullptr;
+    LPA_TRY(sc.get(&mark, nd));
+    LPA_TRY(sc.get(&pos, nd + 1));
+    if (nd > 0) {
+      hipLaunchKernelGGL(k_mark_intra, dim3(grid_for(nd)), dim3(256), 0, s, ek, nd, L, mark);
+      LPA_HIP(hipGetLastError());
+    }
+    int64_t m2 = 0;
+    LPA_TRY(compact_positions(mark, nd, pos, &m2, s));
+    LPA_TRY(sc.get(&s2, m2));
+    LPA_TRY(sc.get(&d2, m2));
+    LPA_TRY(sc.get(&sub, V));
+    LPA_TRY(sc.get(&subsize, V));
+    if (nd > 0) {
+      hipLaunchKernelGGL(k_split_marked, dim3(grid_for(nd)), dim3(256), 0, s, ek, mark, pos, nd, s2, d2);
+      LPA_HIP(hipGetLastError());
+    }
+    LPA_HIP(hipStreamSynchronize(s));
+    // second LPA on the induced simple subgraph (same device, same stream)
+    lpa_graph* h = nullptr;
+    LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE, &h));
+    int rc = run_supersteps(h, sub_iter, nullptr);
+    if (rc == LPA_OK) rc = gather_labels(h, sub);
+    if (rc == LPA_OK && hipStreamSynchronize(s) != hipSuccess) rc = LPA_EHIP;
+    destroy(h);
+    if (rc != LPA_OK) return rc;
+    LPA_HIP(hipMemsetAsync(subsize, 0, sizeof(int32_t) * V, s));
+    hipLaunchKernelGGL(k_histogram, dim3(grid_for(V)), dim3(256), 0, s, sub, V, subsize);
+    LPA_HIP(hipGetLastError());
+    // segment of a sub-label group = the community of the sub-label vertex: L itself
+    int64_t ng = 0;
+    LPA_TRY(segmented_threshold(g, sc, subsize, L, V, thr, ngr, &ng));
+    hipLaunchKernelGGL(k_flag, dim3(grid_for(V)), dim3(256), 0, s, sub, subsize, L, thr, V, fl,
+                       segflag, cnt + 1);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(V)), dim3(256), 0, s, segflag, V, cnt + 2);
+    LPA_HIP(hipGetLastError());
+    unsigned long long h_cnt[4];
+    LPA_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
+    if (sub_labels) LPA_HIP(hipMemcpyAsync(sub_labels, sub, sizeof(int32_t) * V, hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    sum.n_groups = ng;
+    sum.k = -1;
+    sum.threshold = -1;
+    sum.n_flagged = (int64_t)h_cnt[1];
+    sum.n_communities = (int64_t)h_cnt[0];
+    sum.n_communities_flagged = (int64_t)h_cnt[2];
+  }
+
+  if (size_hist) {
+    hipLaunchKernelGGL(k_widen, dim3(grid_for(V)), dim3(256), 0, s, size, V, wide);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipMemcpyAsync(size_hist, wide, sizeof(int64_t) * V, hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+  }
+  if (incident) {
+    hipLaunchKernelGGL(k_widen, dim3(grid_for(V)), dim3(256), 0, s, inc, V, wide);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipMemcpyAsync(incident, wide, sizeof(int64_t) * V, hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+  }
+  if (flags) LPA_HIP(hipMemcpyAsync(flags, fl, V, hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  if (summary) *summary = sum;
+  return LPA_OK;
+}
+
+}  // namespace lpa

@@ -1,0 +1,244 @@
+// Device-wide primitives for graph construction: LSD radix sort of 64-bit
+// keys and exclusive scans.  Build-time only (not on the per-superstep path);
+// written for wave64 (ballot-based digit ranking, 64-bit lane masks).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "lpa_internal.h"
+
+namespace lpa {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kItems = 16;
+constexpr int kTile = kThreads * kItems;  // keys per block per radix pass
+
+// ---------------------------------------------------------------------------
+// block-level helpers (256 threads = 4 waves)
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    T o = __shfl_up(v, off, 64);
+    if (lane >= off) v += o;
+  }
+  return v;
+}
+
+// exclusive scan over the block; returns the thread's exclusive prefix and the block total
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* total) {
+  __shared__ T wsum[kThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  T incl = wave_incl_scan(v, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  T before = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kThreads / 64; ++i) {
+    if (i < w) before += wsum[i];
+    tot += wsum[i];
+  }
+  __syncthreads();
+  *total = tot;
+  return before + incl - v;
+}
+
+// ---------------------------------------------------------------------------
+// exclusive scan: reduce -> (recursive scan of partials) -> apply
+// ---------------------------------------------------------------------------
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(kThreads) void k_scan_reduce(const Tin* __restrict__ in, int64_t n,
+                                                          Tout* __restrict__ part) {
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  Tout s = 0;
+#pragma unroll
+  for (int i = 0; i < kItems; ++i) {
+    int64_t idx = base + (int64_t)i * kThreads + threadIdx.x;
+    if (idx < n) s += (Tout)in[idx];
+  }
+  Tout tot;
+  block_excl_scan<Tout>(s, &tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(kThreads) void k_scan_apply(const Tin* __restrict__ in, int64_t n,
+                                                         Tout* __restrict__ out,
+                                                         const Tout* __restrict__ part_excl) {
+  const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+  Tout v[kItems];
+  Tout loc = 0;
+#pragma unroll
+  for (int j = 0; j < kItems; ++j) {
+    int64_t idx = base + j;
+    v[j] = idx < n ? (Tout)in[idx] : (Tout)0;
+    loc += v[j];
+  }
+  Tout tot;
+  Tout run = block_excl_scan<Tout>(loc, &tot) + (part_excl ? part_excl[blockIdx.x] : (Tout)0);
+#pragma unroll
+  for (int j = 0; j < kItems; ++j) {
+    int64_t idx = base + j;
+    if (idx < n) out[idx] = run;
+    run += v[j];
+    if (idx == n - 1) out[n] = run;  // grand total
+  }
+}
+
+template <typename Tin, typename Tout>
+int scan_impl(const Tin* in, Tout* out, int64_t n, hipStream_t s) {
+  if (n <= 0) {
+    LPA_HIP(hipMemsetAsync(out, 0, sizeof(Tout), s));
+    return LPA_OK;
+  }
+  const int64_t nblk = (n + kTile - 1) / kTile;
+  if (nblk == 1) {
+    hipLaunchKernelGGL((k_scan_apply<Tin, Tout>), dim3(1), dim3(kThreads), 0, s, in, n, out,
+                       (const Tout*)nullptr);
+    LPA_HIP(hipGetLastError());
+    return LPA_OK;
+  }
+  Tout* part = nullptr;
+  Tout* partx = nullptr;
+  LPA_HIP(hipMallocAsync((void**)&part, sizeof(Tout) * nblk, s));
+  LPA_HIP(hipMallocAsync((void**)&partx, sizeof(Tout) * (nblk + 1), s));
+  hipLaunchKernelGGL((k_scan_reduce<Tin, Tout>), dim3((unsigned)nblk), dim3(kThreads), 0, s, in,
+                     n, part);
+  LPA_HIP(hipGetLastError());
+  int rc = scan_impl<Tout, Tout>(part, partx, nblk, s);
+  if (rc == LPA_OK) {
+    hipLaunchKernelGGL((k_scan_apply<Tin, Tout>), dim3((unsigned)nblk), dim3(kThreads), 0, s, in,
+                       n, out, (const Tout*)partx);
+    LPA_HIP(hipGetLastError());
+  }
+  LPA_HIP(hipFreeAsync(part, s));
+  LPA_HIP(hipFreeAsync(partx, s));
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// LSD radix sort, 8-bit digits, stable.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_rs_hist(const u64* __restrict__ keys, int64_t n,
+                                                      int shift, u32* __restrict__ hist,
+                                                      int64_t nblk) {
+  __shared__ u32 cnt[256];
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int lane = threadIdx.x & 63;
+#pragma unroll 4
+  for (int i = 0; i < kItems; ++i) {
+    int64_t idx = base + (int64_t)i * kThreads + threadIdx.x;
+    bool ok = idx < n;
+    u32 dg = ok ? (u32)((keys[idx] >> shift) & 255u) : 0u;
+    // wave-aggregate lanes with equal digits: one LDS atomic per distinct digit
+    u64 peers = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      bool bit = (dg >> b) & 1u;
+      u64 bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    if (ok && (peers & ((1ull << lane) - 1ull)) == 0) atomicAdd(&cnt[dg], (u32)__popcll(peers));
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * nblk + blockIdx.x] = cnt[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kThreads) void k_rs_scatter(const u64* __restrict__ in,
+                                                         u64* __restrict__ out, int64_t n,
+                                                         int shift, const u32* __restrict__ offs,
+                                                         int64_t nblk) {
+  __shared__ u32 run[256];
+  __shared__ u32 wcnt[kThreads / 64][256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  run[tid] = offs[(int64_t)tid * nblk + blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < kThreads / 64; ++i) wcnt[i][tid] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const u64 lt = (1ull << lane) - 1ull;
+  for (int i = 0; i < kItems; ++i) {
+    const int64_t idx = base + (int64_t)i * kThreads + tid;
+    const bool ok = idx < n;
+    const u64 k = ok ? in[idx] : 0ull;
+    const u32 dg = (u32)((k >> shift) & 255u);
+    u64 peers = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      bool bit = (dg >> b) & 1u;
+      u64 bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const u32 rank = (u32)__popcll(peers & lt);
+    if (ok && rank == 0) wcnt[w][dg] = (u32)__popcll(peers);
+    __syncthreads();
+    if (ok) {
+      u32 off = run[dg] + rank;
+      for (int ww = 0; ww < w; ++ww) off += wcnt[ww][dg];
+      out[off] = k;
+    }
+    __syncthreads();
+    u32 tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < kThreads / 64; ++ww) {
+      tot += wcnt[ww][tid];
+      wcnt[ww][tid] = 0;
+    }
+    run[tid] += tot;
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+int bits_for(uint64_t maxval) { return maxval == 0 ? 0 : 64 - __builtin_clzll(maxval); }
+
+int exclusive_scan_i32_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s) {
+  return scan_impl<int32_t, int64_t>(in, out, n, s);
+}
+
+int exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s) {
+  return scan_impl<int64_t, int64_t>(in, out, n, s);
+}
+
+int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshifts,
+                   hipStream_t s) {
+  if (n <= 1 || nshifts == 0) return LPA_OK;
+  if (n >= (int64_t)UINT32_MAX) {
+    set_error("radix_sort_u64: %lld keys exceed the 32-bit offset range", (long long)n);
+    return LPA_EINVAL;
+  }
+  const int64_t nblk = (n + kTile - 1) / kTile;
+  const int64_t nh = 256 * nblk;
+  u32* hist = nullptr;
+  u32* offs = nullptr;
+  LPA_HIP(hipMallocAsync((void**)&hist, sizeof(u32) * nh, s));
+  LPA_HIP(hipMallocAsync((void**)&offs, sizeof(u32) * (nh + 1), s));
+  u64* a = keys;
+  u64* b = tmp;
+  int rc = LPA_OK;
+  for (int p = 0; p < nshifts && rc == LPA_OK; ++p) {
+    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nblk), dim3(kThreads), 0, s, a, n, shifts[p],
+                       hist, nblk);
+    LPA_HIP(hipGetLastError());
+    rc = scan_impl<u32, u32>(hist, offs, nh, s);
+    if (rc != LPA_OK) break;
+    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nblk), dim3(kThreads), 0, s, a, b, n,
+                       shifts[p], offs, nblk);
+    LPA_HIP(hipGetLastError());
+    u64* t = a;
+    a = b;
+    b = t;
+  }
+  if (rc == LPA_OK && a != keys) LPA_HIP(hipMemcpyAsync(keys, a, sizeof(u64) * n, hipMemcpyDeviceToDevice, s));
+  LPA_HIP(hipFreeAsync(hist, s));
+  LPA_HIP(hipFreeAsync(offs, s));
+  return rc;
+}
+
+}  // namespace lpa

@@ -1,0 +1,204 @@
+"""Low-level handle over liblpa_hip.so: one built graph on one GPU (or one rank's slice).
+
+Inputs are dense int32 edge arrays: host numpy arrays, or device tensors (any
+object with ``data_ptr()`` and ``is_cuda``, e.g. torch-ROCm tensors), which are
+handed to the C ABI as plain device pointers (torch is only the allocator).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+OUTLIER_MODES = {"L1": 1, "L2": 2, 1: 1, 2: 2}
+
+
+def _is_device_tensor(x) -> bool:
+    return hasattr(x, "data_ptr") and getattr(x, "is_cuda", False)
+
+
+def _edge_ptrs(src, dst):
+    """Returns (src_ptr, dst_ptr, m, flags, keepalive)."""
+    if _is_device_tensor(src) != _is_device_tensor(dst):
+        raise ValueError("src and dst must both be host arrays or both device tensors")
+    if _is_device_tensor(src):
+        import torch
+
+        if src.dtype != torch.int32 or dst.dtype != torch.int32:
+            raise ValueError("device edge tensors must be int32")
+        if src.numel() != dst.numel():
+            raise ValueError("src/dst length mismatch")
+        src = src.contiguous()
+        dst = dst.contiguous()
+        torch.cuda.current_stream(src.device).synchronize()
+        return src.data_ptr(), dst.data_ptr(), int(src.numel()), _lib.LPA_INPUT_DEVICE, (src, dst)
+    s = np.ascontiguousarray(src, dtype=np.int32)
+    d = np.ascontiguousarray(dst, dtype=np.int32)
+    if s.shape != d.shape or s.ndim != 1:
+        raise ValueError("src/dst must be 1-D arrays of equal length")
+    return s.ctypes.data, d.ctypes.data, int(s.size), 0, (s, d)
+
+
+class Graph:
+    """A symmetrised, degree-sorted CSR resident in HBM plus its label vectors.
+
+    ``Graph(src, dst, V)`` builds on ``device``; ``Graph(..., rank=r, nranks=P,
+    comm_id=id)`` builds rank r's slice for a P-GPU run (one process per GPU,
+    RCCL allgather per superstep); ``comm_id=None`` with ``nranks > 1`` selects the
+    caller-driven exchange (``exchange_get`` / ``exchange_put``).
+    """
+
+    def __init__(self, src, dst, num_vertices: int, device: int = 0, rank: int = 0,
+                 nranks: int = 1, comm_id: bytes | None = None):
+        lib = _lib.load()
+        self._lib = lib
+        self._h = ctypes.c_void_p()
+        sp, dp, m, flags, keep = _edge_ptrs(src, dst)
+        V = int(num_vertices)
+        if V < 0 or V > np.iinfo(np.int32).max:
+            raise ValueError(f"num_vertices out of range: {V}")
+        if nranks == 1:
+            rc = lib.lpa_graph_create(sp, dp, m, V, device, flags, ctypes.byref(self._h))
+        else:
+            cid = None if comm_id is None else bytes(comm_id)
+            if cid is not None and len(cid) != 128:
+                raise ValueError("comm_id must be 128 bytes")
+            rc = lib.lpa_graph_create_dist(sp, dp, m, V, device, flags, rank, nranks, cid,
+                                           ctypes.byref(self._h))
+        del keep
+        _lib.check(rc)
+        self.num_vertices = V
+        self.num_edges = m
+        self.device = device
+        self.rank = rank
+        self.nranks = nranks
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self):
+        if self._h:
+            self._lib.lpa_graph_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _handle(self):
+        if not self._h:
+            raise ValueError("graph handle is closed")
+        return self._h
+
+    # -- LPA ----------------------------------------------------------------
+    def info(self) -> dict:
+        info = _lib.LpaGraphInfo()
+        _lib.check(self._lib.lpa_graph_get_info(self._handle(), ctypes.byref(info)))
+        return info.to_dict()
+
+    def reset(self):
+        _lib.check(self._lib.lpa_reset(self._handle()))
+
+    def step(self, n: int = 1, stats: bool = False):
+        st = _lib.LpaStats() if stats else None
+        _lib.check(self._lib.lpa_step(self._handle(), int(n), ctypes.byref(st) if stats else None))
+        return st.to_dict() if stats else None
+
+    def labels(self, out=None) -> np.ndarray:
+        """Current labels by dense vertex id (host int32), or into a device tensor `out`."""
+        if out is not None and _is_device_tensor(out):
+            _lib.check(self._lib.lpa_get_labels(self._handle(), out.data_ptr(), 1))
+            return out
+        lab = np.empty(self.num_vertices, dtype=np.int32)
+        _lib.check(self._lib.lpa_get_labels(self._handle(), lab.ctypes.data, 0))
+        return lab
+
+    def run(self, max_iter: int, stats: bool = False):
+        """labelPropagation(maxIter): reset, exactly max_iter supersteps, labels."""
+        lab = np.empty(self.num_vertices, dtype=np.int32)
+        st = _lib.LpaStats() if stats else None
+        _lib.check(self._lib.lpa_run(self._handle(), int(max_iter), lab.ctypes.data, 0,
+                                     ctypes.byref(st) if stats else None))
+        return (lab, st.to_dict()) if stats else lab
+
+    def degrees(self) -> np.ndarray:
+        deg = np.empty(self.num_vertices, dtype=np.int32)
+        _lib.check(self._lib.lpa_degrees(self._handle(), deg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return deg
+
+    # -- caller-driven exchange (virtual ranks) -------------------------------
+    def exchange_get(self) -> np.ndarray:
+        sl = np.empty(self.info()["slice"], dtype=np.int32)
+        _lib.check(self._lib.lpa_exchange_get(self._handle(), sl.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return sl
+
+    def exchange_put(self, full: np.ndarray):
+        full = np.ascontiguousarray(full, dtype=np.int32)
+        _lib.check(self._lib.lpa_exchange_put(self._handle(), full.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+
+    # -- outlier stage --------------------------------------------------------
+    def outlier(self, labels, mode="L1", sub_iter: int = 5):
+        """Appendix B outlier stage.  Returns dict(size, incident, sub_labels, flags, summary)."""
+        if mode not in OUTLIER_MODES:
+            raise ValueError(f"mode must be 'L1' or 'L2', got {mode!r}")
+        md = OUTLIER_MODES[mode]
+        V = self.num_vertices
+        lab = np.ascontiguousarray(labels, dtype=np.int32)
+        if lab.shape != (V,):
+            raise ValueError(f"labels must have shape ({V},)")
+        size = np.empty(V, dtype=np.int64)
+        inc = np.empty(V, dtype=np.int64)
+        sub = np.empty(V, dtype=np.int32) if md == 2 else None
+        flags = np.empty(V, dtype=np.uint8)
+        summ = _lib.LpaOutlierSummary()
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        _lib.check(self._lib.lpa_outlier(
+            self._handle(), lab.ctypes.data, 0, md, int(sub_iter),
+            size.ctypes.data_as(i64p), inc.ctypes.data_as(i64p),
+            sub.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)) if sub is not None else None,
+            flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(summ)))
+        return dict(size=size, incident=inc, sub_labels=sub, flags=flags.astype(bool),
+                    summary=summ.to_dict())
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id for a distributed build (create on one rank, broadcast)."""
+    buf = ctypes.create_string_buffer(128)
+    _lib.check(_lib.load().lpa_comm_unique_id(buf))
+    return buf.raw
+
+
+def gen_rmat(scale: int, edgefactor: int = 16, seed: int = 1, scramble: bool = True, device: int = 0):
+    """R-MAT edge list generated in HBM (torch int32 tensors on `device`)."""
+    import torch
+
+    m = edgefactor << scale
+    dev = torch.device("cuda", device)
+    src = torch.empty(m, dtype=torch.int32, device=dev)
+    dst = torch.empty(m, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    _lib.check(_lib.load().lpa_gen_rmat(scale, m, seed, int(scramble), src.data_ptr(), dst.data_ptr(),
+                                        device, None))
+    return src, dst
+
+
+def gen_sbm(num_vertices: int, blocks: int, m: int, seed: int = 20261015,
+            p_in_q32: int = 3865470566, device: int = 0):
+    """Planted-partition SBM edge list generated in HBM (p_in = p_in_q32 / 2^32)."""
+    import torch
+
+    dev = torch.device("cuda", device)
+    src = torch.empty(m, dtype=torch.int32, device=dev)
+    dst = torch.empty(m, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    _lib.check(_lib.load().lpa_gen_sbm(num_vertices, blocks, m, p_in_q32, seed, src.data_ptr(),
+                                       dst.data_ptr(), device, None))
+    return src, dst

@@ -1,0 +1,177 @@
+/*
+ * lpa.h -- C ABI of the MI355X-native label-propagation + outlier library
+ * (liblpa_hip.so, hand-written HIP for gfx950, RCCL for the multi-GPU label
+ * exchange).  Plain pointers and sizes only; no torch types.
+ *
+ * Each entry point replaces one piece of the reference's hot path, which is
+ * the JVM call chain behind
+ *     /root/reference/CommunityDetection/Graphframes.py:78   GraphFrame(v, e)
+ *     /root/reference/CommunityDetection/Graphframes.py:81   .labelPropagation(maxIter=5)
+ *     /root/reference/CommunityDetection/Graphframes.py:92-137 outlier stage
+ * (GraphFrames 0.6.0 / Spark 2.4.5 GraphX, not vendored; see SURVEY.md §2.2
+ * U1-U5).  Semantics: SURVEY.md Appendix A (LPA-DET) and Appendix B
+ * (OUTLIER-DET).  Bindings a host would add: INTEGRATION.md.
+ *
+ * Conventions
+ *   - vertex ids are dense int32 in [0, V); the dense order is the ascending
+ *     order of the caller's original ids, so "smallest label" is preserved;
+ *   - every function returns LPA_OK (0) or a negative LPA_E* code; the
+ *     message is available from lpa_last_error() (thread-local);
+ *   - calls block until the device work they issued has finished;
+ *   - a handle is not thread-safe; distinct handles are independent.
+ */
+#ifndef LPA_H_
+#define LPA_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LPA_OK 0
+#define LPA_EINVAL (-22)   /* bad argument (maxIter <= 0, id out of range, ...) */
+#define LPA_ENOMEM (-12)   /* device or host allocation failed                  */
+#define LPA_ENODEV (-19)   /* no HIP device / bad device ordinal                */
+#define LPA_EHIP (-1000)   /* HIP runtime error                                  */
+#define LPA_ERCCL (-2000)  /* RCCL error                                         */
+
+/* lpa_graph_create* flags */
+#define LPA_INPUT_DEVICE 0x1u /* src/dst are device pointers on `device`        */
+
+#define LPA_NBINS 8
+#define LPA_STATS_MAX_ITERS 64
+
+typedef struct lpa_graph lpa_graph;
+
+/* Per-call timing, filled by lpa_step / lpa_run (HIP events on the handle's stream). */
+typedef struct lpa_stats {
+  int32_t iters;                           /* supersteps executed by this call          */
+  int32_t n_iter_ms;                       /* entries filled in iter_ms                 */
+  float iter_ms[LPA_STATS_MAX_ITERS];      /* device time per superstep (incl. exchange) */
+  float bin_ms[LPA_NBINS];                 /* summed device time per bin kernel         */
+  float exchange_ms;                       /* summed RCCL allgather time                */
+  double total_ms;                         /* device time of all supersteps of the call */
+} lpa_stats;
+
+/* Layout facts of a built graph (this rank's slice). */
+typedef struct lpa_graph_info {
+  int64_t V;            /* vertices (global)                                  */
+  int64_t m;            /* input directed edges (global)                      */
+  int64_t arcs;         /* symmetrised arcs owned by this rank (= 2m at P=1)  */
+  int64_t slice;        /* vertex slots per rank (V padded to P * slice)      */
+  int64_t own_begin;    /* first global (internal) vertex slot of this rank   */
+  int32_t rank, nranks, device;
+  int32_t max_degree;   /* global maximum symmetrised degree                  */
+  int64_t bin_vertices[LPA_NBINS]; /* bins: 0 seg(hub) 1 wave 2 g16 3 g8 4 g4 5 g2 6 g1 7 isolated */
+  int64_t bin_arcs[LPA_NBINS];
+  int64_t hub_vertices; /* vertices split over several segments (global merge) */
+  int64_t segments;     /* segment count of bin 0                             */
+  int64_t device_bytes; /* device memory held by the handle                   */
+} lpa_graph_info;
+
+/* Outlier summary. */
+typedef struct lpa_outlier_summary {
+  int64_t n_groups;      /* L1: distinct communities; L2: distinct (community, sub-label) groups */
+  int64_t k;             /* L1: n_groups / 10                                        */
+  int64_t threshold;     /* L1: size threshold (flag iff size < threshold)           */
+  int64_t n_flagged;     /* vertices flagged                                         */
+  int64_t n_communities; /* distinct top-level communities                           */
+  int64_t n_communities_flagged; /* L2: communities with >= 1 flagged sub-community  */
+  int64_t distinct_edges;        /* distinct directed (s,d) pairs                     */
+} lpa_outlier_summary;
+
+/*
+ * Build the symmetrised, degree-sorted CSR of the multigraph (src[i], dst[i]),
+ * i < m, on HIP device `device`.  Duplicate edges are kept (each is a vote),
+ * a self-loop gives two votes (GraphX sendMessage both ways).
+ * Replaces: GraphFrame.__init__ + cachedTopologyGraphX / GraphX Graph build
+ * (Graphframes.py:78; U1, U2, U5 in SURVEY.md §2.2).
+ */
+int lpa_graph_create(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                     int32_t device, uint32_t flags, lpa_graph** out);
+
+/* RCCL unique id (128 bytes) for lpa_graph_create_dist; produced on one rank and
+ * broadcast by the caller (MPI, torch.distributed, ...). */
+int lpa_comm_unique_id(uint8_t id_out[128]);
+
+/*
+ * Multi-GPU build: one process per GPU.  Every rank passes the SAME edge list;
+ * the rank keeps the CSR rows of its vertex slice (degree-ranked round-robin
+ * 1D partition) and refreshes the replicated label vector with one RCCL
+ * allgather per superstep.  Results are bit-identical to
+ * the single-GPU build.  Replaces the Spark shuffle of aggregateMessages (U5).
+ * comm_id == NULL with nranks > 1 selects the caller-driven exchange below.
+ */
+int lpa_graph_create_dist(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                          int32_t device, uint32_t flags, int32_t rank, int32_t nranks,
+                          const uint8_t comm_id[128], lpa_graph** out);
+
+/*
+ * Caller-driven label exchange (a handle built by lpa_graph_create_dist with
+ * nranks > 1 and comm_id == NULL performs no RCCL collective): after each
+ * lpa_step(g, 1) the caller collects every rank's owned slice of the current
+ * label vector (lpa_exchange_get: `slice` entries, internal slot order) and
+ * writes the concatenation of all slices in rank order back to every rank
+ * (lpa_exchange_put: nranks * slice entries).  Used to test the partitioned
+ * path with P virtual ranks on one device (SURVEY.md §8(e) fake backend).
+ * Host buffers.
+ */
+int lpa_exchange_get(lpa_graph* g, int32_t* slice_out);
+int lpa_exchange_put(lpa_graph* g, const int32_t* full_in);
+
+/* Run on a caller-provided hipStream_t (NULL = the handle's own stream). */
+int lpa_set_stream(lpa_graph* g, void* hip_stream);
+
+/* Labels := L0 (every vertex its own id; LabelPropagation.run mapVertices(vid => vid)). */
+int lpa_reset(lpa_graph* g);
+
+/* Continue the synchronous BSP loop by n_supersteps (Pregel.apply iterations). */
+int lpa_step(lpa_graph* g, int32_t n_supersteps, lpa_stats* stats /* nullable */);
+
+/* Current labels indexed by dense vertex id; out is host memory unless out_is_device. */
+int lpa_get_labels(lpa_graph* g, int32_t* labels_out, int32_t out_is_device);
+
+/*
+ * labelPropagation(maxIter): reset + max_iter supersteps + labels.
+ * max_iter <= 0 -> LPA_EINVAL ("Maximum of steps must be greater than 0", U3 require).
+ * Replaces: GraphFrame.labelPropagation -> lib.LabelPropagation.run ->
+ * graphx.lib.LabelPropagation.run -> Pregel.apply (Graphframes.py:81).
+ */
+int lpa_run(lpa_graph* g, int32_t max_iter, int32_t* labels_out, int32_t out_is_device,
+            lpa_stats* stats /* nullable */);
+
+/*
+ * Outlier stage over `labels` (dense-id indexed; host unless labels_on_device).
+ * mode 1 = L1 (top-level community-size threshold), mode 2 = L2 (second LPA of
+ * sub_iter supersteps on the intra-community distinct-edge subgraph, threshold
+ * per community).  Outputs are host arrays of V entries, each nullable:
+ *   size_hist[l]   members of community l              (Graphframes.py:100-104, :120)
+ *   incident[l]    distinct directed edges touching l  (Graphframes.py:107-118)
+ *   sub_labels[v]  L2 only: second-level label         (Graphframes.py:121-128)
+ *   flags[v]       1 = outlier                          (Graphframes.py:130-137)
+ */
+int lpa_outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
+                int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
+                uint8_t* flags, lpa_outlier_summary* summary);
+
+/* Symmetrised degree of every vertex (dense ids), host output. */
+int lpa_degrees(lpa_graph* g, int32_t* deg_out);
+
+int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info);
+void lpa_graph_destroy(lpa_graph* g);
+const char* lpa_last_error(void);
+
+/* ---- synthetic inputs; device outputs, caller-allocated ---- */
+/* R-MAT, Graph500 A/B/C/D = .57/.19/.19/.05, m edges over 2^scale vertices,
+ * duplicates and self-loops kept, optional seeded bijective id scramble. */
+int lpa_gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t scramble, int32_t* d_src,
+                 int32_t* d_dst, int32_t device, void* hip_stream);
+/* planted-partition SBM: V vertices in `blocks` equal blocks, p_in as a Q32 fraction. */
+int lpa_gen_sbm(int32_t V, int32_t blocks, int64_t m, uint32_t p_in_q32, uint64_t seed,
+                int32_t* d_src, int32_t* d_dst, int32_t device, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LPA_H_ */

@@ -1,0 +1,53 @@
+"""Seeded test graphs covering every degree bin and the edge cases of the path."""
+import numpy as np
+
+
+def two_cliques(n=5):
+    """Upstream LabelPropagationSuite shape (Spark graphx + GraphFrames): clique1 =
+    all (u, v) for u, v in [0, n) (self-loops included), clique2 = all (u+n, v+n)
+    for u, v in [0, n], plus the bridge (0, n)."""
+    e = [(u, v) for u in range(n) for v in range(n)]
+    e += [(u + n, v + n) for u in range(n + 1) for v in range(n + 1)]
+    e.append((0, n))
+    a = np.array(e, dtype=np.int32)
+    return 2 * n + 1, a[:, 0].copy(), a[:, 1].copy()
+
+
+def star(k):
+    """Hub 0 with leaves 1..k: period-2 oscillation under synchronous LPA."""
+    s = np.zeros(k, dtype=np.int32)
+    d = np.arange(1, k + 1, dtype=np.int32)
+    return k + 1, s, d
+
+
+def degree_mix(seed=0, hubs=(600, 2100, 4500, 9000), n_low=3000, extra=20000):
+    """Random multigraph whose symmetrised degrees span every bin: a few hubs
+    (single- and multi-segment), a wave band, and the g1..g16 bands; duplicates,
+    self-loops and isolated vertices included."""
+    rng = np.random.default_rng(seed)
+    V = n_low + len(hubs) + 50
+    src, dst = [], []
+    for h, deg in enumerate(hubs):
+        nb = rng.integers(len(hubs), V, size=deg)
+        # few distinct neighbours for some hubs -> repeated labels, many for others
+        if h % 2:
+            nb = nb % 97 + len(hubs)
+        src.append(np.full(deg, h))
+        dst.append(nb)
+    s = rng.integers(len(hubs), V - 50, size=extra)
+    d = rng.integers(len(hubs), V - 50, size=extra)
+    # skew: square-law endpoints make a wave band of medium degrees
+    d = (len(hubs) + ((d - len(hubs)) ** 2) // (V - 50 - len(hubs))).astype(np.int64)
+    src.append(s)
+    dst.append(d)
+    src.append(np.array([len(hubs) + 7, len(hubs) + 9]))   # self-loops
+    dst.append(np.array([len(hubs) + 7, len(hubs) + 9]))
+    s = np.concatenate(src).astype(np.int32)
+    d = np.concatenate(dst).astype(np.int32)
+    perm = rng.permutation(V).astype(np.int32)   # scramble ids
+    return V, perm[s], perm[d]
+
+
+def random_multigraph(V, m, seed):
+    rng = np.random.default_rng(seed)
+    return V, rng.integers(0, V, size=m).astype(np.int32), rng.integers(0, V, size=m).astype(np.int32)

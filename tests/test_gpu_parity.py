@@ -1,0 +1,214 @@
+"""GPU parity: liblpa_hip.so (through its C ABI) vs the CPU oracle and the
+committed golden fixture.  Bit-exact labels per superstep (integer path)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from graphs import degree_mix, random_multigraph, star, two_cliques
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gfa():
+    import graphframes_amd
+
+    return graphframes_amd
+
+
+def _per_step(gfa, V, s, d, iters):
+    out = []
+    with gfa.Graph(s, d, V) as g:
+        for _ in range(iters):
+            g.step(1)
+            out.append(g.labels())
+    return np.stack(out) if out else np.empty((0, V), np.int32)
+
+
+def test_r9_golden_every_superstep(gfa, golden):
+    V = golden["ids"].size
+    got = _per_step(gfa, V, golden["src"], golden["dst"], 10)
+    for t in range(10):
+        bad = int((got[t] != golden["labels_iter"][t]).sum())
+        assert bad == 0, f"superstep {t + 1}: {bad} labels differ"
+
+
+def test_r9_run_matches_step(gfa, golden):
+    V = golden["ids"].size
+    with gfa.Graph(golden["src"], golden["dst"], V) as g:
+        lab, st = g.run(5, stats=True)
+        assert st["iters"] == 5 and len(st["iter_ms"]) == 5
+        assert np.array_equal(lab, golden["labels_iter"][4])
+        # run() resets: a second call gives the same answer
+        assert np.array_equal(g.run(5), lab)
+
+
+def test_two_cliques_kat(gfa):
+    V, s, d = two_cliques()
+    with gfa.Graph(s, d, V) as g:
+        lab = g.run(20)
+    assert lab.tolist() == [0] * 5 + [5] * 6
+
+
+def test_star_oscillates(gfa):
+    V, s, d = star(40)
+    got = _per_step(gfa, V, s, d, 4)
+    assert (got[0][1:] == 0).all() and got[0][0] == 1
+    assert (got[1][1:] == 1).all() and got[1][0] == 0
+    assert np.array_equal(got[2], got[0]) and np.array_equal(got[3], got[1])
+
+
+def test_edge_cases(gfa, oracle):
+    # self-loop = 2 votes for own label; duplicates counted; isolated keep label
+    V = 6
+    s = np.array([0, 0, 1, 1, 1, 2], np.int32)
+    d = np.array([0, 1, 2, 2, 3, 4], np.int32)
+    with gfa.Graph(s, d, V) as g:
+        for it in (1, 2, 3, 7):
+            assert np.array_equal(g.run(it), oracle.lpa(V, s, d, it))
+    # edgeless graph: every label stays
+    with gfa.Graph(np.zeros(0, np.int32), np.zeros(0, np.int32), 4) as g:
+        assert g.run(3).tolist() == [0, 1, 2, 3]
+    # single vertex with a self loop
+    with gfa.Graph(np.zeros(1, np.int32), np.zeros(1, np.int32), 1) as g:
+        assert g.run(2).tolist() == [0]
+
+
+def test_bad_arguments(gfa):
+    with gfa.Graph(np.array([0], np.int32), np.array([1], np.int32), 2) as g:
+        with pytest.raises(ValueError, match="Maximum of steps must be greater than 0"):
+            g.run(0)
+    with pytest.raises(ValueError, match="outside"):
+        gfa.Graph(np.array([0], np.int32), np.array([5], np.int32), 2)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_degree_mix_all_bins(gfa, oracle, seed):
+    V, s, d = degree_mix(seed)
+    with gfa.Graph(s, d, V) as g:
+        info = g.info()
+        assert info["hub_vertices"] >= 2 and info["bin_vertices"]["wave"] > 0
+        assert all(info["bin_vertices"][b] > 0 for b in ("g16", "g8", "g4", "g2", "g1"))
+    _, hist, _ = oracle.lpa(V, s, d, 6, per_iter=True)
+    got = _per_step(gfa, V, s, d, 6)
+    for t in range(6):
+        assert np.array_equal(got[t], hist[t]), f"seed {seed} superstep {t + 1}"
+
+
+@pytest.mark.parametrize("V,m,seed", [(50, 2000, 3), (3000, 60000, 4), (20000, 40000, 5)])
+def test_random_multigraphs(gfa, oracle, V, m, seed):
+    V, s, d = random_multigraph(V, m, seed)
+    with gfa.Graph(s, d, V) as g:
+        for it in (1, 4):
+            assert np.array_equal(g.run(it), oracle.lpa(V, s, d, it))
+
+
+def test_generators_match_cpu_restatement(gfa, oracle):
+    s, d = gfa.gen_rmat(14, 16, seed=1)
+    cs, cd = oracle.gen_rmat(14, 16, seed=1)
+    assert np.array_equal(s.cpu().numpy(), cs) and np.array_equal(d.cpu().numpy(), cd)
+    s, d = gfa.gen_sbm(10000, 100, 200000, seed=20261015)
+    cs, cd = oracle.gen_sbm(10000, 100, 200000, seed=20261015)
+    assert np.array_equal(s.cpu().numpy(), cs) and np.array_equal(d.cpu().numpy(), cd)
+
+
+@pytest.mark.parametrize("scale", [12, 16])
+def test_rmat_bit_exact(gfa, oracle, scale):
+    s, d = gfa.gen_rmat(scale, 16, seed=1)
+    V = 1 << scale
+    with gfa.Graph(s, d, V) as g:   # device input path
+        got = []
+        for _ in range(10):
+            g.step(1)
+            got.append(g.labels())
+    _, hist, _ = oracle.lpa(V, s.cpu().numpy(), d.cpu().numpy(), 10, per_iter=True)
+    for t in range(10):
+        assert np.array_equal(got[t], hist[t]), f"R-MAT {scale} superstep {t + 1}"
+
+
+def test_sbm_bit_exact(gfa, oracle):
+    s, d = gfa.gen_sbm(20000, 20, 400000)
+    with gfa.Graph(s, d, 20000) as g:
+        lab = g.run(10)
+    assert np.array_equal(lab, oracle.lpa(20000, s.cpu().numpy(), d.cpu().numpy(), 10))
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_virtual_partitions_bit_exact(gfa, oracle, P):
+    """P ranks on one device with the caller-driven exchange: the partitioned
+    build + kernels give the single-GPU answer bit for bit."""
+    V, s, d = degree_mix(7)
+    ranks = [gfa.Graph(s, d, V, rank=r, nranks=P) for r in range(P)]
+    try:
+        infos = [g.info() for g in ranks]
+        assert sum(i["arcs"] for i in infos) == 2 * s.size
+        _, hist, _ = oracle.lpa(V, s, d, 5, per_iter=True)
+        for t in range(5):
+            for g in ranks:
+                g.step(1)
+            full = np.concatenate([g.exchange_get() for g in ranks])
+            for g in ranks:
+                g.exchange_put(full)
+            assert np.array_equal(ranks[0].labels(), hist[t]), f"P={P} superstep {t + 1}"
+    finally:
+        for g in ranks:
+            g.close()
+
+
+def test_outlier_l1_l2_golden(gfa, golden):
+    V = golden["ids"].size
+    with gfa.Graph(golden["src"], golden["dst"], V) as g:
+        lab = g.run(5)
+        o1 = g.outlier(lab, "L1")
+        assert np.array_equal(o1["size"], golden["l1_size"])
+        assert np.array_equal(o1["incident"], golden["l1_inc"])
+        assert np.array_equal(o1["flags"], golden["l1_flags"].astype(bool))
+        s1 = golden["l1_summary"]
+        assert (o1["summary"]["n_groups"], o1["summary"]["k"], o1["summary"]["threshold"],
+                o1["summary"]["n_flagged"]) == tuple(int(x) for x in s1)
+        o2 = g.outlier(lab, "L2", sub_iter=5)
+        assert np.array_equal(o2["sub_labels"], golden["l2_sub"])
+        assert np.array_equal(o2["flags"], golden["l2_flags"].astype(bool))
+        s2 = golden["l2_summary"]
+        assert (o2["summary"]["n_communities"], o2["summary"]["n_groups"], o2["summary"]["n_flagged"],
+                o2["summary"]["n_communities_flagged"]) == tuple(int(x) for x in s2)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_outlier_vs_oracle(gfa, oracle, seed):
+    V, s, d = degree_mix(seed, hubs=(700, 3000), n_low=2000, extra=8000)
+    with gfa.Graph(s, d, V) as g:
+        lab = g.run(3)
+        o1 = g.outlier(lab, "L1")
+        size, inc, flags, summ = oracle.outlier_l1(V, s, d, lab)
+        assert np.array_equal(o1["size"], size) and np.array_equal(o1["incident"], inc)
+        assert np.array_equal(o1["flags"], flags)
+        assert o1["summary"]["threshold"] == summ["thr"]
+        o2 = g.outlier(lab, "L2", sub_iter=4)
+        sub, flags2, summ2 = oracle.outlier_l2(V, s, d, lab, 4)
+        assert np.array_equal(o2["sub_labels"], sub) and np.array_equal(o2["flags"], flags2)
+        assert o2["summary"]["n_flagged"] == summ2["n_flagged"]
+
+
+def test_dropin_graphframe_r9(gfa, golden):
+    """GraphFrame(v, e).labelPropagation(maxIter=5) exactly as Graphframes.py:78-81 calls it."""
+    ids, names = golden["ids"], golden["names"]
+    v = pd.DataFrame({"id": ids, "name": names}).sample(frac=1.0, random_state=0)
+    e = pd.DataFrame({"src": ids[golden["src"]], "dst": ids[golden["dst"]]})
+    out = gfa.GraphFrame(v, e).labelPropagation(maxIter=5)
+    assert list(out.columns) == ["id", "name", "label"] and out["label"].dtype == np.int64
+    assert out["id"].tolist() == sorted(ids.tolist())
+    assert np.array_equal(out["label"].to_numpy(), golden["labels_iter"][4].astype(np.int64))
+    assert out["label"].nunique() == 619   # Graphframes.py:85 community count
+
+
+def test_dropin_integral_ids_and_dangling(gfa, oracle):
+    V, s, d = two_cliques()
+    ids = np.arange(V, dtype=np.int64) * 10 + 7
+    v = pd.DataFrame({"id": ids, "attr": np.arange(V)})
+    e = pd.DataFrame({"src": np.append(ids[s], 999), "dst": np.append(ids[d], 7)})  # dangling edge
+    out = gfa.label_propagation(v, e, 20)
+    assert out["label"].tolist() == [7] * 5 + [57] * 6   # labels are original ids
+    res = gfa.outlier_scores(v, e, labels=out, mode="L1")
+    assert res.communities["size"].tolist() == [5, 6]
+    assert res.summary["threshold"] == 6 and res.flagged_ids.tolist() == ids[:5].tolist()
