@@ -19,8 +19,11 @@ LPA_EHIP = -1000
 LPA_ERCCL = -2000
 LPA_INPUT_DEVICE = 0x1
 LPA_NBINS = 8
+LPA_NKERNELS = 8
 LPA_STATS_MAX_ITERS = 64
 BIN_NAMES = ("seg", "wave", "g16", "g8", "g4", "g2", "g1", "isolated")
+KERNEL_NAMES = ("k_lpa_seg", "k_lpa_hub_final", "k_lpa_wave", "k_lpa_group<16>", "k_lpa_group<8>",
+                "k_lpa_group<4>", "k_lpa_group<2>", "k_lpa_group<1>")
 
 
 class LpaStats(ctypes.Structure):
@@ -28,14 +31,14 @@ class LpaStats(ctypes.Structure):
         ("iters", ctypes.c_int32),
         ("n_iter_ms", ctypes.c_int32),
         ("iter_ms", ctypes.c_float * LPA_STATS_MAX_ITERS),
-        ("bin_ms", ctypes.c_float * LPA_NBINS),
+        ("kernel_ms", ctypes.c_float * LPA_NKERNELS),
         ("exchange_ms", ctypes.c_float),
         ("total_ms", ctypes.c_double),
     ]
 
     def to_dict(self):
         return dict(iters=self.iters, iter_ms=list(self.iter_ms[: self.n_iter_ms]),
-                    bin_ms={BIN_NAMES[b]: self.bin_ms[b] for b in range(LPA_NBINS)},
+                    kernel_ms={KERNEL_NAMES[k]: self.kernel_ms[k] for k in range(LPA_NKERNELS)},
                     exchange_ms=self.exchange_ms, total_ms=self.total_ms)
 
 
@@ -115,6 +118,14 @@ def load():
         raise ImportError(
             f"{LIB_PATH} is missing: the HIP library has not been built. "
             "Run `python -c 'import __graft_entry__ as g; g.build()'` (or `make -C <pkg>/csrc`).")
+    try:
+        # One HIP runtime per process: torch-ROCm ships its own libamdhip64 /
+        # librccl / libhsa-runtime64 (same sonames as /opt/rocm's).  Loading torch
+        # first makes liblpa_hip.so bind to those already-loaded copies; loading
+        # ours first would leave torch to open a second runtime that sees no GPU.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

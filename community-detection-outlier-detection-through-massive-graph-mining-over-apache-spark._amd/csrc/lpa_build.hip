@@ -202,7 +202,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   // ---- 1. degrees ----
   int32_t* d_err = nullptr;
   int32_t* d_max = nullptr;
-  LPA_HIP(hipMallocAsync((void**)&d_err, 2 * sizeof(int32_t), s));
+  LPA_HIP(hipMalloc((void**)&d_err, 2 * sizeof(int32_t)));
   d_max = d_err + 1;
   LPA_HIP(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), s));
   LPA_TRY(dev_alloc(g, (void**)&g->deg, sizeof(int32_t) * (V > 0 ? V : 1)));
@@ -219,7 +219,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   int32_t h_err[2] = {0, 0};
   LPA_HIP(hipMemcpyAsync(h_err, d_err, sizeof(h_err), hipMemcpyDeviceToHost, s));
   LPA_HIP(hipStreamSynchronize(s));
-  LPA_HIP(hipFreeAsync(d_err, s));
+  LPA_HIP(hipFree(d_err));
   if (h_err[0]) {
     set_error("edge endpoint outside [0, V=%d)", V);
     return LPA_EINVAL;
@@ -232,7 +232,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   LPA_HIP(hipMemsetAsync(g->old_of, 0xFF, sizeof(int32_t) * g->vpad, s));
   if (V > 0) {
     u64* vk = nullptr;
-    LPA_HIP(hipMallocAsync((void**)&vk, sizeof(u64) * 2 * V, s));
+    LPA_HIP(hipMalloc((void**)&vk, sizeof(u64) * 2 * V));
     hipLaunchKernelGGL(k_vertex_keys, dim3(grid_for(V)), dim3(256), 0, s, g->deg, (int64_t)V,
                        g->max_degree, vk);
     LPA_HIP(hipGetLastError());
@@ -244,12 +244,12 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     hipLaunchKernelGGL(k_vertex_order, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, P, S,
                        g->new_of, g->old_of);
     LPA_HIP(hipGetLastError());
-    LPA_HIP(hipFreeAsync(vk, s));
+    LPA_HIP(hipFree(vk));
   }
 
   // ---- owned degrees, row_ptr ----
   int32_t* deg_own = nullptr;
-  LPA_HIP(hipMallocAsync((void**)&deg_own, sizeof(int32_t) * S, s));
+  LPA_HIP(hipMalloc((void**)&deg_own, sizeof(int32_t) * S));
   hipLaunchKernelGGL(k_owned_degree, dim3(grid_for(S)), dim3(256), 0, s, g->old_of + g->own_begin,
                      g->deg, S, deg_own);
   LPA_HIP(hipGetLastError());
@@ -264,7 +264,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
   if (arcs > 0) {
     u64* keys = nullptr;
-    if (hipMallocAsync((void**)&keys, sizeof(u64) * 2 * arcs, s) != hipSuccess) {
+    if (hipMalloc((void**)&keys, sizeof(u64) * 2 * arcs) != hipSuccess) {
       set_error("out of device memory for %lld arc keys", (long long)(2 * arcs));
       return LPA_ENOMEM;
     }
@@ -273,11 +273,11 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
                          g->e_dst, m, g->new_of, keys);
     } else {
       unsigned long long* cursor = nullptr;
-      LPA_HIP(hipMallocAsync((void**)&cursor, sizeof(unsigned long long), s));
+      LPA_HIP(hipMalloc((void**)&cursor, sizeof(unsigned long long)));
       LPA_HIP(hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
       hipLaunchKernelGGL(k_emit_arcs_owned, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
                          g->e_dst, m, g->new_of, g->own_begin, g->own_begin + S, keys, cursor);
-      LPA_HIP(hipFreeAsync(cursor, s));
+      LPA_HIP(hipFree(cursor));
     }
     LPA_HIP(hipGetLastError());
     int shifts[16], ns = 0;
@@ -287,7 +287,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
     hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col);
     LPA_HIP(hipGetLastError());
-    LPA_HIP(hipFreeAsync(keys, s));
+    LPA_HIP(hipFree(keys));
   }
 
   // ---- 4. degree bins (contiguous slot ranges) ----
@@ -295,16 +295,16 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     const int32_t thr_h[8] = {kWaveMaxDeg, 16, 8, 4, 2, 1, 0, kSegArcs};
     int32_t* d_thr = nullptr;
     int64_t* d_bb = nullptr;
-    LPA_HIP(hipMallocAsync((void**)&d_thr, sizeof(thr_h), s));
-    LPA_HIP(hipMallocAsync((void**)&d_bb, sizeof(int64_t) * 8, s));
+    LPA_HIP(hipMalloc((void**)&d_thr, sizeof(thr_h)));
+    LPA_HIP(hipMalloc((void**)&d_bb, sizeof(int64_t) * 8));
     LPA_HIP(hipMemcpyAsync(d_thr, thr_h, sizeof(thr_h), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_bin_bounds, dim3(1), dim3(64), 0, s, deg_own, S, d_thr, 8, d_bb);
     LPA_HIP(hipGetLastError());
     int64_t bb[8];
     LPA_HIP(hipMemcpyAsync(bb, d_bb, sizeof(bb), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
-    LPA_HIP(hipFreeAsync(d_thr, s));
-    LPA_HIP(hipFreeAsync(d_bb, s));
+    LPA_HIP(hipFree(d_thr));
+    LPA_HIP(hipFree(d_bb));
     g->bin_begin[0] = 0;
     for (int b = 1; b < LPA_NBINS; ++b) g->bin_begin[b] = bb[b - 1];
     g->bin_begin[LPA_NBINS] = S;
@@ -323,9 +323,9 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     int32_t* nseg = nullptr;
     int32_t* hubcap = nullptr;
     int64_t* seg_off = nullptr;
-    LPA_HIP(hipMallocAsync((void**)&nseg, sizeof(int32_t) * n0, s));
-    LPA_HIP(hipMallocAsync((void**)&hubcap, sizeof(int32_t) * (g->n_hub > 0 ? g->n_hub : 1), s));
-    LPA_HIP(hipMallocAsync((void**)&seg_off, sizeof(int64_t) * (n0 + 1), s));
+    LPA_HIP(hipMalloc((void**)&nseg, sizeof(int32_t) * n0));
+    LPA_HIP(hipMalloc((void**)&hubcap, sizeof(int32_t) * (g->n_hub > 0 ? g->n_hub : 1)));
+    LPA_HIP(hipMalloc((void**)&seg_off, sizeof(int64_t) * (n0 + 1)));
     hipLaunchKernelGGL(k_seg_counts, dim3(grid_for(n0)), dim3(256), 0, s, deg_own, n0, nseg,
                        hubcap, g->n_hub);
     LPA_HIP(hipGetLastError());
@@ -348,11 +348,11 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
       LPA_HIP(hipMemsetAsync(g->gtab, 0, sizeof(u64) * tot, s));
       LPA_HIP(hipMemsetAsync(g->gcnt, 0, sizeof(int32_t) * g->n_hub, s));
     }
-    LPA_HIP(hipFreeAsync(nseg, s));
-    LPA_HIP(hipFreeAsync(hubcap, s));
-    LPA_HIP(hipFreeAsync(seg_off, s));
+    LPA_HIP(hipFree(nseg));
+    LPA_HIP(hipFree(hubcap));
+    LPA_HIP(hipFree(seg_off));
   }
-  LPA_HIP(hipFreeAsync(deg_own, s));
+  LPA_HIP(hipFree(deg_own));
 
   // ---- labels (replicated, ping-pong) ----
   LPA_TRY(dev_alloc(g, (void**)&g->lab[0], sizeof(int32_t) * g->vpad));

@@ -259,11 +259,11 @@ int lpa_get_labels(lpa_graph* g, int32_t* labels_out, int32_t out_is_device) {
     LPA_TRY(gather_labels(g, labels_out));
   } else {
     int32_t* tmp = nullptr;
-    LPA_HIP(hipMallocAsync((void**)&tmp, sizeof(int32_t) * g->V, g->stream));
+    LPA_HIP(hipMalloc((void**)&tmp, sizeof(int32_t) * g->V));
     int rc = gather_labels(g, tmp);
     if (rc == LPA_OK)
       LPA_HIP(hipMemcpyAsync(labels_out, tmp, sizeof(int32_t) * g->V, hipMemcpyDeviceToHost, g->stream));
-    LPA_HIP(hipFreeAsync(tmp, g->stream));
+    LPA_HIP(hipFree(tmp));
     if (rc != LPA_OK) return rc;
   }
   LPA_HIP(hipStreamSynchronize(g->stream));

@@ -25,7 +25,7 @@ constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 16 < deg <
 constexpr int kWaveCap = 1024;        // per-wave LDS table entries (>= 2 * kWaveMaxDeg)
 constexpr int kSegArcs = 2048;        // arcs per block segment (hub path)
 constexpr int kSegCap = 4096;         // per-block LDS table entries (>= 2 * kSegArcs)
-constexpr int kBinEvents = LPA_NBINS + 1;  // event marks per timed superstep
+constexpr int kBinEvents = LPA_NKERNELS + 2;  // event marks per timed superstep
 
 struct Segment {
   int64_t begin;  // first arc (local CSR index)

@@ -332,25 +332,26 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
 
 // launch the bin kernels of one superstep; bin events optional
 int launch_superstep(lpa_graph* g, const int32_t* Lc, int32_t* Lown, hipEvent_t* bev) {
+  // bev marks: 0 start, k+1 after kernel k (0 seg, 1 hub_final, 2 wave, 3..7 g16..g1)
   hipStream_t s = g->stream;
   const int64_t* bb = g->bin_begin;
   auto mark = [&](int i) -> int {
     if (bev) LPA_HIP(hipEventRecord(bev[i], s));
     return LPA_OK;
   };
-  // seg (+ hub final)
   LPA_TRY(mark(0));
   if (g->n_segs > 0) {
     hipLaunchKernelGGL(k_lpa_seg, dim3(cap_grid(g->n_segs, 1024)), dim3(256), 0, s, g->col, Lc,
                        Lown, g->segs, g->n_segs, g->gtab, g->glist, g->gcnt, g->hub_off);
     LPA_HIP(hipGetLastError());
-    if (g->n_hub > 0) {
-      hipLaunchKernelGGL(k_lpa_hub_final, dim3(cap_grid(g->n_hub, 1024)), dim3(256), 0, s, g->gtab,
-                         g->glist, g->gcnt, g->hub_off, Lown, g->n_hub);
-      LPA_HIP(hipGetLastError());
-    }
   }
   LPA_TRY(mark(1));
+  if (g->n_hub > 0) {
+    hipLaunchKernelGGL(k_lpa_hub_final, dim3(cap_grid(g->n_hub, 1024)), dim3(256), 0, s, g->gtab,
+                       g->glist, g->gcnt, g->hub_off, Lown, g->n_hub);
+    LPA_HIP(hipGetLastError());
+  }
+  LPA_TRY(mark(2));
   {
     const int64_t n = bb[BIN_WAVE + 1] - bb[BIN_WAVE];
     if (n > 0) {
@@ -359,7 +360,7 @@ int launch_superstep(lpa_graph* g, const int32_t* Lc, int32_t* Lown, hipEvent_t*
       LPA_HIP(hipGetLastError());
     }
   }
-  LPA_TRY(mark(2));
+  LPA_TRY(mark(3));
 #define LPA_GROUP_LAUNCH(BIN, G)                                                             \
   {                                                                                          \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
@@ -368,7 +369,7 @@ int launch_superstep(lpa_graph* g, const int32_t* Lc, int32_t* Lown, hipEvent_t*
                          s, g->rp, g->col, Lc, Lown, bb[BIN], bb[BIN + 1]);                 \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
-    LPA_TRY(mark(BIN + 1));                                                                  \
+    LPA_TRY(mark(BIN + 2));                                                                  \
   }
   LPA_GROUP_LAUNCH(BIN_G16, 16)
   LPA_GROUP_LAUNCH(BIN_G8, 8)
@@ -393,8 +394,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       if (!g->bin_ev[i]) LPA_HIP(hipEventCreate(&g->bin_ev[i]));
     LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS], s));
   }
-  // per timed superstep t, bin marks bin_ev[t*kBinEvents + i]:
-  //   0 start, 1 after seg(+hub final), 2 after wave, 3..7 after g16..g1, 8 after exchange
+  // per timed superstep t, marks bin_ev[t*kBinEvents + i]: 0 start, k+1 after kernel k,
+  // LPA_NKERNELS+1 after the exchange
   for (int32_t t = 0; t < n; ++t) {
     const int32_t* Lc = g->lab[g->cur];
     int32_t* Ln = g->lab[g->cur ^ 1];
@@ -411,7 +412,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       }
     }
     if (tt) {
-      LPA_HIP(hipEventRecord(bev[LPA_NBINS], s));
+      LPA_HIP(hipEventRecord(bev[LPA_NKERNELS + 1], s));
       LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     }
     g->cur ^= 1;
@@ -425,11 +426,11 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       LPA_HIP(hipEventElapsedTime(&st->iter_ms[t], g->ev[2 * t], g->ev[2 * t + 1]));
       hipEvent_t* bev = &g->bin_ev[t * kBinEvents];
       float ms;
-      for (int b = BIN_SEG; b <= BIN_G1; ++b) {
-        LPA_HIP(hipEventElapsedTime(&ms, bev[b], bev[b + 1]));
-        st->bin_ms[b] += ms;
+      for (int k = 0; k < LPA_NKERNELS; ++k) {
+        LPA_HIP(hipEventElapsedTime(&ms, bev[k], bev[k + 1]));
+        st->kernel_ms[k] += ms;
       }
-      LPA_HIP(hipEventElapsedTime(&ms, bev[BIN_G1 + 1], bev[LPA_NBINS]));
+      LPA_HIP(hipEventElapsedTime(&ms, bev[LPA_NKERNELS], bev[LPA_NKERNELS + 1]));
       st->exchange_ms += ms;
     }
     float tot;

@@ -158,7 +158,7 @@ struct Scratch {
   template <typename T>
   int get(T** p, int64_t count) {
     if (count < 1) count = 1;
-    if (hipMallocAsync((void**)p, sizeof(T) * count, s) != hipSuccess) {
+    if (hipMalloc((void**)p, sizeof(T) * count) != hipSuccess) {
       set_error("outlier: out of device memory (%lld x %zu B)", (long long)count, sizeof(T));
       return LPA_ENOMEM;
     }
@@ -166,7 +166,7 @@ struct Scratch {
     return LPA_OK;
   }
   ~Scratch() {
-    for (int i = 0; i < n; ++i) (void)hipFreeAsync(ptrs[i], s);
+    for (int i = 0; i < n; ++i) (void)hipFree(ptrs[i]);
   }
 };
 

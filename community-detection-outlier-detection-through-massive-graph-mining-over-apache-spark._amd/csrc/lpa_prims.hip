@@ -103,8 +103,8 @@ int scan_impl(const Tin* in, Tout* out, int64_t n, hipStream_t s) {
   }
   Tout* part = nullptr;
   Tout* partx = nullptr;
-  LPA_HIP(hipMallocAsync((void**)&part, sizeof(Tout) * nblk, s));
-  LPA_HIP(hipMallocAsync((void**)&partx, sizeof(Tout) * (nblk + 1), s));
+  LPA_HIP(hipMalloc((void**)&part, sizeof(Tout) * nblk));
+  LPA_HIP(hipMalloc((void**)&partx, sizeof(Tout) * (nblk + 1)));
   hipLaunchKernelGGL((k_scan_reduce<Tin, Tout>), dim3((unsigned)nblk), dim3(kThreads), 0, s, in,
                      n, part);
   LPA_HIP(hipGetLastError());
@@ -114,8 +114,8 @@ int scan_impl(const Tin* in, Tout* out, int64_t n, hipStream_t s) {
                        n, out, (const Tout*)partx);
     LPA_HIP(hipGetLastError());
   }
-  LPA_HIP(hipFreeAsync(part, s));
-  LPA_HIP(hipFreeAsync(partx, s));
+  LPA_HIP(hipFree(part));
+  LPA_HIP(hipFree(partx));
   return rc;
 }
 
@@ -217,8 +217,8 @@ int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshift
   const int64_t nh = 256 * nblk;
   u32* hist = nullptr;
   u32* offs = nullptr;
-  LPA_HIP(hipMallocAsync((void**)&hist, sizeof(u32) * nh, s));
-  LPA_HIP(hipMallocAsync((void**)&offs, sizeof(u32) * (nh + 1), s));
+  LPA_HIP(hipMalloc((void**)&hist, sizeof(u32) * nh));
+  LPA_HIP(hipMalloc((void**)&offs, sizeof(u32) * (nh + 1)));
   u64* a = keys;
   u64* b = tmp;
   int rc = LPA_OK;
@@ -236,8 +236,8 @@ int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshift
     b = t;
   }
   if (rc == LPA_OK && a != keys) LPA_HIP(hipMemcpyAsync(keys, a, sizeof(u64) * n, hipMemcpyDeviceToDevice, s));
-  LPA_HIP(hipFreeAsync(hist, s));
-  LPA_HIP(hipFreeAsync(offs, s));
+  LPA_HIP(hipFree(hist));
+  LPA_HIP(hipFree(offs));
   return rc;
 }
 

@@ -40,6 +40,7 @@ extern "C" {
 #define LPA_INPUT_DEVICE 0x1u /* src/dst are device pointers on `device`        */
 
 #define LPA_NBINS 8
+#define LPA_NKERNELS 8 /* timed kernels: 0 seg 1 hub_final 2 wave 3 g16 4 g8 5 g4 6 g2 7 g1 */
 #define LPA_STATS_MAX_ITERS 64
 
 typedef struct lpa_graph lpa_graph;
@@ -49,7 +50,7 @@ typedef struct lpa_stats {
   int32_t iters;                           /* supersteps executed by this call          */
   int32_t n_iter_ms;                       /* entries filled in iter_ms                 */
   float iter_ms[LPA_STATS_MAX_ITERS];      /* device time per superstep (incl. exchange) */
-  float bin_ms[LPA_NBINS];                 /* summed device time per bin kernel         */
+  float kernel_ms[LPA_NKERNELS];           /* summed device time per kernel (first 64)  */
   float exchange_ms;                       /* summed RCCL allgather time                */
   double total_ms;                         /* device time of all supersteps of the call */
 } lpa_stats;
