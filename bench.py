@@ -30,9 +30,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
 
 
 def kernel_bytes(info, name):
-    """Algorithmic bytes per launch of one bin kernel (SURVEY.md §8(d) contract):
-    4 B col index + 4 B neighbour-label gather per arc, 8 B row_ptr + 4 B label
-    write per vertex."""
+    """Algorithmic bytes per launch of one tally kernel.  The tally streams the
+    replicated neighbour labels al[] (4 B per arc) instead of col + label gather
+    (SURVEY.md §8(d) counts 8 B per arc for that formulation); per vertex it reads
+    8 B of row offsets (seg: a 16 B segment descriptor per segment) and writes a
+    4 B label."""
     b = {"k_lpa_seg": "seg", "k_lpa_wave": "wave", "k_lpa_group<16>": "g16",
          "k_lpa_group<8>": "g8", "k_lpa_group<4>": "g4", "k_lpa_group<2>": "g2",
          "k_lpa_group<1>": "g1"}.get(name)
@@ -40,7 +42,9 @@ def kernel_bytes(info, name):
         return None
     A = info["bin_arcs"][b]
     n = info["bin_vertices"][b]
-    return 8 * A + 12 * n + 8
+    if b == "seg":
+        return 4 * A + 16 * info["segments"] + 4 * n
+    return 4 * A + 8 * (n + 1) + 4 * n
 
 
 def cpu_baseline(src_np, dst_np, V, gpu_graph, warmup, budget_s=25.0):

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblpa_hip.so")
+# LPA_LIB_PATH: load a diagnostic build instead (profiling experiments only)
+LIB_PATH = os.environ.get("LPA_LIB_PATH") or os.path.join(_HERE, "liblpa_hip.so")
 
 LPA_OK = 0
 LPA_EINVAL = -22
@@ -19,11 +20,11 @@ LPA_EHIP = -1000
 LPA_ERCCL = -2000
 LPA_INPUT_DEVICE = 0x1
 LPA_NBINS = 8
-LPA_NKERNELS = 8
+LPA_NKERNELS = 9
 LPA_STATS_MAX_ITERS = 64
 BIN_NAMES = ("seg", "wave", "g16", "g8", "g4", "g2", "g1", "isolated")
 KERNEL_NAMES = ("k_lpa_seg", "k_lpa_hub_final", "k_lpa_wave", "k_lpa_group<16>", "k_lpa_group<8>",
-                "k_lpa_group<4>", "k_lpa_group<2>", "k_lpa_group<1>")
+                "k_lpa_group<4>", "k_lpa_group<2>", "k_lpa_group<1>", "refresh")
 
 
 class LpaStats(ctypes.Structure):

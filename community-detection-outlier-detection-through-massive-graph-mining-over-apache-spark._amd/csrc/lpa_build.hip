@@ -103,6 +103,30 @@ __global__ void k_keys_to_col(const u64* __restrict__ keys, int64_t n, int32_t* 
     col[j] = (int32_t)(u32)keys[j];
 }
 
+// CSC keys: (column << 32 | position), generated in position order so a stable
+// sort on the column bits alone leaves positions ascending within a column
+__global__ void k_csc_keys(const int32_t* __restrict__ col, int64_t n, u64* __restrict__ keys,
+                           int32_t* __restrict__ colcnt) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    keys[j] = ((u64)(u32)col[j] << 32) | (u64)j;
+    atomicAdd(&colcnt[col[j]], 1);
+  }
+}
+
+__global__ void k_keys_to_pos(const u64* __restrict__ keys, int64_t n, uint32_t* __restrict__ pos) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x)
+    pos[j] = (uint32_t)keys[j];
+}
+
+__global__ void k_gather_al(const int32_t* __restrict__ col, int64_t n, const int32_t* __restrict__ L,
+                            int32_t* __restrict__ al) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x)
+    al[j] = L[__builtin_nontemporal_load(col + j)];
+}
+
 // first index in the non-increasing deg_own[0, S) with deg <= t, for each threshold
 __global__ void k_bin_bounds(const int32_t* __restrict__ deg_own, int64_t S,
                              const int32_t* __restrict__ thr, int nthr, int64_t* __restrict__ out) {
@@ -150,6 +174,20 @@ __global__ void k_fill_segs(const int64_t* __restrict__ rp, const int32_t* __res
   }
 }
 
+__global__ void k_hub_item_counts(const int32_t* __restrict__ deg_own, int64_t n_hub,
+                                  int32_t* __restrict__ cnt) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_hub;
+       v += (int64_t)gridDim.x * blockDim.x)
+    cnt[v] = (deg_own[v] + kHubChunk - 1) / kHubChunk;  // list length <= distinct <= degree
+}
+
+__global__ void k_hub_item_fill(const int32_t* __restrict__ cnt, const int64_t* __restrict__ off,
+                                int64_t n_hub, u64* __restrict__ items) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_hub;
+       v += (int64_t)gridDim.x * blockDim.x)
+    for (int32_t k = 0; k < cnt[v]; ++k) items[off[v] + k] = ((u64)v << 32) | (u64)k;
+}
+
 __global__ void k_init_labels(const int32_t* __restrict__ old_of, int64_t n, int32_t* __restrict__ a,
                               int32_t* __restrict__ b) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -175,6 +213,14 @@ int init_labels(lpa_graph* g) {
                      g->vpad, g->lab[0], g->lab[1]);
   LPA_HIP(hipGetLastError());
   g->cur = 0;
+  return rebuild_arc_labels(g);
+}
+
+int rebuild_arc_labels(lpa_graph* g) {
+  if (g->arcs == 0) return LPA_OK;
+  hipLaunchKernelGGL(k_gather_al, dim3(grid_for(g->arcs)), dim3(256), 0, g->stream, g->col, g->arcs,
+                     g->lab[g->cur], g->al);
+  LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
 
@@ -185,7 +231,8 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   g->V = V;
   g->m = m;
   g->slice = ((int64_t)V + P - 1) / P;
-  if (g->slice == 0) g->slice = 1;
+  g->slice = (g->slice + 63) / 64 * 64;  // vector-aligned slices (k_diff reads int4)
+  if (g->slice == 0) g->slice = 64;
   g->vpad = g->slice * P;
   g->own_begin = (int64_t)r * g->slice;
   const int64_t S = g->slice;
@@ -287,8 +334,36 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
     hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col);
     LPA_HIP(hipGetLastError());
+    // CSC position index over this rank's arcs (for the replicated-label refresh)
+    if (arcs >= (int64_t)UINT32_MAX) {
+      set_error("%lld arcs on one rank exceed the 32-bit position index", (long long)arcs);
+      return LPA_EINVAL;
+    }
+    int32_t* colcnt = nullptr;
+    LPA_HIP(hipMalloc((void**)&colcnt, sizeof(int32_t) * g->vpad));
+    LPA_HIP(hipMemsetAsync(colcnt, 0, sizeof(int32_t) * g->vpad, s));
+    hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(arcs)), dim3(256), 0, s, g->col, arcs, keys, colcnt);
+    LPA_HIP(hipGetLastError());
+    int cs[8], ncs = 0;
+    for (int b = 0; b < bits_for((uint64_t)(g->vpad - 1)); b += 8) cs[ncs++] = 32 + b;
+    LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, cs, ncs, s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
+    LPA_TRY(exclusive_scan_i32_i64(colcnt, g->cptr, g->vpad, s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t) * arcs));
+    hipLaunchKernelGGL(k_keys_to_pos, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->cpos);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipFree(colcnt));
     LPA_HIP(hipFree(keys));
+  } else {
+    LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
+    LPA_HIP(hipMemsetAsync(g->cptr, 0, sizeof(int64_t) * (g->vpad + 1), s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t)));
   }
+  LPA_TRY(dev_alloc(g, (void**)&g->al, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
+  g->n_chunk_cap = arcs / kChunkPos + g->vpad + 1;
+  LPA_TRY(dev_alloc(g, (void**)&g->chunks, sizeof(u64) * g->n_chunk_cap));
+  LPA_TRY(dev_alloc(g, (void**)&g->counters, sizeof(unsigned long long) * 4));
+  LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 4, s));
 
   // ---- 4. degree bins (contiguous slot ranges) ----
   {
@@ -347,6 +422,38 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
       LPA_TRY(dev_alloc(g, (void**)&g->gcnt, sizeof(int32_t) * g->n_hub));
       LPA_HIP(hipMemsetAsync(g->gtab, 0, sizeof(u64) * tot, s));
       LPA_HIP(hipMemsetAsync(g->gcnt, 0, sizeof(int32_t) * g->n_hub, s));
+      LPA_TRY(dev_alloc(g, (void**)&g->hub_best, sizeof(u64) * g->n_hub));
+      LPA_HIP(hipMemsetAsync(g->hub_best, 0, sizeof(u64) * g->n_hub, s));
+      // hub-final work items: one per kHubChunk possible list entries of a hub
+      int32_t* icnt = nullptr;
+      int64_t* ioff = nullptr;
+      LPA_HIP(hipMalloc((void**)&icnt, sizeof(int32_t) * g->n_hub));
+      LPA_HIP(hipMalloc((void**)&ioff, sizeof(int64_t) * (g->n_hub + 1)));
+      hipLaunchKernelGGL(k_hub_item_counts, dim3(grid_for(g->n_hub)), dim3(256), 0, s, deg_own,
+                         g->n_hub, icnt);
+      LPA_HIP(hipGetLastError());
+      LPA_TRY(exclusive_scan_i32_i64(icnt, ioff, g->n_hub, s));
+      LPA_HIP(hipMemcpyAsync(&g->n_hub_items, ioff + g->n_hub, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      LPA_HIP(hipStreamSynchronize(s));
+      LPA_TRY(dev_alloc(g, (void**)&g->hub_items, sizeof(u64) * g->n_hub_items));
+      hipLaunchKernelGGL(k_hub_item_fill, dim3(grid_for(g->n_hub)), dim3(256), 0, s, icnt, ioff,
+                         g->n_hub, g->hub_items);
+      LPA_HIP(hipGetLastError());
+      LPA_HIP(hipFree(icnt));
+      LPA_HIP(hipFree(ioff));
+      // hub segments: staging for their tallies, per-hub segment ranges
+      LPA_TRY(dev_alloc(g, (void**)&g->hub_seg_off, sizeof(int64_t) * (g->n_hub + 1)));
+      LPA_HIP(hipMemcpyAsync(g->hub_seg_off, seg_off, sizeof(int64_t) * (g->n_hub + 1),
+                             hipMemcpyDeviceToDevice, s));
+      LPA_HIP(hipMemcpyAsync(&g->n_hub_segs, seg_off + g->n_hub, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      int64_t hub_arcs = 0;
+      LPA_HIP(hipMemcpyAsync(&hub_arcs, g->rp + g->n_hub, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      LPA_HIP(hipStreamSynchronize(s));
+      LPA_TRY(dev_alloc(g, (void**)&g->stage, sizeof(u64) * hub_arcs));
+      LPA_TRY(dev_alloc(g, (void**)&g->seg_wcnt, sizeof(int32_t) * 4 * g->n_hub_segs));
+      LPA_TRY(dev_alloc(g, (void**)&g->hub_done, sizeof(int32_t) * g->n_hub));
+      LPA_HIP(hipMemsetAsync(g->seg_wcnt, 0, sizeof(int32_t) * 4 * g->n_hub_segs, s));
+      LPA_HIP(hipMemsetAsync(g->hub_done, 0, sizeof(int32_t) * g->n_hub, s));
     }
     LPA_HIP(hipFree(nseg));
     LPA_HIP(hipFree(hubcap));

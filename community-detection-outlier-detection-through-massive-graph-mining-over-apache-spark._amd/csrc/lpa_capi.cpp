@@ -49,7 +49,9 @@ void destroy(lpa_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   void* bufs[] = {g->rp,   g->col,   g->new_of, g->old_of, g->deg,   g->lab[0], g->lab[1],
-                  g->segs, g->hub_off, g->gtab, g->glist,  g->gcnt, g->e_src,  g->e_dst};
+                  g->segs, g->hub_off, g->gtab, g->glist,  g->gcnt, g->e_src,  g->e_dst,
+                  g->al,   g->cptr,  g->cpos,   g->chunks, g->counters, g->hub_best, g->hub_items,
+                  g->hub_seg_off, g->hub_done, g->stage, g->seg_wcnt};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
@@ -205,6 +207,7 @@ int lpa_exchange_put(lpa_graph* g, const int32_t* full_in) {
   LPA_HIP(hipSetDevice(g->device));
   LPA_HIP(hipMemcpyAsync(g->lab[g->cur], full_in, sizeof(int32_t) * g->vpad, hipMemcpyHostToDevice,
                          g->stream));
+  LPA_TRY(rebuild_arc_labels(g));
   LPA_HIP(hipStreamSynchronize(g->stream));
   return LPA_OK;
 }

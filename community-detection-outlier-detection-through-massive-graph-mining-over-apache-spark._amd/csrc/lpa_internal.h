@@ -26,6 +26,11 @@ constexpr int kWaveCap = 1024;        // per-wave LDS table entries (>= 2 * kWav
 constexpr int kSegArcs = 2048;        // arcs per block segment (hub path)
 constexpr int kSegCap = 4096;         // per-block LDS table entries (>= 2 * kSegArcs)
 constexpr int kBinEvents = LPA_NKERNELS + 2;  // event marks per timed superstep
+constexpr int kHubChunk = 2048;       // global-list entries per hub-final work item
+constexpr int kChunkPos = 256;        // arc positions per scatter chunk of a changed vertex
+// replicated-label refresh: scatter the changed vertices' labels while they touch at
+// most this fraction of the arcs, otherwise rebuild al[] with one gather pass
+constexpr double kRebuildFrac = 0.25;
 
 struct Segment {
   int64_t begin;  // first arc (local CSR index)
@@ -98,6 +103,24 @@ struct lpa_graph {
   lpa::u64* gtab = nullptr;       // global hash tables
   int32_t* glist = nullptr;       // touched-slot lists
   int32_t* gcnt = nullptr;        // [n_hub] list lengths
+  lpa::u64* hub_best = nullptr;   // [n_hub] reduced tally word
+  lpa::u64* hub_items = nullptr;  // hub-final work items (hub << 32 | chunk)
+  int64_t n_hub_items = 0;
+  int64_t n_hub_segs = 0;         // hub segments are segs[0, n_hub_segs)
+  int64_t* hub_seg_off = nullptr; // [n_hub + 1] first segment of each hub
+  int32_t* hub_done = nullptr;    // [n_hub] combined in LDS this superstep
+  lpa::u64* stage = nullptr;      // [hub arcs] staged segment tally words
+  int32_t* seg_wcnt = nullptr;    // [n_hub_segs * 4] staged words per segment wave
+
+  // replicated neighbour labels (GraphX ReplicatedVertexView analogue):
+  // al[i] = L_cur[col[i]]; kept current by scatter (few changes) or rebuild
+  int32_t* al = nullptr;        // [arcs]
+  int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
+  uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])
+  // per-superstep change bookkeeping (device)
+  int64_t n_chunk_cap = 0;
+  lpa::u64* chunks = nullptr;   // changed-vertex position chunks: (u << 32 | chunk index)
+  unsigned long long* counters = nullptr;  // [0] chunk count, [1] dirty arcs, [2] changed vertices
 
   // original edge list kept for the outlier stage (device, dense ids)
   int32_t* e_src = nullptr;
@@ -128,6 +151,7 @@ int bits_for(uint64_t maxval);  // bits needed to represent maxval (0 -> 0)
 int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
                 uint32_t flags);
 int init_labels(lpa_graph* g);
+int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
 
 // iteration (lpa_iter.hip)
 int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st);

@@ -4,29 +4,41 @@
 //
 // For every owned vertex v with deg(v) > 0:
 //     L_next[v] = min{ l : cnt_v(l) = max_l' cnt_v(l') },  cnt_v(l) = #{arcs v->u : L_cur[u] = l}
-// Vertices are degree-sorted, so each bin below is one contiguous slot range and
-// every wave sees rows of near-equal length (no intra-wave imbalance).
+//
+// Data flow of a superstep (one handle = one rank's slice of the degree-sorted CSR):
+//   1. tally    every arc's vote comes from al[i] = L_cur[col[i]], the replicated
+//               neighbour label (GraphX ReplicatedVertexView: edge partitions hold
+//               copies of the endpoint attributes).  al[] is STREAMED (coalesced,
+//               non-temporal), so the dense superstep has no random gathers.
+//   2. exchange (P > 1) RCCL allgather of the owned label slices.
+//   3. refresh  diff L_next vs L_cur over all vertex slots; the changed vertices'
+//               new labels are scattered into al[] through the CSC position index
+//               (cptr/cpos) while they touch <= kRebuildFrac of the arcs, otherwise
+//               al[] is rebuilt with one gather pass al[i] = L_next[col[i]].
+//   Every superstep tallies every arc of every vertex; the refresh only keeps the
+//   replica exact, so labels are bit-identical to the plain gather formulation.
 //
 // A vote tally is packed into one 64-bit word  (count << 32) | ~label : the
 // maximum word is the highest count and, among equal counts, the smallest label,
 // so "mode with smallest-label tie-break" is a plain u64 max-reduction; an empty
-// slot is 0 (label 0xFFFFFFFF never occurs).
+// slot is 0 (label 0xFFFFFFFF never occurs; it also marks an empty lane below).
 //
-//   bin g1   deg == 1       thread per vertex: the neighbour's label
-//   bin g2   deg == 2       min of the two labels (1-1 tie or equal)
-//   bin g4/8/16 deg <= G    G lanes per vertex, ballot "peel": each round takes the
-//                           group's first unresolved label, counts its lanes with one
-//                           64-bit ballot, retires them (rounds = distinct labels)
-//   bin wave 16 < deg <= 512   one wave per vertex, per-wave LDS hash (64-bit CAS/add),
-//                           wave-level peel pre-aggregates repeated labels so converged
-//                           neighbourhoods cost one LDS atomic per 64 arcs
-//   bin seg  deg > 512      one 256-thread block per <= 2048-arc segment, block LDS hash;
-//                           single-segment rows finish in-block, longer rows merge their
-//                           segment tallies into a per-vertex global hash (64-bit device
-//                           atomics) that k_lpa_hub_final reduces
-// Tables keep a touched-slot list, so finishing a vertex costs O(distinct labels),
-// not O(table size).  Column indices are streamed with non-temporal loads (read
-// once per superstep) so they do not evict the label vector from L2 / MALL.
+// Degree bins (vertices are degree-sorted, so each bin is a contiguous slot range
+// and the rows a wave sees have near-equal length):
+//   g1   deg == 1       thread per vertex: the neighbour's label
+//   g2   deg == 2       min of the two labels (1-1 tie or equal)
+//   g4/8/16 deg <= G    G lanes per vertex, ballot "peel": each round takes the
+//                       group's first unresolved label, counts its lanes with one
+//                       64-bit ballot, retires them (rounds = distinct labels)
+//   wave 16 < deg <= 512   one wave per vertex, per-wave LDS hash (64-bit CAS/add);
+//                       a wave-level peel pre-aggregates repeated labels so a
+//                       converged neighbourhood costs one LDS atomic per 64 arcs
+//   seg  deg > 512      one 256-thread block per <= 2048-arc segment, block LDS hash;
+//                       single-segment rows finish in-block, longer rows merge their
+//                       segment tallies into a per-vertex global hash (batched 64-bit
+//                       device atomics) that k_lpa_hub_final reduces in 2048-entry
+//                       chunks (so one giant hub is spread over many blocks)
+// Tables keep a touched-slot list: finishing a vertex costs O(distinct labels).
 #include <string.h>
 
 #include "lpa_internal.h"
@@ -35,12 +47,20 @@ namespace lpa {
 
 namespace {
 
-constexpr int kPeel = 2;  // wave-level pre-aggregation rounds per 64-arc chunk
-constexpr int kUnroll = 4;  // 64-arc chunks in flight per wave
-static_assert(kSegArcs % (256 * kUnroll) == 0, "each wave of a segment block must own kSegArcs/4 arcs");
+// Diagnostic ablations (separate builds only, `make diag`; never in liblpa_hip.so):
+//   1 = stream the labels but skip the tally, 2 = skip the hub global merge,
+//   3 = peel only (no LDS hash of the residual votes)
+#ifndef LPA_DIAG
+#define LPA_DIAG 0
+#endif
 
-__device__ __forceinline__ int32_t ld_stream(const int32_t* p) {
-  return __builtin_nontemporal_load(p);
+constexpr int kChunks = 8;    // 64-arc chunks per wave: a wave-bin row / a quarter segment
+constexpr u32 kNone = 0xFFFFFFFFu;  // empty lane
+static_assert(kSegArcs == 4 * 64 * kChunks, "a segment block's 4 waves own 64*kChunks arcs each");
+static_assert(kWaveMaxDeg == 64 * kChunks, "a wave-bin row fits one batch of chunks");
+
+__device__ __forceinline__ u32 ld_stream(const int32_t* p) {
+  return (u32)__builtin_nontemporal_load(p);
 }
 
 __device__ __forceinline__ u64 tally(u32 cnt, u32 label) {
@@ -59,6 +79,8 @@ __device__ __forceinline__ u32 hash_slot(u32 label, int shift) {
   return (label * 0x9E3779B1u) >> shift;
 }
 
+__device__ __forceinline__ int ceil_log2(u32 x) { return x <= 1 ? 0 : 32 - __clz(x - 1); }
+
 // Insert `cnt` votes for `label` into an LDS open-addressing table of (mask+1)
 // slots.  Returns the slot index when this call claimed an empty slot, else -1.
 __device__ __forceinline__ int lds_insert(u64* tab, int shift, u32 mask, u32 label, u32 cnt) {
@@ -75,56 +97,155 @@ __device__ __forceinline__ int lds_insert(u64* tab, int shift, u32 mask, u32 lab
   }
 }
 
-// Global (HBM) variant for hub vertices; claimed slots are appended to `list`.
-__device__ __forceinline__ void global_insert(u64* tab, int shift, u32 mask, u64 word,
-                                              int32_t* list, int32_t* count) {
+// Continue a global-table insert whose first probe at slot h returned `old`;
+// returns the claimed slot or -1 (merged into an existing key).
+__device__ __forceinline__ int global_resolve(u64* tab, u32 mask, u64 word, u32 h, u64 old) {
   const u32 key = (u32)word;
   const u64 add = word & 0xFFFFFFFF00000000ull;
-  u32 h = hash_slot(~key, shift);
   while (true) {
-    u64 old = atomicCAS(&tab[h], 0ull, word);
-    if (old == 0ull) {
-      int p = atomicAdd(count, 1);
-      list[p] = (int32_t)h;
-      return;
-    }
+    if (old == 0ull) return (int)h;
     if ((u32)old == key) {
       atomicAdd(&tab[h], add);
-      return;
+      return -1;
     }
     h = (h + 1u) & mask;
+    old = atomicCAS(&tab[h], 0ull, word);
   }
 }
 
-__device__ __forceinline__ int ceil_log2(u32 x) { return x <= 1 ? 0 : 32 - __clz(x - 1); }
+// Continue an LDS insert of `word` whose probe at slot h hit another key.
+__device__ __forceinline__ int lds_probe(u64* tab, u32 mask, u64 word, u32 h) {
+  const u32 key = (u32)word;
+  while (true) {
+    h = (h + 1u) & mask;
+    const u64 old = atomicCAS(&tab[h], 0ull, word);
+    if (old == 0ull) return (int)h;
+    if ((u32)old == key) {
+      atomicAdd(&tab[h], word & 0xFFFFFFFF00000000ull);
+      return -1;
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
-// Process one 64-arc chunk held in registers (lab valid where `valid`) against
-// a wave-owned list: peel up to kPeel repeated labels with ballots, then insert
-// the remaining lanes individually.  Claimed slots appended to `lst` (wave-local
-// counter `cnt`, kept uniform).
+// Tally of a batch of up to NC 64-arc chunks held in registers (kNone = empty
+// lane; chunks >= nch, a uniform bound, are skipped).
+//   peel_batch   (no LDS) the first active label of the batch and all its copies
+//                are counted with one ballot per chunk and retired; repeated while
+//                a round retires >= 2 lanes (a repeated label), up to kPeelMax.
+//                Peel group p's tally word is left in lane p; pbest (uniform) is
+//                their maximum.  A converged neighbourhood is usually resolved
+//                here completely (nact == 0) and then needs no LDS at all.
+//   hash_batch   the peel groups (one lane each) and every remaining lane go into
+//                a wave-owned LDS open-addressing table: all first probes issued
+//                back to back, then resolved; claimed slots appended to `lst`.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void tally_chunk(u64* tab, uint16_t* lst, int& cnt, int shift,
-                                            u32 mask, u32 lab, bool valid, int lane, u64 lt) {
-  u64 act = __ballot(valid);
+constexpr int kPeelMax = 8;
+
+template <int NC>
+struct Batch {
+  u64 act[NC];
+  int nact;
+  u64 pword;   // lane p: tally word of peel group p
+  int npeel;   // uniform
+  u64 pbest;   // uniform
+};
+
+template <int NC>
+__device__ __forceinline__ void peel_batch(Batch<NC>& bt, const u32 (&lab)[NC], int nch, int lane) {
+  bt.nact = 0;
 #pragma unroll
-  for (int p = 0; p < kPeel; ++p) {
-    if (act == 0ull) break;
-    const int lead = __ffsll((unsigned long long)act) - 1;
-    const u32 x = (u32)__builtin_amdgcn_readlane((int)lab, lead);
-    const u64 mm = __ballot(lab == x) & act;
-    int slot = -1;
-    if (lane == lead) slot = lds_insert(tab, shift, mask, x, (u32)__popcll(mm));
-    const u64 cm = __ballot(slot >= 0);
-    if (slot >= 0) lst[cnt] = (uint16_t)slot;
-    cnt += cm ? 1 : 0;
-    act &= ~mm;
+  for (int u = 0; u < NC; ++u) {
+    bt.act[u] = u < nch ? __ballot(lab[u] != kNone) : 0ull;
+    bt.nact += __popcll(bt.act[u]);
   }
-  int slot = -1;
-  if ((act >> lane) & 1ull) slot = lds_insert(tab, shift, mask, lab, 1u);
-  const u64 cm = __ballot(slot >= 0);
-  if (slot >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)slot;
-  cnt += __popcll(cm);
+  bt.pword = 0ull;
+  bt.npeel = 0;
+  bt.pbest = 0ull;
+#pragma unroll
+  for (int p = 0; p < kPeelMax; ++p) {
+    if (bt.nact == 0) break;
+    u32 x = 0u;
+    bool found = false;
+#pragma unroll
+    for (int u = 0; u < NC; ++u) {
+      if (!found && bt.act[u] != 0ull) {
+        x = (u32)__builtin_amdgcn_readlane((int)lab[u], __ffsll((unsigned long long)bt.act[u]) - 1);
+        found = true;
+      }
+    }
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < NC; ++u) {
+      if (u < nch) {
+        const u64 mm = __ballot(lab[u] == x) & bt.act[u];
+        bt.act[u] &= ~mm;
+        c += __popcll(mm);
+      }
+    }
+    bt.nact -= c;
+    const u64 word = tally((u32)c, x);
+    if (lane == p) bt.pword = word;
+    bt.pbest = umax64(bt.pbest, word);
+    bt.npeel = p + 1;
+    if (c < 2) break;
+  }
+}
+
+template <int NC>
+__device__ __forceinline__ void hash_batch(u64* tab, uint16_t* lst, int& cnt, int shift, u32 mask,
+                                           const Batch<NC>& bt, const u32 (&lab)[NC], int nch,
+                                           int lane, u64 lt) {
+  int pslot = -1;
+  if (lane < bt.npeel) pslot = lds_insert(tab, shift, mask, ~(u32)bt.pword, (u32)(bt.pword >> 32));
+  u64 old[NC];
+  u32 hh[NC];
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    old[u] = 0ull;
+    hh[u] = 0u;
+    if (u < nch && ((bt.act[u] >> lane) & 1ull)) {
+      hh[u] = hash_slot(lab[u], shift);
+      old[u] = atomicCAS(&tab[hh[u]], 0ull, (1ull << 32) | (u64)(u32)(~lab[u]));
+    }
+  }
+  int slot[NC];
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    slot[u] = -1;
+    if (u < nch && ((bt.act[u] >> lane) & 1ull)) {
+      const u64 word = (1ull << 32) | (u64)(u32)(~lab[u]);
+      if (old[u] == 0ull) {
+        slot[u] = (int)hh[u];
+      } else if ((u32)old[u] == (u32)word) {
+        atomicAdd(&tab[hh[u]], 1ull << 32);
+      } else {
+        slot[u] = lds_probe(tab, mask, word, hh[u]);
+      }
+    }
+  }
+  {
+    const u64 cm = __ballot(pslot >= 0);
+    if (pslot >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)pslot;
+    cnt += __popcll(cm);
+  }
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    if (u < nch) {
+      const u64 cm = __ballot(slot[u] >= 0);
+      if (slot[u] >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)slot[u];
+      cnt += __popcll(cm);
+    }
+  }
+}
+
+__device__ __forceinline__ void load_labels(u32 (&lab)[kChunks], const int32_t* __restrict__ al,
+                                            int64_t b, int64_t e, int lane) {
+#pragma unroll
+  for (int u = 0; u < kChunks; ++u) {
+    const int64_t i = b + u * 64 + lane;
+    lab[u] = i < e ? ld_stream(al + i) : kNone;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -132,8 +253,7 @@ __device__ __forceinline__ void tally_chunk(u64* tab, uint16_t* lst, int& cnt, i
 // ---------------------------------------------------------------------------
 template <int G>
 __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ rp,
-                                                   const int32_t* __restrict__ col,
-                                                   const int32_t* __restrict__ Lc,
+                                                   const int32_t* __restrict__ al,
                                                    int32_t* __restrict__ Ln, int64_t vbeg,
                                                    int64_t vend) {
   const int lane = threadIdx.x & 63;
@@ -146,8 +266,7 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
     b = rp[v];
     d = (int)(rp[v + 1] - b);
   }
-  const bool ok = j < d;
-  const u32 lab = ok ? (u32)Lc[ld_stream(col + b + j)] : 0u;
+  const u32 lab = j < d ? ld_stream(al + b + j) : kNone;
   if constexpr (G == 1) {
     if (live) Ln[v] = (int32_t)lab;
   } else if constexpr (G == 2) {
@@ -156,7 +275,7 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
   } else {
     const int gbase = lane & ~(G - 1);
     const u64 gm = (1ull << G) - 1ull;
-    u64 act = __ballot(ok);
+    u64 act = __ballot(lab != kNone);
     u64 best = 0ull;
     while (act) {
       const u64 my = (act >> gbase) & gm;
@@ -172,11 +291,12 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
 }
 
 // ---------------------------------------------------------------------------
-// bin wave: 16 < deg <= kWaveMaxDeg, one wave per vertex (grid-stride)
+// bin wave: 16 < deg <= kWaveMaxDeg (= 64 * kChunks), one wave per vertex,
+// grid-stride, software-pipelined: the next vertex's labels stream in while the
+// current one is tallied (row bounds two vertices ahead).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp,
-                                                  const int32_t* __restrict__ col,
-                                                  const int32_t* __restrict__ Lc,
+                                                  const int32_t* __restrict__ al,
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend) {
   __shared__ u64 tab_all[4][kWaveCap];
@@ -187,49 +307,85 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   uint16_t* lst = lst_all[w];
   for (int i = lane; i < kWaveCap; i += 64) tab[i] = 0ull;
   const u64 lt = (1ull << lane) - 1ull;
-  for (int64_t v = vbeg + (int64_t)blockIdx.x * 4 + w; v < vend; v += (int64_t)gridDim.x * 4) {
-    const int64_t b = rp[v], e = rp[v + 1];
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t v = vbeg + (int64_t)blockIdx.x * 4 + w;
+  if (v >= vend) return;  // no block-level barriers in this kernel
+  int64_t b = rp[v], e = rp[v + 1];
+  int64_t bn = 0, en = 0;
+  if (v + stride < vend) {
+    bn = rp[v + stride];
+    en = rp[v + stride + 1];
+  }
+  u32 lab[kChunks];
+  load_labels(lab, al, b, e, lane);
+  while (true) {
+    const int64_t vn = v + stride, vnn = vn + stride;
+    const bool has_next = vn < vend;
+    int64_t bnn = 0, enn = 0;
+    if (vnn < vend) {
+      bnn = rp[vnn];
+      enn = rp[vnn + 1];
+    }
+    u32 labn[kChunks];
+    if (has_next) {
+      load_labels(labn, al, bn, en, lane);
+    } else {
+#pragma unroll
+      for (int u = 0; u < kChunks; ++u) labn[u] = kNone;
+    }
     const int d = (int)(e - b);
     int lg = ceil_log2(2u * (u32)d);
     lg = lg < 6 ? 6 : lg;
     const u32 mask = (1u << lg) - 1u;
     const int shift = 32 - lg;
-    int cnt = 0;
-    for (int64_t base = b; base < e; base += 64 * kUnroll) {
-      int32_t c[kUnroll];
-      u32 lab[kUnroll];
+    const int nch = (d + 63) >> 6;
+#if LPA_DIAG == 1
+    {
+      u32 acc = 0;
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int64_t i = base + u * 64 + lane;
-        c[u] = i < e ? ld_stream(col + i) : -1;
+      for (int u = 0; u < kChunks; ++u) acc ^= lab[u];
+      if (acc == 0x9E3779B1u) Ln[0] = (int32_t)acc;
+    }
+#else
+    Batch<kChunks> bt;
+    peel_batch<kChunks>(bt, lab, nch, lane);
+    if (bt.nact == 0 || LPA_DIAG == 3) {
+      // every vote is in a peel group: the mode is their maximum, no LDS needed
+      if (lane == 0) Ln[v] = (int32_t)(~(u32)bt.pbest);
+    } else {
+      int cnt = 0;
+      hash_batch<kChunks>(tab, lst, cnt, shift, mask, bt, lab, nch, lane, lt);
+      u64 best = 0ull;
+      for (int i = lane; i < cnt; i += 64) {
+        const int s = lst[i];
+        best = umax64(best, tab[s]);
+        tab[s] = 0ull;
       }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) lab[u] = c[u] >= 0 ? (u32)Lc[c[u]] : 0u;
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u)
-        tally_chunk(tab, lst, cnt, shift, mask, lab[u], c[u] >= 0, lane, lt);
+      best = wave_max_u64(best);
+      if (lane == 0) Ln[v] = (int32_t)(~(u32)best);
     }
-    u64 best = 0ull;
-    for (int i = lane; i < cnt; i += 64) {
-      const int s = lst[i];
-      best = umax64(best, tab[s]);
-      tab[s] = 0ull;
-    }
-    best = wave_max_u64(best);
-    if (lane == 0) Ln[v] = (int32_t)(~(u32)best);
+#endif
+    if (!has_next) break;
+    v = vn;
+    b = bn;
+    e = en;
+    bn = bnn;
+    en = enn;
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u) lab[u] = labn[u];
   }
 }
 
 // ---------------------------------------------------------------------------
 // bin seg: deg > kWaveMaxDeg, one block per segment of <= kSegArcs arcs
+// (wave w owns arcs [w * 64 * kChunks, (w + 1) * 64 * kChunks) of the segment),
+// grid-stride over segments, software-pipelined one segment ahead.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_lpa_seg(const int32_t* __restrict__ col,
-                                                 const int32_t* __restrict__ Lc,
+__global__ __launch_bounds__(256) void k_lpa_seg(const int32_t* __restrict__ al,
                                                  int32_t* __restrict__ Ln,
                                                  const Segment* __restrict__ segs, int64_t nseg,
-                                                 u64* __restrict__ gtab, int32_t* __restrict__ glist,
-                                                 int32_t* __restrict__ gcnt,
-                                                 const int64_t* __restrict__ hub_off) {
+                                                 u64* __restrict__ stage,
+                                                 int32_t* __restrict__ seg_wcnt) {
   __shared__ u64 tab[kSegCap];
   __shared__ uint16_t lst_all[4][kSegArcs / 4];
   __shared__ u64 red[4];
@@ -239,28 +395,44 @@ __global__ __launch_bounds__(256) void k_lpa_seg(const int32_t* __restrict__ col
   for (int i = threadIdx.x; i < kSegCap; i += 256) tab[i] = 0ull;
   __syncthreads();
   const u64 lt = (1ull << lane) - 1ull;
-  for (int64_t si = blockIdx.x; si < nseg; si += gridDim.x) {
-    const Segment sg = segs[si];
+  int64_t si = blockIdx.x;
+  if (si >= nseg) return;  // uniform over the block
+  Segment sg = segs[si];
+  const int64_t woff = (int64_t)w * 64 * kChunks;
+  u32 lab[kChunks];
+  load_labels(lab, al, sg.begin + woff, sg.begin + sg.len, lane);
+  while (true) {
+    const int64_t sn = si + gridDim.x;
+    const bool has_next = sn < nseg;
+    Segment sgn = sg;
+    if (has_next) sgn = segs[sn];
+    u32 labn[kChunks];
+    if (has_next) {
+      load_labels(labn, al, sgn.begin + woff, sgn.begin + sgn.len, lane);
+    } else {
+#pragma unroll
+      for (int u = 0; u < kChunks; ++u) labn[u] = kNone;
+    }
     int lg = ceil_log2(2u * (u32)sg.len);
     lg = lg < 6 ? 6 : lg;
     const u32 mask = (1u << lg) - 1u;
     const int shift = 32 - lg;
-    const int64_t e = sg.begin + sg.len;
     int cnt = 0;
-    for (int64_t base = sg.begin + (int64_t)w * 64 * kUnroll; base < e; base += 256 * kUnroll) {
-      int32_t c[kUnroll];
-      u32 lab[kUnroll];
+#if LPA_DIAG == 1
+    {
+      u32 acc = 0;
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int64_t i = base + u * 64 + lane;
-        c[u] = i < e ? ld_stream(col + i) : -1;
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) lab[u] = c[u] >= 0 ? (u32)Lc[c[u]] : 0u;
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u)
-        tally_chunk(tab, lst, cnt, shift, mask, lab[u], c[u] >= 0, lane, lt);
+      for (int u = 0; u < kChunks; ++u) acc ^= lab[u];
+      if (acc == 0x9E3779B1u) Ln[0] = (int32_t)acc;
     }
+#else
+    {
+      Batch<kChunks> bt;
+      const int nch = (int)min((int64_t)kChunks, (sg.len - woff + 63) / 64);
+      peel_batch<kChunks>(bt, lab, nch > 0 ? nch : 0, lane);
+      if (LPA_DIAG != 3) hash_batch<kChunks>(tab, lst, cnt, shift, mask, bt, lab, nch > 0 ? nch : 0, lane, lt);
+    }
+#endif
     __syncthreads();  // all tallies of the segment are in `tab`
     if (sg.v >= 0) {
       u64 best = 0ull;
@@ -275,47 +447,344 @@ __global__ __launch_bounds__(256) void k_lpa_seg(const int32_t* __restrict__ col
       if (threadIdx.x == 0)
         Ln[sg.v] = (int32_t)(~(u32)umax64(umax64(red[0], red[1]), umax64(red[2], red[3])));
     } else {
-      const int64_t h = -(int64_t)sg.v - 1;
-      const int64_t off = hub_off[h];
-      const u32 cap = (u32)(hub_off[h + 1] - off);
-      const int gshift = 32 - ceil_log2(cap);
+      // hub segment: stage this wave's tallies with plain stores; k_hub_small /
+      // k_hub_merge combine the segments of the hub afterwards
+      u64* st = stage + sg.begin + woff;
       for (int i = lane; i < cnt; i += 64) {
-        const int s = lst[i];
-        const u64 word = tab[s];
-        tab[s] = 0ull;
-        global_insert(gtab + off, gshift, cap - 1u, word, glist + off, gcnt + h);
+        const int slt = lst[i];
+        st[i] = tab[slt];
+        tab[slt] = 0ull;
       }
+      if (lane == 0) seg_wcnt[si * 4 + w] = cnt;
     }
     __syncthreads();  // table slots cleared before the next segment
+    if (!has_next) break;
+    si = sn;
+    sg = sgn;
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u) lab[u] = labn[u];
   }
 }
 
-// reduce the global tallies of multi-segment (hub) vertices
-__global__ __launch_bounds__(256) void k_lpa_hub_final(u64* __restrict__ gtab,
-                                                       const int32_t* __restrict__ glist,
-                                                       int32_t* __restrict__ gcnt,
-                                                       const int64_t* __restrict__ hub_off,
-                                                       int32_t* __restrict__ Ln, int64_t n_hub) {
+// Hub vertices (rows split over several segments).  Segment tallies are staged
+// as tally words; per hub:
+//   k_hub_small  total staged words <= kSegCap/2: combine them in an LDS table,
+//                write the label, mark the hub done (every converged superstep)
+//   k_hub_merge  otherwise: merge each segment's words into the hub's global
+//                hash (first probes back to back, batched list appends)
+//   k_lpa_hub_final / k_lpa_hub_write: reduce the global tables in 2048-entry
+//                work items (a giant hub spreads over many blocks)
+constexpr int kUnitWin = 2048;  // hub segment-wave units combined per window in k_hub_small
+
+__global__ __launch_bounds__(256) void k_hub_small(const Segment* __restrict__ segs,
+                                                   const int64_t* __restrict__ hub_seg_off,
+                                                   const int32_t* __restrict__ seg_wcnt,
+                                                   const u64* __restrict__ stage, int64_t n_hub,
+                                                   int32_t* __restrict__ Ln,
+                                                   int32_t* __restrict__ done) {
+  __shared__ u64 tab[kSegCap];
+  __shared__ uint16_t lst[kSegCap / 2];
+  __shared__ int upre[kUnitWin + 1];  // window prefix of staged words per unit
+  __shared__ int lcount;
   __shared__ u64 red[4];
+  __shared__ int tred[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const u64 lt = (1ull << lane) - 1ull;
+  for (int i = threadIdx.x; i < kSegCap; i += 256) tab[i] = 0ull;
   for (int64_t h = blockIdx.x; h < n_hub; h += gridDim.x) {
-    const int64_t off = hub_off[h];
-    const int n = gcnt[h];
+    const int64_t s0 = hub_seg_off[h], s1 = hub_seg_off[h + 1];
+    const int nunits = (int)(s1 - s0) * 4;
+    const int32_t* wc = seg_wcnt + s0 * 4;
+    int t = 0;
+    for (int k = threadIdx.x; k < nunits; k += 256) t += wc[k];
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+    if (lane == 0) tred[w] = t;
+    if (threadIdx.x == 0) lcount = 0;
+    __syncthreads();
+    const int T = tred[0] + tred[1] + tred[2] + tred[3];
+    if (T > kSegCap / 2) {
+      if (threadIdx.x == 0) done[h] = 0;
+      __syncthreads();
+      continue;
+    }
+    int lg = ceil_log2(2u * (u32)(T > 0 ? T : 1));
+    lg = lg < 6 ? 6 : lg;
+    const u32 mask = (1u << lg) - 1u;
+    const int shift = 32 - lg;
+    for (int k0 = 0; k0 < nunits; k0 += kUnitWin) {
+      const int nu = min(kUnitWin, nunits - k0);
+      // exclusive prefix of the window's unit counts (thread-contiguous stripes)
+      const int per = (nu + 255) / 256;
+      const int j0 = min(nu, (int)threadIdx.x * per), j1 = min(nu, j0 + per);
+      int loc = 0;
+      for (int j = j0; j < j1; ++j) loc += wc[k0 + j];
+      int incl = loc;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+      }
+      if (lane == 63) tred[w] = incl;
+      __syncthreads();
+      int run = incl - loc;
+      for (int i = 0; i < w; ++i) run += tred[i];
+      for (int j = j0; j < j1; ++j) {
+        upre[j] = run;
+        run += wc[k0 + j];
+      }
+      if (threadIdx.x == 255) upre[nu] = run;
+      __syncthreads();
+      const int nw = upre[nu];
+      // one staged word per thread per round: find its unit by binary search
+      for (int q = threadIdx.x; q < nw; q += 256) {
+        int lo = 0, hi = nu - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (upre[mid] <= q) lo = mid; else hi = mid - 1;
+        }
+        const int k = k0 + lo;
+        const u64 word = stage[segs[s0 + k / 4].begin + (int64_t)(k % 4) * 64 * kChunks + (q - upre[lo])];
+        const int slot = lds_insert(tab, shift, mask, ~(u32)word, (u32)(word >> 32));
+        const u64 cm = __ballot(slot >= 0);
+        int basei = 0;
+        if (cm) {
+          const int first = __ffsll((unsigned long long)cm) - 1;
+          if (lane == first) basei = atomicAdd(&lcount, __popcll(cm));
+          basei = __builtin_amdgcn_readlane(basei, first);
+        }
+        if (slot >= 0) lst[basei + __popcll(cm & lt)] = (uint16_t)slot;
+      }
+      __syncthreads();
+    }
     u64 best = 0ull;
-    for (int i = threadIdx.x; i < n; i += 256) {
-      const int32_t s = glist[off + i];
-      best = umax64(best, gtab[off + s]);
-      gtab[off + s] = 0ull;
+    for (int i = threadIdx.x; i < lcount; i += 256) {
+      const int slt = lst[i];
+      best = umax64(best, tab[slt]);
+      tab[slt] = 0ull;
     }
     best = wave_max_u64(best);
     if (lane == 0) red[w] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
       Ln[h] = (int32_t)(~(u32)umax64(umax64(red[0], red[1]), umax64(red[2], red[3])));
-      gcnt[h] = 0;
+      done[h] = 1;
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(256) void k_hub_merge(const Segment* __restrict__ segs,
+                                                   int64_t n_hub_segs,
+                                                   const int32_t* __restrict__ seg_wcnt,
+                                                   const u64* __restrict__ stage,
+                                                   const int32_t* __restrict__ done,
+                                                   u64* __restrict__ gtab, int32_t* __restrict__ glist,
+                                                   int32_t* __restrict__ gcnt,
+                                                   const int64_t* __restrict__ hub_off) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 lt = (1ull << lane) - 1ull;
+  for (int64_t si = blockIdx.x; si < n_hub_segs; si += gridDim.x) {
+    const Segment sg = segs[si];
+    const int64_t h = -(int64_t)sg.v - 1;
+    if (done[h]) continue;
+    const int cnt = seg_wcnt[si * 4 + w];
+    const u64* st = stage + sg.begin + (int64_t)w * 64 * kChunks;
+    const int64_t off = hub_off[h];
+    const u32 cap = (u32)(hub_off[h + 1] - off);
+    const int gshift = 32 - ceil_log2(cap);
+    u64* gt = gtab + off;
+    u64 word[kChunks], old[kChunks];
+    u32 hs[kChunks];
+#pragma unroll
+    for (int r = 0; r < kChunks; ++r) {
+      const int i = r * 64 + lane;
+      word[r] = i < cnt ? st[i] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kChunks; ++r) {
+      hs[r] = hash_slot(~(u32)word[r], gshift);
+      old[r] = 0ull;
+      if (LPA_DIAG != 2 && word[r] != 0ull) old[r] = atomicCAS(&gt[hs[r]], 0ull, word[r]);
+    }
+    int claimed[kChunks];
+    int total = 0;
+#pragma unroll
+    for (int r = 0; r < kChunks; ++r) {
+      claimed[r] = -1;
+      if (LPA_DIAG != 2 && word[r] != 0ull)
+        claimed[r] = global_resolve(gt, cap - 1u, word[r], hs[r], old[r]);
+      total += __popcll(__ballot(claimed[r] >= 0));
+    }
+    if (total > 0) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(gcnt + h, total);
+      base = __builtin_amdgcn_readlane(base, 0);
+#pragma unroll
+      for (int r = 0; r < kChunks; ++r) {
+        const u64 cm = __ballot(claimed[r] >= 0);
+        if (claimed[r] >= 0) glist[off + base + __popcll(cm & lt)] = claimed[r];
+        base += __popcll(cm);
+      }
+    }
+  }
+}
+
+// one work item per kHubChunk listed slots of a hub (items precomputed from the
+// table capacity; items past the hub's current list length exit at once)
+__global__ __launch_bounds__(256) void k_lpa_hub_final(u64* __restrict__ gtab,
+                                                       const int32_t* __restrict__ glist,
+                                                       const int32_t* __restrict__ gcnt,
+                                                       const int64_t* __restrict__ hub_off,
+                                                       const u64* __restrict__ items, int64_t n_items,
+                                                       u64* __restrict__ hbest) {
+  __shared__ u64 red[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const u64 item = items[it];
+    const int64_t h = (int64_t)(item >> 32);
+    const int begin = (int)(u32)item * kHubChunk;
+    const int n = gcnt[h];
+    if (begin >= n) continue;  // uniform over the block
+    const int end = min(n, begin + kHubChunk);
+    const int64_t off = hub_off[h];
+    u64 best = 0ull;
+    for (int i = begin + threadIdx.x; i < end; i += 256) {
+      const int32_t slt = glist[off + i];
+      best = umax64(best, gtab[off + slt]);
+      gtab[off + slt] = 0ull;
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) red[w] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      best = umax64(umax64(red[0], red[1]), umax64(red[2], red[3]));
+      atomicMax(&hbest[h], best);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_lpa_hub_write(u64* __restrict__ hbest, int32_t* __restrict__ gcnt,
+                                const int32_t* __restrict__ done, int32_t* __restrict__ Ln,
+                                int64_t n_hub) {
+  for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_hub;
+       h += (int64_t)gridDim.x * blockDim.x) {
+    if (!done[h]) Ln[h] = (int32_t)(~(u32)hbest[h]);
+    hbest[h] = 0ull;
+    gcnt[h] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// refresh of the replicated neighbour labels al[]
+// ---------------------------------------------------------------------------
+// changed vertices -> position chunks (u << 32 | k) and the dirty-arc count.
+// Each block scans one contiguous range of 4-slot quads (int4 loads; vpad is a
+// multiple of 64), queues its changed slots in LDS, then reserves its chunk slots
+// with ONE global atomic (a global counter hit by every wave serialises).
+constexpr int kDiffQuads = 2048;  // quads (8192 slots) per block
+__global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
+                                              const int4* __restrict__ Ln4, int64_t n4,
+                                              const int64_t* __restrict__ cptr,
+                                              u64* __restrict__ chunks,
+                                              unsigned long long* __restrict__ counters) {
+  __shared__ int32_t q_slot[kDiffQuads * 4];
+  __shared__ int32_t q_nch[kDiffQuads * 4];
+  __shared__ int qn;
+  __shared__ int wsum[4];
+  __shared__ unsigned long long base_s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) qn = 0;
+  __syncthreads();
+  const int64_t q0 = (int64_t)blockIdx.x * kDiffQuads;
+  const int64_t q1 = min(n4, q0 + kDiffQuads);
+  unsigned long long dirty = 0;
+  for (int64_t q = q0 + threadIdx.x; q < q1; q += 256) {
+    const int4 a = Lc4[q], b = Ln4[q];
+    const int chg = (a.x != b.x) | ((a.y != b.y) << 1) | ((a.z != b.z) << 2) | ((a.w != b.w) << 3);
+    if (chg) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((chg >> k) & 1) {
+          const int64_t u = q * 4 + k;
+          const int64_t cnt = cptr[u + 1] - cptr[u];
+          const int i = atomicAdd(&qn, 1);
+          q_slot[i] = (int32_t)(u - q0 * 4);
+          q_nch[i] = (int)((cnt + kChunkPos - 1) / kChunkPos);
+          dirty += (unsigned long long)cnt;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int n = qn;
+  if (n == 0) return;  // uniform
+  // exclusive scan of q_nch over the queue (serial per thread over its stripe)
+  const int per = (n + 255) / 256;
+  const int i0 = min(n, (int)threadIdx.x * per), i1 = min(n, i0 + per);
+  int loc = 0;
+  for (int i = i0; i < i1; ++i) loc += q_nch[i];
+  int incl = loc;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  for (int off = 32; off > 0; off >>= 1) dirty += __shfl_xor(dirty, off, 64);
+  __syncthreads();
+  int before = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i < w) before += wsum[i];
+    tot += wsum[i];
+  }
+  if (threadIdx.x == 0) base_s = atomicAdd(&counters[0], (unsigned long long)tot);
+  if (lane == 0 && dirty) atomicAdd(&counters[1], dirty);
+  __syncthreads();
+  u64 pos = base_s + (u64)(before + incl - loc);
+  for (int i = i0; i < i1; ++i) {
+    const u64 u = (u64)(q0 * 4 + q_slot[i]);
+    for (int c = 0; c < q_nch[i]; ++c) chunks[pos++] = (u << 32) | (u64)c;
+  }
+}
+
+__device__ __forceinline__ bool rebuild_wanted(const unsigned long long* counters, int64_t arcs) {
+  return (double)counters[1] > kRebuildFrac * (double)arcs;
+}
+
+// few changes: al[cpos[p]] = L_next[u] for the positions of each changed u
+__global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chunks,
+                                                    const unsigned long long* __restrict__ counters,
+                                                    const int64_t* __restrict__ cptr,
+                                                    const uint32_t* __restrict__ cpos,
+                                                    const int32_t* __restrict__ Ln,
+                                                    int32_t* __restrict__ al, int64_t arcs) {
+  if (rebuild_wanted(counters, arcs)) return;
+  const int64_t nchunks = (int64_t)counters[0];
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t c = wid; c < nchunks; c += nw) {
+    const u64 ch = chunks[c];
+    const int64_t u = (int64_t)(ch >> 32);
+    const int64_t b = cptr[u] + (int64_t)(u32)ch * kChunkPos;
+    const int64_t e = min(cptr[u + 1], b + kChunkPos);
+    const int32_t lab = Ln[u];
+    for (int64_t p = b + lane; p < e; p += 64) al[cpos[p]] = lab;
+  }
+}
+
+// many changes: al[i] = L_next[col[i]]
+__global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __restrict__ counters,
+                                                    const int32_t* __restrict__ col, int64_t arcs,
+                                                    const int32_t* __restrict__ Ln,
+                                                    int32_t* __restrict__ al) {
+  if (!rebuild_wanted(counters, arcs)) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < arcs;
+       i += (int64_t)gridDim.x * blockDim.x)
+    al[i] = Ln[__builtin_nontemporal_load(col + i)];
 }
 
 __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __restrict__ new_of,
@@ -330,9 +799,9 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
   return (unsigned)(want < cap ? want : cap);
 }
 
-// launch the bin kernels of one superstep; bin events optional
-int launch_superstep(lpa_graph* g, const int32_t* Lc, int32_t* Lown, hipEvent_t* bev) {
-  // bev marks: 0 start, k+1 after kernel k (0 seg, 1 hub_final, 2 wave, 3..7 g16..g1)
+// tally kernels of one superstep; bev marks: 0 start, k+1 after kernel k
+// (0 seg, 1 hub_final + hub_write, 2 wave, 3..7 g16..g1)
+int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
   hipStream_t s = g->stream;
   const int64_t* bb = g->bin_begin;
   auto mark = [&](int i) -> int {
@@ -341,14 +810,25 @@ int launch_superstep(lpa_graph* g, const int32_t* Lc, int32_t* Lown, hipEvent_t*
   };
   LPA_TRY(mark(0));
   if (g->n_segs > 0) {
-    hipLaunchKernelGGL(k_lpa_seg, dim3(cap_grid(g->n_segs, 1024)), dim3(256), 0, s, g->col, Lc,
-                       Lown, g->segs, g->n_segs, g->gtab, g->glist, g->gcnt, g->hub_off);
+    hipLaunchKernelGGL(k_lpa_seg, dim3(cap_grid(g->n_segs, 1024)), dim3(256), 0, s, g->al, Lown,
+                       g->segs, g->n_segs, g->stage, g->seg_wcnt);
     LPA_HIP(hipGetLastError());
   }
   LPA_TRY(mark(1));
   if (g->n_hub > 0) {
-    hipLaunchKernelGGL(k_lpa_hub_final, dim3(cap_grid(g->n_hub, 1024)), dim3(256), 0, s, g->gtab,
-                       g->glist, g->gcnt, g->hub_off, Lown, g->n_hub);
+    hipLaunchKernelGGL(k_hub_small, dim3(cap_grid(g->n_hub, 1024)), dim3(256), 0, s, g->segs,
+                       g->hub_seg_off, g->seg_wcnt, g->stage, g->n_hub, Lown, g->hub_done);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_merge, dim3(cap_grid(g->n_hub_segs, 2048)), dim3(256), 0, s, g->segs,
+                       g->n_hub_segs, g->seg_wcnt, g->stage, g->hub_done, g->gtab, g->glist,
+                       g->gcnt, g->hub_off);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_lpa_hub_final, dim3(cap_grid(g->n_hub_items, 2048)), dim3(256), 0, s,
+                       g->gtab, g->glist, g->gcnt, g->hub_off, g->hub_items, g->n_hub_items,
+                       g->hub_best);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_lpa_hub_write, dim3(cap_grid((g->n_hub + 255) / 256, 1024)), dim3(256), 0,
+                       s, g->hub_best, g->gcnt, g->hub_done, Lown, g->n_hub);
     LPA_HIP(hipGetLastError());
   }
   LPA_TRY(mark(2));
@@ -356,7 +836,7 @@ int launch_superstep(lpa_graph* g, const int32_t* Lc, int32_t* Lown, hipEvent_t*
     const int64_t n = bb[BIN_WAVE + 1] - bb[BIN_WAVE];
     if (n > 0) {
       hipLaunchKernelGGL(k_lpa_wave, dim3(cap_grid((n + 3) / 4, 4096)), dim3(256), 0, s, g->rp,
-                         g->col, Lc, Lown, bb[BIN_WAVE], bb[BIN_WAVE + 1]);
+                         g->al, Lown, bb[BIN_WAVE], bb[BIN_WAVE + 1]);
       LPA_HIP(hipGetLastError());
     }
   }
@@ -366,7 +846,7 @@ int launch_superstep(lpa_graph* g, const int32_t* Lc, int32_t* Lown, hipEvent_t*
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
     if (n > 0) {                                                                             \
       hipLaunchKernelGGL(k_lpa_group<G>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
-                         s, g->rp, g->col, Lc, Lown, bb[BIN], bb[BIN + 1]);                 \
+                         s, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                      \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(BIN + 2));                                                                  \
@@ -377,6 +857,24 @@ int launch_superstep(lpa_graph* g, const int32_t* Lc, int32_t* Lown, hipEvent_t*
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
 #undef LPA_GROUP_LAUNCH
+  return LPA_OK;
+}
+
+// refresh al[] for L_next (after the exchange, so every rank sees all changes)
+int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
+  if (g->arcs == 0) return LPA_OK;
+  hipStream_t s = g->stream;
+  LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 2, s));
+  hipLaunchKernelGGL(k_diff, dim3((unsigned)((g->vpad / 4 + kDiffQuads - 1) / kDiffQuads)), dim3(256),
+                     0, s, (const int4*)Lc, (const int4*)Ln, g->vpad / 4, g->cptr, g->chunks,
+                     g->counters);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, g->counters, g->cptr,
+                     g->cpos, Ln, g->al, g->arcs);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_al_rebuild, dim3(cap_grid((g->arcs + 255) / 256, 8192)), dim3(256), 0, s,
+                     g->counters, g->col, g->arcs, Ln, g->al);
+  LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
 
@@ -394,8 +892,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       if (!g->bin_ev[i]) LPA_HIP(hipEventCreate(&g->bin_ev[i]));
     LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS], s));
   }
-  // per timed superstep t, marks bin_ev[t*kBinEvents + i]: 0 start, k+1 after kernel k,
-  // LPA_NKERNELS+1 after the exchange
+  // per timed superstep t, marks bin_ev[t*kBinEvents + i]: 0 start, k+1 after
+  // tally kernel k (k < LPA_NKERNELS - 1), then after the exchange, after the refresh
   for (int32_t t = 0; t < n; ++t) {
     const int32_t* Lc = g->lab[g->cur];
     int32_t* Ln = g->lab[g->cur ^ 1];
@@ -403,7 +901,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     const bool tt = timed && t < nt;
     hipEvent_t* bev = tt ? &g->bin_ev[t * kBinEvents] : nullptr;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
-    LPA_TRY(launch_superstep(g, Lc, Lown, bev));
+    LPA_TRY(launch_tally(g, Lown, bev));
     if (g->nranks > 1 && g->comm) {
       ncclResult_t r = ncclAllGather(Lown, Ln, (size_t)g->slice, ncclInt32, g->comm, s);
       if (r != ncclSuccess) {
@@ -411,6 +909,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
         return LPA_ERCCL;
       }
     }
+    if (tt) LPA_HIP(hipEventRecord(bev[LPA_NKERNELS], s));
+    LPA_TRY(launch_refresh(g, Lc, Ln));
     if (tt) {
       LPA_HIP(hipEventRecord(bev[LPA_NKERNELS + 1], s));
       LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
@@ -426,12 +926,14 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       LPA_HIP(hipEventElapsedTime(&st->iter_ms[t], g->ev[2 * t], g->ev[2 * t + 1]));
       hipEvent_t* bev = &g->bin_ev[t * kBinEvents];
       float ms;
-      for (int k = 0; k < LPA_NKERNELS; ++k) {
+      for (int k = 0; k < LPA_NKERNELS - 1; ++k) {
         LPA_HIP(hipEventElapsedTime(&ms, bev[k], bev[k + 1]));
         st->kernel_ms[k] += ms;
       }
-      LPA_HIP(hipEventElapsedTime(&ms, bev[LPA_NKERNELS], bev[LPA_NKERNELS + 1]));
+      LPA_HIP(hipEventElapsedTime(&ms, bev[LPA_NKERNELS - 1], bev[LPA_NKERNELS]));
       st->exchange_ms += ms;
+      LPA_HIP(hipEventElapsedTime(&ms, bev[LPA_NKERNELS], bev[LPA_NKERNELS + 1]));
+      st->kernel_ms[LPA_NKERNELS - 1] += ms;
     }
     float tot;
     LPA_HIP(hipEventElapsedTime(&tot, g->ev[2 * LPA_STATS_MAX_ITERS], g->ev[2 * LPA_STATS_MAX_ITERS + 1]));

@@ -40,7 +40,7 @@ extern "C" {
 #define LPA_INPUT_DEVICE 0x1u /* src/dst are device pointers on `device`        */
 
 #define LPA_NBINS 8
-#define LPA_NKERNELS 8 /* timed kernels: 0 seg 1 hub_final 2 wave 3 g16 4 g8 5 g4 6 g2 7 g1 */
+#define LPA_NKERNELS 9 /* timed: 0 seg 1 hub_final 2 wave 3 g16 4 g8 5 g4 6 g2 7 g1 8 refresh */
 #define LPA_STATS_MAX_ITERS 64
 
 typedef struct lpa_graph lpa_graph;
