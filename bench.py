@@ -35,9 +35,9 @@ def kernel_bytes(info, name):
     (SURVEY.md §8(d) counts 8 B per arc for that formulation); per vertex it reads
     8 B of row offsets (seg: a 16 B segment descriptor per segment) and writes a
     4 B label."""
-    b = {"k_lpa_seg": "seg", "k_lpa_wave": "wave", "k_lpa_group<16>": "g16",
-         "k_lpa_group<8>": "g8", "k_lpa_group<4>": "g4", "k_lpa_group<2>": "g2",
-         "k_lpa_group<1>": "g1"}.get(name)
+    from graphframes_amd import _lib
+
+    b = _lib.KERNEL_BIN.get(name)
     if b is None:
         return None
     A = info["bin_arcs"][b]

@@ -367,15 +367,19 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
 
   // ---- 4. degree bins (contiguous slot ranges) ----
   {
-    const int32_t thr_h[8] = {kWaveMaxDeg, 16, 8, 4, 2, 1, 0, kSegArcs};
+    // thresholds: bin b+1 starts at the first vertex with deg <= kBinMaxDeg[b+1];
+    // the last entry finds the hubs (rows longer than one segment)
+    int32_t thr_h[LPA_NBINS];
+    for (int b = 1; b < LPA_NBINS; ++b) thr_h[b - 1] = kBinMaxDeg[b];
+    thr_h[LPA_NBINS - 1] = kSegArcs;
     int32_t* d_thr = nullptr;
     int64_t* d_bb = nullptr;
     LPA_HIP(hipMalloc((void**)&d_thr, sizeof(thr_h)));
-    LPA_HIP(hipMalloc((void**)&d_bb, sizeof(int64_t) * 8));
+    LPA_HIP(hipMalloc((void**)&d_bb, sizeof(int64_t) * LPA_NBINS));
     LPA_HIP(hipMemcpyAsync(d_thr, thr_h, sizeof(thr_h), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_bin_bounds, dim3(1), dim3(64), 0, s, deg_own, S, d_thr, 8, d_bb);
+    hipLaunchKernelGGL(k_bin_bounds, dim3(1), dim3(64), 0, s, deg_own, S, d_thr, LPA_NBINS, d_bb);
     LPA_HIP(hipGetLastError());
-    int64_t bb[8];
+    int64_t bb[LPA_NBINS];
     LPA_HIP(hipMemcpyAsync(bb, d_bb, sizeof(bb), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
     LPA_HIP(hipFree(d_thr));
@@ -383,7 +387,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     g->bin_begin[0] = 0;
     for (int b = 1; b < LPA_NBINS; ++b) g->bin_begin[b] = bb[b - 1];
     g->bin_begin[LPA_NBINS] = S;
-    g->n_hub = bb[7];
+    g->n_hub = bb[LPA_NBINS - 1];
     int64_t rpb[LPA_NBINS + 1];
     for (int b = 0; b <= LPA_NBINS; ++b)
       LPA_HIP(hipMemcpyAsync(&rpb[b], g->rp + g->bin_begin[b], sizeof(int64_t),

@@ -18,11 +18,16 @@ typedef uint32_t u32;
 // Degree bins (SURVEY.md §7 kernel inventory).  Vertices of a rank's slice are
 // sorted by degree (descending), so every bin is one contiguous range.
 // ---------------------------------------------------------------------------
-enum Bin { BIN_SEG = 0, BIN_WAVE = 1, BIN_G16 = 2, BIN_G8 = 3, BIN_G4 = 4, BIN_G2 = 5, BIN_G1 = 6,
-           BIN_ISO = 7 };
+//   seg  deg > 512          block per 2048-arc segment        (k_lpa_seg + hub kernels)
+//   w8/w4/w2  deg <= 512/256/128   wave per vertex, 8/4/2 chunks (k_lpa_wave<NC>)
+//   g64 .. g1 deg <= G          G lanes per vertex                (k_lpa_group<G>)
+enum Bin { BIN_SEG = 0, BIN_W8 = 1, BIN_W4 = 2, BIN_W2 = 3, BIN_G64 = 4, BIN_G32 = 5, BIN_G16 = 6,
+           BIN_G8 = 7, BIN_G4 = 8, BIN_G2 = 9, BIN_G1 = 10, BIN_ISO = 11 };
+static_assert(BIN_ISO + 1 == LPA_NBINS, "bin table");
+// upper degree bound of each bin (bin b holds bin_max[b+1] < deg <= bin_max[b])
+constexpr int kBinMaxDeg[LPA_NBINS] = {1 << 30, 512, 256, 128, 64, 32, 16, 8, 4, 2, 1, 0};
 
-constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 16 < deg <= 512
-constexpr int kWaveCap = 1024;        // per-wave LDS table entries (>= 2 * kWaveMaxDeg)
+constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 64 < deg <= 512
 constexpr int kSegArcs = 2048;        // arcs per block segment (hub path)
 constexpr int kSegCap = 4096;         // per-block LDS table entries (>= 2 * kSegArcs)
 constexpr int kBinEvents = LPA_NKERNELS + 2;  // event marks per timed superstep

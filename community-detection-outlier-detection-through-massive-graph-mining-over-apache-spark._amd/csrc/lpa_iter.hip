@@ -27,21 +27,35 @@
 // and the rows a wave sees have near-equal length):
 //   g1   deg == 1       thread per vertex: the neighbour's label
 //   g2   deg == 2       min of the two labels (1-1 tie or equal)
-//   g4/8/16 deg <= G    G lanes per vertex, ballot "peel": each round takes the
+//   g4 .. g64 deg <= G  G lanes per vertex, ballot "peel": each round takes the
 //                       group's first unresolved label, counts its lanes with one
 //                       64-bit ballot, retires them (rounds = distinct labels)
-//   wave 16 < deg <= 512   one wave per vertex, per-wave LDS hash (64-bit CAS/add);
-//                       a wave-level peel pre-aggregates repeated labels so a
-//                       converged neighbourhood costs one LDS atomic per 64 arcs
+//   w2/w4/w8 deg <= 64*NC  one wave per vertex, NC chunks: cross-chunk peel in
+//                       registers; a row the peel does not resolve completely goes
+//                       through a per-wave LDS hash (64-bit CAS/add)
 //   seg  deg > 512      one 256-thread block per <= 2048-arc segment, block LDS hash;
 //                       single-segment rows finish in-block, longer rows merge their
 //                       segment tallies into a per-vertex global hash (batched 64-bit
 //                       device atomics) that k_lpa_hub_final reduces in 2048-entry
 //                       chunks (so one giant hub is spread over many blocks)
 // Tables keep a touched-slot list: finishing a vertex costs O(distinct labels).
+#include <stdio.h>
 #include <string.h>
 
 #include "lpa_internal.h"
+
+// LPA_TRACE (diagnostic build only): synchronise and log after every kernel
+#ifdef LPA_TRACE
+#define LPA_TRACE_POINT(name)                                        \
+  do {                                                               \
+    hipError_t te_ = hipStreamSynchronize(s);                        \
+    fprintf(stderr, "[lpa-trace] %s done (%s)\n", name, hipGetErrorString(te_)); \
+  } while (0)
+#else
+#define LPA_TRACE_POINT(name) \
+  do {                        \
+  } while (0)
+#endif
 
 namespace lpa {
 
@@ -239,10 +253,11 @@ __device__ __forceinline__ void hash_batch(u64* tab, uint16_t* lst, int& cnt, in
   }
 }
 
-__device__ __forceinline__ void load_labels(u32 (&lab)[kChunks], const int32_t* __restrict__ al,
+template <int NC>
+__device__ __forceinline__ void load_labels(u32 (&lab)[NC], const int32_t* __restrict__ al,
                                             int64_t b, int64_t e, int lane) {
 #pragma unroll
-  for (int u = 0; u < kChunks; ++u) {
+  for (int u = 0; u < NC; ++u) {
     const int64_t i = b + u * 64 + lane;
     lab[u] = i < e ? ld_stream(al + i) : kNone;
   }
@@ -274,7 +289,7 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
     if (live && j == 0) Ln[v] = (int32_t)(lab < o ? lab : o);
   } else {
     const int gbase = lane & ~(G - 1);
-    const u64 gm = (1ull << G) - 1ull;
+    const u64 gm = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
     u64 act = __ballot(lab != kNone);
     u64 best = 0ull;
     while (act) {
@@ -291,21 +306,23 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
 }
 
 // ---------------------------------------------------------------------------
-// bin wave: 16 < deg <= kWaveMaxDeg (= 64 * kChunks), one wave per vertex,
-// grid-stride, software-pipelined: the next vertex's labels stream in while the
-// current one is tallied (row bounds two vertices ahead).
+// bins w2 / w4 / w8: 64 < deg <= 64 * NC, one wave per vertex, grid-stride,
+// software-pipelined: the next vertex's labels stream in while the current one is
+// tallied (row bounds two vertices ahead).  Per-wave LDS table of 2 * 64 * NC.
 // ---------------------------------------------------------------------------
+template <int NC>
 __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp,
                                                   const int32_t* __restrict__ al,
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend) {
-  __shared__ u64 tab_all[4][kWaveCap];
-  __shared__ uint16_t lst_all[4][kWaveCap];
+  constexpr int kCap = 2 * 64 * NC;
+  __shared__ u64 tab_all[4][kCap];
+  __shared__ uint16_t lst_all[4][64 * NC];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   u64* tab = tab_all[w];
   uint16_t* lst = lst_all[w];
-  for (int i = lane; i < kWaveCap; i += 64) tab[i] = 0ull;
+  for (int i = lane; i < kCap; i += 64) tab[i] = 0ull;
   const u64 lt = (1ull << lane) - 1ull;
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t v = vbeg + (int64_t)blockIdx.x * 4 + w;
@@ -316,8 +333,8 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
     bn = rp[v + stride];
     en = rp[v + stride + 1];
   }
-  u32 lab[kChunks];
-  load_labels(lab, al, b, e, lane);
+  u32 lab[NC];
+  load_labels<NC>(lab, al, b, e, lane);
   while (true) {
     const int64_t vn = v + stride, vnn = vn + stride;
     const bool has_next = vn < vend;
@@ -326,12 +343,12 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
       bnn = rp[vnn];
       enn = rp[vnn + 1];
     }
-    u32 labn[kChunks];
+    u32 labn[NC];
     if (has_next) {
-      load_labels(labn, al, bn, en, lane);
+      load_labels<NC>(labn, al, bn, en, lane);
     } else {
 #pragma unroll
-      for (int u = 0; u < kChunks; ++u) labn[u] = kNone;
+      for (int u = 0; u < NC; ++u) labn[u] = kNone;
     }
     const int d = (int)(e - b);
     int lg = ceil_log2(2u * (u32)d);
@@ -343,18 +360,18 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
     {
       u32 acc = 0;
 #pragma unroll
-      for (int u = 0; u < kChunks; ++u) acc ^= lab[u];
+      for (int u = 0; u < NC; ++u) acc ^= lab[u];
       if (acc == 0x9E3779B1u) Ln[0] = (int32_t)acc;
     }
 #else
-    Batch<kChunks> bt;
-    peel_batch<kChunks>(bt, lab, nch, lane);
+    Batch<NC> bt;
+    peel_batch<NC>(bt, lab, nch, lane);
     if (bt.nact == 0 || LPA_DIAG == 3) {
       // every vote is in a peel group: the mode is their maximum, no LDS needed
       if (lane == 0) Ln[v] = (int32_t)(~(u32)bt.pbest);
     } else {
       int cnt = 0;
-      hash_batch<kChunks>(tab, lst, cnt, shift, mask, bt, lab, nch, lane, lt);
+      hash_batch<NC>(tab, lst, cnt, shift, mask, bt, lab, nch, lane, lt);
       u64 best = 0ull;
       for (int i = lane; i < cnt; i += 64) {
         const int s = lst[i];
@@ -372,7 +389,7 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
     bn = bnn;
     en = enn;
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u) lab[u] = labn[u];
+    for (int u = 0; u < NC; ++u) lab[u] = labn[u];
   }
 }
 
@@ -400,7 +417,7 @@ __global__ __launch_bounds__(256) void k_lpa_seg(const int32_t* __restrict__ al,
   Segment sg = segs[si];
   const int64_t woff = (int64_t)w * 64 * kChunks;
   u32 lab[kChunks];
-  load_labels(lab, al, sg.begin + woff, sg.begin + sg.len, lane);
+  load_labels<kChunks>(lab, al, sg.begin + woff, sg.begin + sg.len, lane);
   while (true) {
     const int64_t sn = si + gridDim.x;
     const bool has_next = sn < nseg;
@@ -408,7 +425,7 @@ __global__ __launch_bounds__(256) void k_lpa_seg(const int32_t* __restrict__ al,
     if (has_next) sgn = segs[sn];
     u32 labn[kChunks];
     if (has_next) {
-      load_labels(labn, al, sgn.begin + woff, sgn.begin + sgn.len, lane);
+      load_labels<kChunks>(labn, al, sgn.begin + woff, sgn.begin + sgn.len, lane);
     } else {
 #pragma unroll
       for (int u = 0; u < kChunks; ++u) labn[u] = kNone;
@@ -487,7 +504,8 @@ __global__ __launch_bounds__(256) void k_hub_small(const Segment* __restrict__ s
   __shared__ int upre[kUnitWin + 1];  // window prefix of staged words per unit
   __shared__ int lcount;
   __shared__ u64 red[4];
-  __shared__ int tred[4];
+  __shared__ int tred[4];   // per-wave word totals of the hub
+  __shared__ int wpre[4];   // per-wave sums of a unit window
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const u64 lt = (1ull << lane) - 1ull;
   for (int i = threadIdx.x; i < kSegCap; i += 256) tab[i] = 0ull;
@@ -511,6 +529,19 @@ __global__ __launch_bounds__(256) void k_hub_small(const Segment* __restrict__ s
     lg = lg < 6 ? 6 : lg;
     const u32 mask = (1u << lg) - 1u;
     const int shift = 32 - lg;
+    if (T <= 4 * nunits) {
+      // few words per unit (a converged hub): one thread per unit
+      for (int k = threadIdx.x; k < nunits; k += 256) {
+        const int n = wc[k];
+        const u64* st = stage + segs[s0 + k / 4].begin + (int64_t)(k % 4) * 64 * kChunks;
+        for (int i = 0; i < n; ++i) {
+          const u64 word = st[i];
+          const int slot = lds_insert(tab, shift, mask, ~(u32)word, (u32)(word >> 32));
+          if (slot >= 0) lst[atomicAdd(&lcount, 1)] = (uint16_t)slot;
+        }
+      }
+      __syncthreads();  // all inserts and list appends done before the finalize
+    } else
     for (int k0 = 0; k0 < nunits; k0 += kUnitWin) {
       const int nu = min(kUnitWin, nunits - k0);
       // exclusive prefix of the window's unit counts (thread-contiguous stripes)
@@ -524,10 +555,10 @@ __global__ __launch_bounds__(256) void k_hub_small(const Segment* __restrict__ s
         const int o = __shfl_up(incl, off, 64);
         if (lane >= off) incl += o;
       }
-      if (lane == 63) tred[w] = incl;
+      if (lane == 63) wpre[w] = incl;
       __syncthreads();
       int run = incl - loc;
-      for (int i = 0; i < w; ++i) run += tred[i];
+      for (int i = 0; i < w; ++i) run += wpre[i];
       for (int j = j0; j < j1; ++j) {
         upre[j] = run;
         run += wc[k0 + j];
@@ -802,6 +833,7 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
 // tally kernels of one superstep; bev marks: 0 start, k+1 after kernel k
 // (0 seg, 1 hub_final + hub_write, 2 wave, 3..7 g16..g1)
 int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
+  // bev marks: 0 start, k+1 after kernel k (0 seg, 1 hub kernels, 2..11 bins w8..g1)
   hipStream_t s = g->stream;
   const int64_t* bb = g->bin_begin;
   auto mark = [&](int i) -> int {
@@ -813,34 +845,40 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
     hipLaunchKernelGGL(k_lpa_seg, dim3(cap_grid(g->n_segs, 1024)), dim3(256), 0, s, g->al, Lown,
                        g->segs, g->n_segs, g->stage, g->seg_wcnt);
     LPA_HIP(hipGetLastError());
+    LPA_TRACE_POINT("seg");
   }
   LPA_TRY(mark(1));
   if (g->n_hub > 0) {
     hipLaunchKernelGGL(k_hub_small, dim3(cap_grid(g->n_hub, 1024)), dim3(256), 0, s, g->segs,
                        g->hub_seg_off, g->seg_wcnt, g->stage, g->n_hub, Lown, g->hub_done);
     LPA_HIP(hipGetLastError());
+    LPA_TRACE_POINT("hub_small");
     hipLaunchKernelGGL(k_hub_merge, dim3(cap_grid(g->n_hub_segs, 2048)), dim3(256), 0, s, g->segs,
                        g->n_hub_segs, g->seg_wcnt, g->stage, g->hub_done, g->gtab, g->glist,
                        g->gcnt, g->hub_off);
     LPA_HIP(hipGetLastError());
+    LPA_TRACE_POINT("hub_merge");
     hipLaunchKernelGGL(k_lpa_hub_final, dim3(cap_grid(g->n_hub_items, 2048)), dim3(256), 0, s,
                        g->gtab, g->glist, g->gcnt, g->hub_off, g->hub_items, g->n_hub_items,
                        g->hub_best);
     LPA_HIP(hipGetLastError());
+    LPA_TRACE_POINT("hub_final");
     hipLaunchKernelGGL(k_lpa_hub_write, dim3(cap_grid((g->n_hub + 255) / 256, 1024)), dim3(256), 0,
                        s, g->hub_best, g->gcnt, g->hub_done, Lown, g->n_hub);
     LPA_HIP(hipGetLastError());
   }
   LPA_TRY(mark(2));
-  {
-    const int64_t n = bb[BIN_WAVE + 1] - bb[BIN_WAVE];
-    if (n > 0) {
-      hipLaunchKernelGGL(k_lpa_wave, dim3(cap_grid((n + 3) / 4, 4096)), dim3(256), 0, s, g->rp,
-                         g->al, Lown, bb[BIN_WAVE], bb[BIN_WAVE + 1]);
-      LPA_HIP(hipGetLastError());
-    }
+#define LPA_WAVE_LAUNCH(BIN, NC)                                                              \
+  {                                                                                           \
+    const int64_t n = bb[BIN + 1] - bb[BIN];                                                  \
+    if (n > 0) {                                                                              \
+      hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, s,   \
+                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                          \
+      LPA_HIP(hipGetLastError());                                                             \
+      LPA_TRACE_POINT("wave" #NC);                                                            \
+    }                                                                                         \
+    LPA_TRY(mark(BIN + 2));                                                                   \
   }
-  LPA_TRY(mark(3));
 #define LPA_GROUP_LAUNCH(BIN, G)                                                             \
   {                                                                                          \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
@@ -848,15 +886,22 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
       hipLaunchKernelGGL(k_lpa_group<G>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
                          s, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                      \
       LPA_HIP(hipGetLastError());                                                            \
+      LPA_TRACE_POINT("group" #G);                                                           \
     }                                                                                        \
     LPA_TRY(mark(BIN + 2));                                                                  \
   }
+  LPA_WAVE_LAUNCH(BIN_W8, 8)
+  LPA_WAVE_LAUNCH(BIN_W4, 4)
+  LPA_WAVE_LAUNCH(BIN_W2, 2)
+  LPA_GROUP_LAUNCH(BIN_G64, 64)
+  LPA_GROUP_LAUNCH(BIN_G32, 32)
   LPA_GROUP_LAUNCH(BIN_G16, 16)
   LPA_GROUP_LAUNCH(BIN_G8, 8)
   LPA_GROUP_LAUNCH(BIN_G4, 4)
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
 #undef LPA_GROUP_LAUNCH
+#undef LPA_WAVE_LAUNCH
   return LPA_OK;
 }
 
@@ -869,9 +914,11 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
                      0, s, (const int4*)Lc, (const int4*)Ln, g->vpad / 4, g->cptr, g->chunks,
                      g->counters);
   LPA_HIP(hipGetLastError());
+  LPA_TRACE_POINT("diff");
   hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, g->counters, g->cptr,
                      g->cpos, Ln, g->al, g->arcs);
   LPA_HIP(hipGetLastError());
+  LPA_TRACE_POINT("scatter");
   hipLaunchKernelGGL(k_al_rebuild, dim3(cap_grid((g->arcs + 255) / 256, 8192)), dim3(256), 0, s,
                      g->counters, g->col, g->arcs, Ln, g->al);
   LPA_HIP(hipGetLastError());

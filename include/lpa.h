@@ -39,8 +39,8 @@ extern "C" {
 /* lpa_graph_create* flags */
 #define LPA_INPUT_DEVICE 0x1u /* src/dst are device pointers on `device`        */
 
-#define LPA_NBINS 8
-#define LPA_NKERNELS 9 /* timed: 0 seg 1 hub_final 2 wave 3 g16 4 g8 5 g4 6 g2 7 g1 8 refresh */
+#define LPA_NBINS 12   /* 0 seg 1 w8 2 w4 3 w2 4 g64 5 g32 6 g16 7 g8 8 g4 9 g2 10 g1 11 isolated */
+#define LPA_NKERNELS 13 /* timed: 0 seg 1 hub 2 w8 3 w4 4 w2 5 g64 6 g32 7 g16 8 g8 9 g4 10 g2 11 g1 12 refresh */
 #define LPA_STATS_MAX_ITERS 64
 
 typedef struct lpa_graph lpa_graph;
@@ -64,7 +64,7 @@ typedef struct lpa_graph_info {
   int64_t own_begin;    /* first global (internal) vertex slot of this rank   */
   int32_t rank, nranks, device;
   int32_t max_degree;   /* global maximum symmetrised degree                  */
-  int64_t bin_vertices[LPA_NBINS]; /* bins: 0 seg(hub) 1 wave 2 g16 3 g8 4 g4 5 g2 6 g1 7 isolated */
+  int64_t bin_vertices[LPA_NBINS]; /* degree bins, see LPA_NBINS */
   int64_t bin_arcs[LPA_NBINS];
   int64_t hub_vertices; /* vertices split over several segments (global merge) */
   int64_t segments;     /* segment count of bin 0                             */

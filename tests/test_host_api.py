@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_is_hip_gfx950():
     data = open(_lib.LIB_PATH, "rb").read()
-    assert b"gfx950" in data and b"k_lpa_wave" in data
+    assert b"gfx950" in data and b"k_lpa_wave" in data and b"k_lpa_group" in data
 
 
 def test_no_device_fails_loudly():

@@ -116,7 +116,8 @@ def test_degree_mix_covers_bins():
     V, s, d = degree_mix(0)
     deg = np.bincount(s, minlength=V) + np.bincount(d, minlength=V)
     assert (deg > 4096).sum() >= 2 and ((deg > 512) & (deg <= 2048)).sum() >= 1
-    for lo, hi in ((16, 512), (8, 16), (4, 8), (2, 4), (1, 2), (0, 1)):
+    for lo, hi in ((256, 512), (128, 256), (64, 128), (32, 64), (16, 32), (8, 16), (4, 8), (2, 4),
+                   (1, 2), (0, 1)):
         assert ((deg > lo) & (deg <= hi)).sum() > 0, (lo, hi)
     assert (deg == 0).sum() > 0
 
