@@ -14,7 +14,7 @@
 //      slots, so their labels sit densely in a few cache lines).
 //   4. row_ptr = exclusive scan of owned degrees (int64: >2^31 arcs at scale 26).
 //   5. degree bins = contiguous slot ranges (binary search on the sorted degrees),
-//      hub segments and their global merge tables.
+//      hub segments, their tally staging and the combine work items.
 #include "lpa_internal.h"
 
 namespace lpa {
@@ -120,13 +120,6 @@ __global__ void k_keys_to_pos(const u64* __restrict__ keys, int64_t n, uint32_t*
     pos[j] = (uint32_t)keys[j];
 }
 
-__global__ void k_gather_al(const int32_t* __restrict__ col, int64_t n, const int32_t* __restrict__ L,
-                            int32_t* __restrict__ al) {
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += (int64_t)gridDim.x * blockDim.x)
-    al[j] = L[__builtin_nontemporal_load(col + j)];
-}
-
 // first index in the non-increasing deg_own[0, S) with deg <= t, for each threshold
 __global__ void k_bin_bounds(const int32_t* __restrict__ deg_own, int64_t S,
                              const int32_t* __restrict__ thr, int nthr, int64_t* __restrict__ out) {
@@ -142,17 +135,11 @@ __global__ void k_bin_bounds(const int32_t* __restrict__ deg_own, int64_t S,
 }
 
 __global__ void k_seg_counts(const int32_t* __restrict__ deg_own, int64_t n0,
-                             int32_t* __restrict__ nseg, int32_t* __restrict__ hubcap, int64_t n_hub) {
+                             int32_t* __restrict__ nseg) {
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n0;
        v += (int64_t)gridDim.x * blockDim.x) {
     int32_t d = deg_own[v];
     nseg[v] = (d + kSegArcs - 1) / kSegArcs;
-    if (v < n_hub) {
-      // global table: next power of two >= 2d
-      u32 c = 1u;
-      while (c < 2u * (u32)d) c <<= 1;
-      hubcap[v] = (int32_t)c;
-    }
   }
 }
 
@@ -167,25 +154,11 @@ __global__ void k_fill_segs(const int64_t* __restrict__ rp, const int32_t* __res
     for (int32_t j = 0; j < ns; ++j) {
       Segment sg;
       sg.begin = rp[v] + (int64_t)j * kSegArcs;
-      sg.len = min(kSegArcs, d - j * kSegArcs);
-      sg.v = v < n_hub ? -(int32_t)(v + 1) : (int32_t)v;
+      sg.len = min(kSegArcs, d - j * kSegArcs) | (j << 10);
+      sg.v = (int32_t)v;
       segs[o + j] = sg;
     }
   }
-}
-
-__global__ void k_hub_item_counts(const int32_t* __restrict__ deg_own, int64_t n_hub,
-                                  int32_t* __restrict__ cnt) {
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_hub;
-       v += (int64_t)gridDim.x * blockDim.x)
-    cnt[v] = (deg_own[v] + kHubChunk - 1) / kHubChunk;  // list length <= distinct <= degree
-}
-
-__global__ void k_hub_item_fill(const int32_t* __restrict__ cnt, const int64_t* __restrict__ off,
-                                int64_t n_hub, u64* __restrict__ items) {
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_hub;
-       v += (int64_t)gridDim.x * blockDim.x)
-    for (int32_t k = 0; k < cnt[v]; ++k) items[off[v] + k] = ((u64)v << 32) | (u64)k;
 }
 
 __global__ void k_init_labels(const int32_t* __restrict__ old_of, int64_t n, int32_t* __restrict__ a,
@@ -214,14 +187,6 @@ int init_labels(lpa_graph* g) {
   LPA_HIP(hipGetLastError());
   g->cur = 0;
   return rebuild_arc_labels(g);
-}
-
-int rebuild_arc_labels(lpa_graph* g) {
-  if (g->arcs == 0) return LPA_OK;
-  hipLaunchKernelGGL(k_gather_al, dim3(grid_for(g->arcs)), dim3(256), 0, g->stream, g->col, g->arcs,
-                     g->lab[g->cur], g->al);
-  LPA_HIP(hipGetLastError());
-  return LPA_OK;
 }
 
 int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
@@ -400,13 +365,10 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   const int64_t n0 = g->bin_begin[1];
   if (n0 > 0) {
     int32_t* nseg = nullptr;
-    int32_t* hubcap = nullptr;
     int64_t* seg_off = nullptr;
     LPA_HIP(hipMalloc((void**)&nseg, sizeof(int32_t) * n0));
-    LPA_HIP(hipMalloc((void**)&hubcap, sizeof(int32_t) * (g->n_hub > 0 ? g->n_hub : 1)));
     LPA_HIP(hipMalloc((void**)&seg_off, sizeof(int64_t) * (n0 + 1)));
-    hipLaunchKernelGGL(k_seg_counts, dim3(grid_for(n0)), dim3(256), 0, s, deg_own, n0, nseg,
-                       hubcap, g->n_hub);
+    hipLaunchKernelGGL(k_seg_counts, dim3(grid_for(n0)), dim3(256), 0, s, deg_own, n0, nseg);
     LPA_HIP(hipGetLastError());
     LPA_TRY(exclusive_scan_i32_i64(nseg, seg_off, n0, s));
     LPA_HIP(hipMemcpyAsync(&g->n_segs, seg_off + n0, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -415,55 +377,16 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     hipLaunchKernelGGL(k_fill_segs, dim3(grid_for(n0)), dim3(256), 0, s, g->rp, deg_own, seg_off,
                        n0, g->n_hub, g->segs);
     LPA_HIP(hipGetLastError());
-    if (g->n_hub > 0) {
-      LPA_TRY(dev_alloc(g, (void**)&g->hub_off, sizeof(int64_t) * (g->n_hub + 1)));
-      LPA_TRY(exclusive_scan_i32_i64(hubcap, g->hub_off, g->n_hub, s));
-      int64_t tot = 0;
-      LPA_HIP(hipMemcpyAsync(&tot, g->hub_off + g->n_hub, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-      LPA_HIP(hipStreamSynchronize(s));
-      LPA_TRY(dev_alloc(g, (void**)&g->gtab, sizeof(u64) * tot));
-      LPA_TRY(dev_alloc(g, (void**)&g->glist, sizeof(int32_t) * tot));
-      LPA_TRY(dev_alloc(g, (void**)&g->gcnt, sizeof(int32_t) * g->n_hub));
-      LPA_HIP(hipMemsetAsync(g->gtab, 0, sizeof(u64) * tot, s));
-      LPA_HIP(hipMemsetAsync(g->gcnt, 0, sizeof(int32_t) * g->n_hub, s));
-      LPA_TRY(dev_alloc(g, (void**)&g->hub_best, sizeof(u64) * g->n_hub));
-      LPA_HIP(hipMemsetAsync(g->hub_best, 0, sizeof(u64) * g->n_hub, s));
-      // hub-final work items: one per kHubChunk possible list entries of a hub
-      int32_t* icnt = nullptr;
-      int64_t* ioff = nullptr;
-      LPA_HIP(hipMalloc((void**)&icnt, sizeof(int32_t) * g->n_hub));
-      LPA_HIP(hipMalloc((void**)&ioff, sizeof(int64_t) * (g->n_hub + 1)));
-      hipLaunchKernelGGL(k_hub_item_counts, dim3(grid_for(g->n_hub)), dim3(256), 0, s, deg_own,
-                         g->n_hub, icnt);
-      LPA_HIP(hipGetLastError());
-      LPA_TRY(exclusive_scan_i32_i64(icnt, ioff, g->n_hub, s));
-      LPA_HIP(hipMemcpyAsync(&g->n_hub_items, ioff + g->n_hub, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-      LPA_HIP(hipStreamSynchronize(s));
-      LPA_TRY(dev_alloc(g, (void**)&g->hub_items, sizeof(u64) * g->n_hub_items));
-      hipLaunchKernelGGL(k_hub_item_fill, dim3(grid_for(g->n_hub)), dim3(256), 0, s, icnt, ioff,
-                         g->n_hub, g->hub_items);
-      LPA_HIP(hipGetLastError());
-      LPA_HIP(hipFree(icnt));
-      LPA_HIP(hipFree(ioff));
-      // hub segments: staging for their tallies, per-hub segment ranges
-      LPA_TRY(dev_alloc(g, (void**)&g->hub_seg_off, sizeof(int64_t) * (g->n_hub + 1)));
-      LPA_HIP(hipMemcpyAsync(g->hub_seg_off, seg_off, sizeof(int64_t) * (g->n_hub + 1),
-                             hipMemcpyDeviceToDevice, s));
-      LPA_HIP(hipMemcpyAsync(&g->n_hub_segs, seg_off + g->n_hub, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-      int64_t hub_arcs = 0;
-      LPA_HIP(hipMemcpyAsync(&hub_arcs, g->rp + g->n_hub, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-      LPA_HIP(hipStreamSynchronize(s));
-      LPA_TRY(dev_alloc(g, (void**)&g->stage, sizeof(u64) * hub_arcs));
-      LPA_TRY(dev_alloc(g, (void**)&g->seg_wcnt, sizeof(int32_t) * 4 * g->n_hub_segs));
-      LPA_TRY(dev_alloc(g, (void**)&g->hub_done, sizeof(int32_t) * g->n_hub));
-      LPA_HIP(hipMemsetAsync(g->seg_wcnt, 0, sizeof(int32_t) * 4 * g->n_hub_segs, s));
-      LPA_HIP(hipMemsetAsync(g->hub_done, 0, sizeof(int32_t) * g->n_hub, s));
-    }
+    LPA_TRY(build_hub_tables(g, deg_own));
     LPA_HIP(hipFree(nseg));
-    LPA_HIP(hipFree(hubcap));
-    LPA_HIP(hipFree(seg_off));
+    LPA_TRY(dev_alloc(g, (void**)&g->ucnt, sizeof(int32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
+    g->hub_uoff = seg_off;  // the seg bin is exactly the hub rows (deg > kSegArcs)
+    g->device_bytes += (int64_t)sizeof(int64_t) * (n0 + 1);
   }
   LPA_HIP(hipFree(deg_own));
+
+  LPA_TRY(dev_alloc(g, (void**)&g->dev_err, sizeof(int32_t)));
+  LPA_HIP(hipMemsetAsync(g->dev_err, 0, sizeof(int32_t), s));
 
   // ---- labels (replicated, ping-pong) ----
   LPA_TRY(dev_alloc(g, (void**)&g->lab[0], sizeof(int32_t) * g->vpad));

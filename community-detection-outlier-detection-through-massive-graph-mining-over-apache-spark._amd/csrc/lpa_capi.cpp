@@ -49,9 +49,10 @@ void destroy(lpa_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   void* bufs[] = {g->rp,   g->col,   g->new_of, g->old_of, g->deg,   g->lab[0], g->lab[1],
-                  g->segs, g->hub_off, g->gtab, g->glist,  g->gcnt, g->e_src,  g->e_dst,
-                  g->al,   g->cptr,  g->cpos,   g->chunks, g->counters, g->hub_best, g->hub_items,
-                  g->hub_seg_off, g->hub_done, g->stage, g->seg_wcnt};
+                  g->segs, g->e_src,  g->e_dst, g->al,   g->cptr,  g->cpos,   g->chunks,
+                  g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
+                  g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->items_cb,
+                  g->items_cc, g->hub_uoff, g->ucnt};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);

@@ -1,0 +1,857 @@
+// Hub combine: the mode of a row longer than one segment (deg > kSegArcs).
+//
+// k_lpa_units tallies each 512-arc unit of a seg-bin row (one wave) and leaves
+// the unit's tally words (count << 32 | ~label) in the unit's staging slots
+// (ucnt[unit] words at stage[unit begin ...)).  This file merges the units of a
+// row, T_h words in all (SURVEY.md §7
+// "lpa_hub_bin": block LDS hash with a global spill; here the spill is a
+// bucket-partitioned staging area instead of a global hash, because random
+// 64-bit global atomics run at ~20 G lanes/s on MI355X while block-aggregated
+// partitioning streams).  Three regimes, chosen per hub on the device from T_h:
+//
+//   T <= 512            k_hub_small   one wave: words in registers, weighted
+//                                     ballot peel, residual in a per-wave LDS table
+//                                     (converged rows: one word per unit)
+//   512 < T <= 6144     k_hub_mid     one block: 8192-slot LDS table
+//   T > 6144            K = 2^ceil(log2(T / 2048)) label-hash buckets:
+//                       k_hub_count   per 8-unit chunk: bucket histogram
+//                       k_hub_scan    per hub: bucket offsets
+//                       k_hub_scatter per chunk: words -> bucket-contiguous runs
+//                       k_hub_bucket  per (hub, bucket): LDS tally -> atomicMax
+//                       k_hub_final   per hub: write the label, reset
+//
+// Every label's votes fall in exactly one bucket, so the maximum over bucket
+// maxima is the exact mode with the smallest-label tie-break; the result is
+// independent of the (non-deterministic) order in which words are staged.
+// In the converged supersteps every hub takes the k_hub_small path.
+#include "lpa_device.h"
+
+namespace lpa {
+
+namespace {
+
+using namespace dev;
+
+constexpr int kSmallWords = 512;    // k_hub_small capacity (8 chunks x 64 lanes)
+constexpr int kSmallSlots = 1024;   // its per-wave LDS table
+constexpr int kChunkUnits = 8;      // units per k_hub_count / k_hub_scatter work item
+constexpr int kPeelRounds = 8;
+constexpr int kLaneUnits = 8;       // k_hub_lanes: rows of <= 8 units (deg <= 4096)
+
+__device__ __forceinline__ u32 comb_bucket(u32 label, int lg) {
+  return lg == 0 ? 0u : (label * 0x85EBCA77u) >> (32 - lg);
+}
+__device__ __forceinline__ u32 comb_sub(u32 label, int lg) {
+  return lg == 0 ? 0u : (label * 0xC2B2AE3Du) >> (32 - lg);
+}
+// buckets of a hub with T staged words (T > kCombDirect)
+__device__ __forceinline__ int comb_lgK(int T) {
+  const int lg = ceil_log2((u32)((T + kCombWords - 1) / kCombWords));
+  return lg < kMaxBucketsLg ? lg : kMaxBucketsLg;
+}
+
+// Staged words of row h: unit j (j < nu = uoff[h+1] - uoff[h]) left ucnt[uoff[h] + j]
+// words at stage[rp[h] + j * kSegArcs ...).
+struct RowUnits {
+  int64_t sbase;  // rp[h]
+  int64_t u0;     // first unit
+  int nu;         // units
+};
+
+__device__ __forceinline__ RowUnits row_units(const int64_t* __restrict__ rp,
+                                              const int64_t* __restrict__ uoff, int64_t h) {
+  RowUnits r;
+  r.sbase = rp[h];
+  r.u0 = uoff[h];
+  r.nu = (int)(uoff[h + 1] - r.u0);
+  return r;
+}
+
+// Per-lane insert of one word with a wave pre-combine: the first active label of
+// the wave's 64 words is summed in registers and inserted once.
+__device__ __forceinline__ void insert_word(u64 word, bool act, u64* tab, uint16_t* lst, int* lcount,
+                                            int lg, int lane, int32_t* err) {
+  const u64 am = __ballot(act);
+  if (am == 0ull) return;  // uniform over the wave
+  const u32 lab = ~(u32)word;
+  const int f = __ffsll((unsigned long long)am) - 1;
+  const u32 x = (u32)__builtin_amdgcn_readlane((int)lab, f);
+  const bool mt = act && lab == x;
+  const u32 c = wave_sum_u32(mt ? (u32)(word >> 32) : 0u);
+  u32 ilab = lab, icnt = (u32)(word >> 32);
+  bool ins = act && !mt;
+  if (lane == f) {
+    ins = true;
+    ilab = x;
+    icnt = c;
+  }
+  int slot = -1;
+  if (ins) slot = lds_insert_bounded(tab, 32 - lg, (1u << lg) - 1u, ilab, icnt, err);
+  list_append(lst, lcount, slot, lane);
+}
+
+// ---------------------------------------------------------------------------
+// rows of <= kLaneUnits units (deg <= 4096): one LANE per row.  A converged
+// row left one word per unit; the lane loads them and takes the mode of <= 8
+// words in registers.  Any other row is handed to k_hub_small (list W).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hub_lanes(int64_t h_begin, int64_t h_end,
+                                                   const int64_t* __restrict__ rp,
+                                                   const int64_t* __restrict__ uoff,
+                                                   const int32_t* __restrict__ ucnt,
+                                                   const u64* __restrict__ stage,
+                                                   int32_t* __restrict__ Ln,
+                                                   int32_t* __restrict__ listW,
+                                                   int32_t* __restrict__ lcnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t h0 = h_begin + (int64_t)blockIdx.x * blockDim.x; h0 < h_end; h0 += stride) {
+    const int64_t h = h0 + threadIdx.x;
+    const bool live = h < h_end;
+    bool one = false;
+    if (live) {
+      const int64_t b = rp[h];
+      const int nu = (int)((rp[h + 1] - b + kSegArcs - 1) / kSegArcs);
+      const int32_t* uc = ucnt + uoff[h];
+      int c[kLaneUnits];
+#pragma unroll
+      for (int k = 0; k < kLaneUnits; ++k) c[k] = k < nu ? uc[k] : 1;
+      one = true;
+#pragma unroll
+      for (int k = 0; k < kLaneUnits; ++k) one = one && c[k] == 1;
+      if (one) {
+        const u64* wd = stage + b;
+        u64 wv[kLaneUnits];
+#pragma unroll
+        for (int k = 0; k < kLaneUnits; ++k) wv[k] = k < nu ? wd[(int64_t)k * kSegArcs] : 0ull;
+        u64 best = 0ull;
+#pragma unroll
+        for (int k = 0; k < kLaneUnits; ++k) {
+          u32 cs = 0u;
+#pragma unroll
+          for (int q = 0; q < kLaneUnits; ++q)
+            if ((u32)wv[q] == (u32)wv[k]) cs += (u32)(wv[q] >> 32);
+          if (wv[k] != 0ull) best = umax64(best, ((u64)cs << 32) | (u64)(u32)wv[k]);
+        }
+        Ln[h] = (int32_t)(~(u32)best);
+      }
+    }
+    const u64 m = __ballot(live && !one);
+    if (m) {
+      const int lead = __ffsll((unsigned long long)m) - 1;
+      int base = 0;
+      if (lane == lead) base = atomicAdd(&lcnt[4], __popcll(m));
+      base = __builtin_amdgcn_readlane(base, lead);
+      if (live && !one) listW[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)h;
+    }
+  }
+}
+
+// queue row h (T staged words) for k_hub_mid or the bucket path
+__device__ __forceinline__ void queue_row(int64_t h, int T, int nu, int lane,
+                                          int32_t* __restrict__ wcount, int32_t* __restrict__ listB,
+                                          int32_t* __restrict__ listC, int32_t* __restrict__ lcnt,
+                                          u64* __restrict__ itemsCB, u64* __restrict__ itemsCC) {
+  if (lane == 0) {
+    wcount[h] = T;
+    if (T <= kCombDirect) {
+      listB[atomicAdd(&lcnt[0], 1)] = (int32_t)h;
+    } else {
+      listC[atomicAdd(&lcnt[1], 1)] = (int32_t)h;
+    }
+  }
+  if (T > kCombDirect) {
+    const int K = 1 << comb_lgK(T);
+    const int nch = (nu + kChunkUnits - 1) / kChunkUnits;
+    int cb = 0, cc = 0;
+    if (lane == 0) {
+      cb = atomicAdd(&lcnt[2], K);
+      cc = atomicAdd(&lcnt[3], nch);
+    }
+    cb = __builtin_amdgcn_readfirstlane(cb);
+    cc = __builtin_amdgcn_readfirstlane(cc);
+    for (int k = lane; k < K; k += 64) itemsCB[cb + k] = ((u64)h << 32) | (u64)k;
+    for (int c = lane; c < nch; c += 64) itemsCC[cc + c] = ((u64)h << 32) | (u64)c;
+  }
+}
+
+// weighted ballot peel over NC word chunks: rounds retire the first unretired
+// label's words; lane p ends with round p's tally word in *pw, returns rounds.
+template <int NC>
+__device__ __forceinline__ int weighted_peel(const u64 (&wv)[NC], u64 (&act)[NC], int& nact,
+                                             u64& best, u64& pw, int lane) {
+  int np = 0;
+  for (int p = 0; p < kPeelRounds && nact > 0; ++p) {
+    u32 x = 0u;
+    bool found = false;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (!found && act[c] != 0ull) {
+        x = ~(u32)__builtin_amdgcn_readlane((int)(u32)wv[c], __ffsll((unsigned long long)act[c]) - 1);
+        found = true;
+      }
+    }
+    u32 cs = 0u;
+    int k = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const u64 mm = __ballot(((act[c] >> lane) & 1ull) && ~(u32)wv[c] == x);
+      act[c] &= ~mm;
+      k += __popcll(mm);
+      if ((mm >> lane) & 1ull) cs += (u32)(wv[c] >> 32);
+    }
+    nact -= k;
+    const u64 tw = tally(wave_sum_u32(cs), x);
+    best = umax64(best, tw);
+    if (lane == p) pw = tw;
+    np = p + 1;
+    if (k < 2) break;
+  }
+  return np;
+}
+
+// ---------------------------------------------------------------------------
+// one wave per row (grid-stride over rows [0, h_lane) and list W):
+//   <= 512 units and <= 512 words      words in registers, weighted peel,
+//                                      residual in the wave's LDS table
+//   > 512 units, one word each         512-unit batches merged in the LDS table
+//                                      (giant converged rows)
+//   otherwise                          queued with T in wcount[h]
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, const int64_t* __restrict__ rp,
+                                                   const int64_t* __restrict__ uoff,
+                                                   const int32_t* __restrict__ ucnt,
+                                                   const u64* __restrict__ stage,
+                                                   int32_t* __restrict__ wcount,
+                                                   int32_t* __restrict__ Ln,
+                                                   const int32_t* __restrict__ listW,
+                                                   int32_t* __restrict__ listB,
+                                                   int32_t* __restrict__ listC,
+                                                   int32_t* __restrict__ lcnt,
+                                                   u64* __restrict__ itemsCB,
+                                                   u64* __restrict__ itemsCC) {
+  __shared__ u64 tab_all[4][kSmallSlots];
+  __shared__ int32_t aux_all[4][kSmallWords];  // unit prefixes, then the slot list
+  __shared__ int lc_all[4];
+  constexpr int NC = kSmallWords / 64;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  u64* tab = tab_all[w];
+  int32_t* pre = aux_all[w];
+  uint16_t* lst = reinterpret_cast<uint16_t*>(aux_all[w]);
+  for (int i = lane; i < kSmallSlots; i += 64) tab[i] = 0ull;
+  const int64_t nq = h_lane + lcnt[4];
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t q = (int64_t)blockIdx.x * 4 + w; q < nq; q += stride) {
+    const int64_t h = q < h_lane ? q : (int64_t)listW[q - h_lane];
+    const RowUnits ru = row_units(rp, uoff, h);
+    const int nu = ru.nu;
+    const int32_t* uc = ucnt + ru.u0;
+    const u64* wd = stage + ru.sbase;
+    int cnt[NC];
+    int T = 0;
+    if (nu <= kSmallWords) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int j = c * 64 + lane;
+        cnt[c] = (c * 64 < nu && j < nu) ? uc[j] : 0;
+        T += cnt[c];
+      }
+    } else {
+      for (int j = lane; j < nu; j += 64) T += uc[j];
+    }
+    T = (int)wave_sum_u32((u32)T);
+    if (nu > kSmallWords && T == nu) {
+      // giant converged row: 512-unit batches, peel groups + residual merged in LDS
+      if (lane == 0) lc_all[w] = 0;
+      bool ovf = false;
+      u64 best = 0ull;
+      for (int b0 = 0; b0 < nu; b0 += kSmallWords) {
+        u64 wv[NC], act[NC];
+        int nact = 0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int j = b0 + c * 64 + lane;
+          wv[c] = j < nu ? wd[(int64_t)j * kSegArcs] : 0ull;
+          act[c] = __ballot(wv[c] != 0ull);
+          nact += __popcll(act[c]);
+        }
+        u64 pw = 0ull, pbest = 0ull;
+        const int np = weighted_peel<NC>(wv, act, nact, pbest, pw, lane);
+        if (lc_all[w] + np + nact > kSmallWords) {
+          ovf = true;
+          break;
+        }
+        int slot = -1;
+        if (lane < np) slot = lds_insert(tab, 32 - 10, kSmallSlots - 1u, ~(u32)pw, (u32)(pw >> 32));
+        list_append(lst, &lc_all[w], slot, lane);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          slot = -1;
+          if ((act[c] >> lane) & 1ull)
+            slot = lds_insert(tab, 32 - 10, kSmallSlots - 1u, ~(u32)wv[c], (u32)(wv[c] >> 32));
+          list_append(lst, &lc_all[w], slot, lane);
+        }
+      }
+      const int n = lc_all[w];
+      for (int i = lane; i < n; i += 64) {
+        const int sl = lst[i];
+        best = umax64(best, tab[sl]);
+        tab[sl] = 0ull;
+      }
+      best = wave_max_u64(best);
+      if (ovf) {
+        queue_row(h, T, nu, lane, wcount, listB, listC, lcnt, itemsCB, itemsCC);
+      } else if (lane == 0) {
+        Ln[h] = (int32_t)(~(u32)best);
+      }
+      continue;
+    }
+    if (nu > kSmallWords || T > kSmallWords) {
+      queue_row(h, T, nu, lane, wcount, listB, listC, lcnt, itemsCB, itemsCC);
+      continue;
+    }
+    u64 wv[NC];
+    if (T == nu) {
+      // converged rows: one word per unit, at the unit's first staging slot
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int j = c * 64 + lane;
+        wv[c] = (c * 64 < nu && j < nu) ? wd[(int64_t)j * kSegArcs] : 0ull;
+      }
+    } else {
+      // unit prefixes into LDS, then word i = unit j (largest pre[j] <= i)
+      int carry = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (c * 64 < nu) {
+          int incl = cnt[c];
+#pragma unroll
+          for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+          }
+          if (c * 64 + lane < nu) pre[c * 64 + lane] = carry + incl - cnt[c];
+          carry += __shfl(incl, 63, 64);
+        }
+      }
+      const int steps = ceil_log2((u32)nu);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int i = c * 64 + lane;
+        wv[c] = 0ull;
+        if (c * 64 < T && i < T) {
+          int lo = 0;
+          for (int st = steps - 1; st >= 0; --st) {
+            const int mid = lo + (1 << st);
+            if (mid < nu && pre[mid] <= i) lo = mid;
+          }
+          wv[c] = wd[(int64_t)lo * kSegArcs + (i - pre[lo])];
+        }
+      }
+    }
+    u64 act[NC];
+    int nact = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      act[c] = __ballot(wv[c] != 0ull);
+      nact += __popcll(act[c]);
+    }
+    u64 best = 0ull, pw = 0ull;
+    weighted_peel<NC>(wv, act, nact, best, pw, lane);
+    if (nact > 0) {
+      if (lane == 0) lc_all[w] = 0;
+      int lg = ceil_log2(2u * (u32)T);
+      lg = lg < 6 ? 6 : lg;
+      const u32 mask = (1u << lg) - 1u;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        int slot = -1;
+        if ((act[c] >> lane) & 1ull)
+          slot = lds_insert(tab, 32 - lg, mask, ~(u32)wv[c], (u32)(wv[c] >> 32));
+        list_append(lst, &lc_all[w], slot, lane);
+      }
+      const int n = lc_all[w];
+      for (int i = lane; i < n; i += 64) {
+        const int sl = lst[i];
+        best = umax64(best, tab[sl]);
+        tab[sl] = 0ull;
+      }
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) Ln[h] = (int32_t)(~(u32)best);
+  }
+}
+
+// Tally the words of units [j0, j1) of a row whose labels pass `keep` into the
+// block's LDS table (kCombSlots slots).  Returns the block-uniform maximum.
+template <typename Keep>
+__device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __restrict__ uc, int j0,
+                                 int j1, Keep keep, u64* tab, uint16_t* lst, int* lcount, u64* redw,
+                                 int32_t* err) {
+  constexpr int kLg = 13;
+  static_assert((1 << kLg) == kCombSlots, "combine table size");
+  constexpr int NC = kSegArcs / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) *lcount = 0;
+  __syncthreads();
+  // wave w takes units j0 + w + 4i, 64 at a time: lane-per-unit for each unit's
+  // first kFirst words (converged units hold one), then unit-major for longer units
+  constexpr int kFirst = 4;
+  for (int jb = j0 + w; jb < j1; jb += 256) {
+    const int j = jb + 4 * lane;
+    const int nj = j < j1 ? uc[j] : 0;
+    const u64* src = wd + (int64_t)j * kSegArcs;
+    u64 fv[kFirst];
+#pragma unroll
+    for (int k = 0; k < kFirst; ++k) fv[k] = k < nj ? src[k] : 0ull;
+#pragma unroll
+    for (int k = 0; k < kFirst; ++k)
+      insert_word(fv[k], fv[k] != 0ull && keep(~(u32)fv[k]), tab, lst, lcount, kLg, lane, err);
+    // longer units one at a time, the next one's words loading meanwhile
+    u64 big = __ballot(nj > kFirst);
+    u64 wv[NC];
+    int n = 0;
+    auto load_big = [&](u64 set, u64(&dst)[NC], int& cnt) {
+      cnt = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dst[c] = 0ull;
+      if (set == 0ull) return;
+      const int bl = __ffsll((unsigned long long)set) - 1;
+      cnt = __builtin_amdgcn_readlane(nj, bl);
+      const u64* us = wd + (int64_t)(jb + 4 * bl) * kSegArcs;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int i = kFirst + c * 64 + lane;
+        dst[c] = (kFirst + c * 64 < cnt && i < cnt) ? us[i] : 0ull;
+      }
+    };
+    load_big(big, wv, n);
+    while (big) {
+      big &= big - 1ull;
+      u64 wn[NC];
+      int nn = 0;
+      load_big(big, wn, nn);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (kFirst + c * 64 >= n) break;  // uniform over the wave
+        insert_word(wv[c], wv[c] != 0ull && keep(~(u32)wv[c]), tab, lst, lcount, kLg, lane, err);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) wv[c] = wn[c];
+      n = nn;
+    }
+  }
+  __syncthreads();
+  const int cnt = *lcount;
+  u64 best = 0ull;
+  for (int i = threadIdx.x; i < cnt; i += 256) {
+    const int sl = lst[i];
+    best = umax64(best, tab[sl]);
+    tab[sl] = 0ull;
+  }
+  best = wave_max_u64(best);
+  if (lane == 0) redw[w] = best;
+  __syncthreads();
+  best = umax64(umax64(redw[0], redw[1]), umax64(redw[2], redw[3]));
+  __syncthreads();
+  return best;
+}
+
+// Same over a compact word run wd[0, n) (a bucket after the scatter).
+template <typename Keep>
+__device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64* tab, uint16_t* lst,
+                               int* lcount, u64* redw, int32_t* err) {
+  constexpr int kLg = 13;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) *lcount = 0;
+  __syncthreads();
+  constexpr int R = kCombDirect / 256;
+  for (int b0 = 0; b0 < n; b0 += R * 256) {
+    u64 wv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = b0 + r * 256 + threadIdx.x;
+      wv[r] = i < n ? wd[i] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (b0 + r * 256 >= n) break;  // uniform over the block
+      insert_word(wv[r], wv[r] != 0ull && keep(~(u32)wv[r]), tab, lst, lcount, kLg, lane, err);
+    }
+  }
+  __syncthreads();
+  const int cnt = *lcount;
+  u64 best = 0ull;
+  for (int i = threadIdx.x; i < cnt; i += 256) {
+    const int sl = lst[i];
+    best = umax64(best, tab[sl]);
+    tab[sl] = 0ull;
+  }
+  best = wave_max_u64(best);
+  if (lane == 0) redw[w] = best;
+  __syncthreads();
+  best = umax64(umax64(redw[0], redw[1]), umax64(redw[2], redw[3]));
+  __syncthreads();
+  return best;
+}
+
+// ---------------------------------------------------------------------------
+// 512 < T <= kCombDirect: one block per queued row (grid-stride over the queue).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hub_mid(const int32_t* __restrict__ listB,
+                                                 const int32_t* __restrict__ lcnt,
+                                                 const int64_t* __restrict__ rp,
+                                                 const int64_t* __restrict__ uoff,
+                                                 const int32_t* __restrict__ ucnt,
+                                                 const u64* __restrict__ stage,
+                                                 int32_t* __restrict__ wcount,
+                                                 int32_t* __restrict__ Ln, int32_t* __restrict__ err) {
+  __shared__ u64 tab[kCombSlots];
+  __shared__ uint16_t lst[kCombSlots];
+  __shared__ int lcount;
+  __shared__ u64 redw[4];
+  const int nB = lcnt[0];
+  if ((int)blockIdx.x >= nB) return;
+  for (int i = threadIdx.x; i < kCombSlots; i += 256) tab[i] = 0ull;
+  for (int q = blockIdx.x; q < nB; q += gridDim.x) {
+    const int64_t h = listB[q];
+    const RowUnits ru = row_units(rp, uoff, h);
+    const u64 best = block_tally_units(stage + ru.sbase, ucnt + ru.u0, 0, ru.nu,
+                                       [](u32) { return true; }, tab, lst, &lcount, redw, err);
+    if (threadIdx.x == 0) {
+      Ln[h] = (int32_t)(~(u32)best);
+      wcount[h] = 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// T > kCombDirect: bucket partition of the staged words, kChunkUnits units per
+// count / scatter work item.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hub_count(const u64* __restrict__ itemsCC,
+                                                   const int32_t* __restrict__ lcnt,
+                                                   const int64_t* __restrict__ rp,
+                                                   const int64_t* __restrict__ uoff,
+                                                   const int32_t* __restrict__ ucnt,
+                                                   const u64* __restrict__ stage,
+                                                   const int32_t* __restrict__ wcount,
+                                                   const int64_t* __restrict__ hoff,
+                                                   int32_t* __restrict__ ghist) {
+  __shared__ int hist[kMaxBuckets];
+  constexpr int NC = kSegArcs / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = lcnt[3];
+  for (int it = blockIdx.x; it < n; it += gridDim.x) {
+    const u64 item = itemsCC[it];
+    const int64_t h = (int64_t)(item >> 32);
+    const int c = (int)(u32)item;
+    const RowUnits ru = row_units(rp, uoff, h);
+    const int lgK = comb_lgK(wcount[h]), K = 1 << lgK;
+    for (int k = threadIdx.x; k < K; k += 256) hist[k] = 0;
+    __syncthreads();
+    const int j1 = min(ru.nu, (c + 1) * kChunkUnits);
+    for (int j = c * kChunkUnits + w; j < j1; j += 4) {
+      const int nw = ucnt[ru.u0 + j];
+      const u64* src = stage + ru.sbase + (int64_t)j * kSegArcs;
+      u64 wv[NC];
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const int i = q * 64 + lane;
+        wv[q] = (q * 64 < nw && i < nw) ? src[i] : 0ull;
+      }
+#pragma unroll
+      for (int q = 0; q < NC; ++q)
+        if (wv[q] != 0ull) atomicAdd(&hist[comb_bucket(~(u32)wv[q], lgK)], 1);
+    }
+    __syncthreads();
+    int32_t* gh = ghist + hoff[h];
+    for (int k = threadIdx.x; k < K; k += 256)
+      if (hist[k]) atomicAdd(&gh[k], hist[k]);
+    __syncthreads();
+  }
+}
+
+// one wave per queued row: gcur[k] = exclusive prefix of ghist[k]
+__global__ __launch_bounds__(256) void k_hub_scan(const int32_t* __restrict__ listC,
+                                                  const int32_t* __restrict__ lcnt,
+                                                  const int32_t* __restrict__ wcount,
+                                                  const int64_t* __restrict__ hoff,
+                                                  const int32_t* __restrict__ ghist,
+                                                  int32_t* __restrict__ gcur) {
+  const int lane = threadIdx.x & 63;
+  const int nC = lcnt[1];
+  for (int q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nC; q += gridDim.x * 4) {
+    const int64_t h = listC[q];
+    const int K = 1 << comb_lgK(wcount[h]);
+    const int32_t* gh = ghist + hoff[h];
+    int32_t* gc = gcur + hoff[h];
+    int carry = 0;
+    for (int k0 = 0; k0 < K; k0 += 64) {
+      const int v = k0 + lane < K ? gh[k0 + lane] : 0;
+      int incl = v;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+      }
+      if (k0 + lane < K) gc[k0 + lane] = carry + incl - v;
+      carry += __shfl(incl, 63, 64);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_hub_scatter(const u64* __restrict__ itemsCC,
+                                                     const int32_t* __restrict__ lcnt,
+                                                     const int64_t* __restrict__ rp,
+                                                     const int64_t* __restrict__ uoff,
+                                                     const int32_t* __restrict__ ucnt,
+                                                     const u64* __restrict__ stage,
+                                                     const int32_t* __restrict__ wcount,
+                                                     const int64_t* __restrict__ hoff,
+                                                     int32_t* __restrict__ gcur,
+                                                     u64* __restrict__ scat) {
+  __shared__ int lh[kMaxBuckets];
+  __shared__ int lb[kMaxBuckets];
+  constexpr int NC = kSegArcs / 64;
+  constexpr int kPerWave = kChunkUnits / 4;  // units per wave per item
+  static_assert(kChunkUnits % 4 == 0, "units per chunk item");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = lcnt[3];
+  for (int it = blockIdx.x; it < n; it += gridDim.x) {
+    const u64 item = itemsCC[it];
+    const int64_t h = (int64_t)(item >> 32);
+    const int c = (int)(u32)item;
+    const RowUnits ru = row_units(rp, uoff, h);
+    const int lgK = comb_lgK(wcount[h]), K = 1 << lgK;
+    for (int k = threadIdx.x; k < K; k += 256) lh[k] = 0;
+    __syncthreads();
+    const int j1 = min(ru.nu, (c + 1) * kChunkUnits);
+    u64 wv[kPerWave][NC];
+    int bk[kPerWave][NC], rk[kPerWave][NC];
+#pragma unroll
+    for (int a = 0; a < kPerWave; ++a) {
+      const int j = c * kChunkUnits + w + 4 * a;
+      const int nw = j < j1 ? ucnt[ru.u0 + j] : 0;
+      const u64* src = stage + ru.sbase + (int64_t)j * kSegArcs;
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const int i = q * 64 + lane;
+        wv[a][q] = (q * 64 < nw && i < nw) ? src[i] : 0ull;
+        bk[a][q] = -1;
+        rk[a][q] = 0;
+      }
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        if (wv[a][q] != 0ull) {
+          bk[a][q] = (int)comb_bucket(~(u32)wv[a][q], lgK);
+          rk[a][q] = atomicAdd(&lh[bk[a][q]], 1);
+        }
+      }
+    }
+    __syncthreads();
+    int32_t* gc = gcur + hoff[h];
+    for (int k = threadIdx.x; k < K; k += 256)
+      if (lh[k]) lb[k] = atomicAdd(&gc[k], lh[k]);
+    __syncthreads();
+    u64* out = scat + ru.sbase;
+#pragma unroll
+    for (int a = 0; a < kPerWave; ++a)
+#pragma unroll
+      for (int q = 0; q < NC; ++q)
+        if (bk[a][q] >= 0) out[lb[bk[a][q]] + rk[a][q]] = wv[a][q];
+    __syncthreads();
+  }
+}
+
+// one block per (row, bucket): after the scatter, bucket k of row h is
+// scat[rp[h] + gcur[k] - ghist[k], rp[h] + gcur[k])
+__global__ __launch_bounds__(256) void k_hub_bucket(const u64* __restrict__ itemsCB,
+                                                    const int32_t* __restrict__ lcnt,
+                                                    const int64_t* __restrict__ rp,
+                                                    const u64* __restrict__ scat,
+                                                    const int64_t* __restrict__ hoff,
+                                                    const int32_t* __restrict__ ghist,
+                                                    const int32_t* __restrict__ gcur,
+                                                    u64* __restrict__ hub_best,
+                                                    int32_t* __restrict__ err) {
+  __shared__ u64 tab[kCombSlots];
+  __shared__ uint16_t lst[kCombSlots];
+  __shared__ int lcount;
+  __shared__ u64 redw[4];
+  const int n = lcnt[2];
+  if ((int)blockIdx.x >= n) return;
+  for (int i = threadIdx.x; i < kCombSlots; i += 256) tab[i] = 0ull;
+  for (int it = blockIdx.x; it < n; it += gridDim.x) {
+    const u64 item = itemsCB[it];
+    const int64_t h = (int64_t)(item >> 32);
+    const int k = (int)(u32)item;
+    const int cnt = ghist[hoff[h] + k];
+    if (cnt == 0) continue;  // uniform
+    const u64* wd = scat + rp[h] + (gcur[hoff[h] + k] - cnt);
+    // a bucket far above its expected load is tallied in sub-bucket passes
+    const int lgJ = cnt > kCombDirect ? ceil_log2((u32)((cnt + 4095) / 4096)) : 0;
+    u64 best = 0ull;
+    for (u32 j = 0; j < (1u << lgJ); ++j)
+      best = umax64(best, block_tally_run(wd, cnt, [=](u32 lab) { return comb_sub(lab, lgJ) == j; },
+                                          tab, lst, &lcount, redw, err));
+    if (threadIdx.x == 0 && best) atomicMax(&hub_best[h], best);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_hub_final(const int32_t* __restrict__ listC,
+                                                   const int32_t* __restrict__ lcnt,
+                                                   int32_t* __restrict__ wcount,
+                                                   const int64_t* __restrict__ hoff,
+                                                   int32_t* __restrict__ ghist,
+                                                   u64* __restrict__ hub_best,
+                                                   int32_t* __restrict__ Ln) {
+  const int lane = threadIdx.x & 63;
+  const int nC = lcnt[1];
+  for (int q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nC; q += gridDim.x * 4) {
+    const int64_t h = listC[q];
+    const int K = 1 << comb_lgK(wcount[h]);
+    int32_t* gh = ghist + hoff[h];
+    for (int k = lane; k < K; k += 64) gh[k] = 0;
+    if (lane == 0) {
+      Ln[h] = (int32_t)(~(u32)hub_best[h]);
+      hub_best[h] = 0ull;
+      wcount[h] = 0;
+    }
+  }
+}
+
+__global__ void k_hub_bounds(const int32_t* __restrict__ deg_own, int64_t n_hub,
+                             int32_t* __restrict__ nb, int32_t* __restrict__ nc) {
+  for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_hub;
+       h += (int64_t)gridDim.x * blockDim.x) {
+    const int d = deg_own[h];  // staged words <= arcs
+    int lg = 0;
+    if (d > kCombDirect) {
+      lg = ceil_log2((u32)((d + kCombWords - 1) / kCombWords));
+      lg = lg < kMaxBucketsLg ? lg : kMaxBucketsLg;
+    }
+    nb[h] = 1 << lg;
+    const int nu = (d + kSegArcs - 1) / kSegArcs;
+    nc[h] = (nu + kChunkUnits - 1) / kChunkUnits;
+  }
+}
+
+// first index of the non-increasing deg[0, n) with deg <= t
+__global__ void k_first_le(const int32_t* __restrict__ deg, int64_t n, int32_t t, int64_t* out) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (deg[mid] > t) lo = mid + 1; else hi = mid;
+  }
+  *out = lo;
+}
+
+inline unsigned grid_cap(int64_t want, int64_t cap) {
+  if (want < 1) want = 1;
+  return (unsigned)(want < cap ? want : cap);
+}
+
+}  // namespace
+
+int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
+  hipStream_t s = g->stream;
+  const int64_t n = g->n_hub;
+  if (n == 0) return LPA_OK;
+  int64_t hub_arcs = 0;
+  LPA_HIP(hipMemcpyAsync(&hub_arcs, g->rp + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  int32_t *nb = nullptr, *nc = nullptr;
+  int64_t* coff = nullptr;
+  LPA_HIP(hipMalloc((void**)&nb, sizeof(int32_t) * n));
+  LPA_HIP(hipMalloc((void**)&nc, sizeof(int32_t) * n));
+  LPA_HIP(hipMalloc((void**)&coff, sizeof(int64_t) * (n + 1)));
+  hipLaunchKernelGGL(k_hub_bounds, dim3(grid_cap((n + 255) / 256, 65536)), dim3(256), 0, s, deg_own,
+                     n, nb, nc);
+  LPA_HIP(hipGetLastError());
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_hoff, sizeof(int64_t) * (n + 1)));
+  LPA_TRY(exclusive_scan_i32_i64(nb, g->hub_hoff, n, s));
+  LPA_TRY(exclusive_scan_i32_i64(nc, coff, n, s));
+  int64_t nbk = 0, nch = 0;
+  LPA_HIP(hipMemcpyAsync(&nbk, g->hub_hoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipMemcpyAsync(&nch, coff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  LPA_HIP(hipFree(nb));
+  LPA_HIP(hipFree(nc));
+  LPA_HIP(hipFree(coff));
+  if (nbk > INT32_MAX || nch > INT32_MAX || hub_arcs > ((int64_t)1 << 40)) {
+    set_error("hub combine tables too large (%lld buckets, %lld chunks)", (long long)nbk,
+              (long long)nch);
+    return LPA_EINVAL;
+  }
+  g->n_hub_buckets = nbk;
+  g->n_hub_chunks = nch;
+  LPA_TRY(dev_alloc(g, (void**)&g->stage, sizeof(u64) * hub_arcs));
+  LPA_TRY(dev_alloc(g, (void**)&g->scat, sizeof(u64) * hub_arcs));
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_wcount, sizeof(int32_t) * n));
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_best, sizeof(u64) * n));
+  LPA_TRY(dev_alloc(g, (void**)&g->ghist, sizeof(int32_t) * nbk));
+  LPA_TRY(dev_alloc(g, (void**)&g->gcur, sizeof(int32_t) * nbk));
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_lists, sizeof(int32_t) * 3 * n));
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_lcnt, sizeof(int32_t) * 5));
+  {
+    // rows [hub_lane_begin, n_hub) have <= kLaneUnits units (degree-descending order)
+    int64_t* d_pos = nullptr;
+    LPA_HIP(hipMalloc((void**)&d_pos, sizeof(int64_t)));
+    hipLaunchKernelGGL(k_first_le, dim3(1), dim3(1), 0, s, deg_own, n, kLaneUnits * kSegArcs, d_pos);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipMemcpyAsync(&g->hub_lane_begin, d_pos, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    LPA_HIP(hipFree(d_pos));
+  }
+  LPA_TRY(dev_alloc(g, (void**)&g->items_cb, sizeof(u64) * nbk));
+  LPA_TRY(dev_alloc(g, (void**)&g->items_cc, sizeof(u64) * nch));
+  LPA_HIP(hipMemsetAsync(g->hub_wcount, 0, sizeof(int32_t) * n, s));
+  LPA_HIP(hipMemsetAsync(g->hub_best, 0, sizeof(u64) * n, s));
+  LPA_HIP(hipMemsetAsync(g->ghist, 0, sizeof(int32_t) * nbk, s));
+  return LPA_OK;
+}
+
+int launch_hub_combine(lpa_graph* g, int32_t* Lown) {
+  const int64_t n = g->n_hub;
+  if (n == 0) return LPA_OK;
+  hipStream_t s = g->stream;
+  int32_t* listB = g->hub_lists;
+  int32_t* listC = g->hub_lists + n;
+  LPA_HIP(hipMemsetAsync(g->hub_lcnt, 0, sizeof(int32_t) * 5, s));
+  const int64_t hl = g->hub_lane_begin;
+  int32_t* listW = g->hub_lists + 2 * n;
+  if (hl < n) {
+    hipLaunchKernelGGL(k_hub_lanes, dim3(grid_cap((n - hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
+                       g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, listW, g->hub_lcnt);
+    LPA_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, hl, g->rp, g->hub_uoff, g->ucnt,
+                     g->stage, g->hub_wcount, Lown, listW, listB, listC, g->hub_lcnt, g->items_cb,
+                     g->items_cc);
+  LPA_HIP(hipGetLastError());
+  const unsigned nbl = grid_cap(n, 1024);
+  hipLaunchKernelGGL(k_hub_mid, dim3(nbl), dim3(256), 0, s, listB, g->hub_lcnt, g->rp, g->hub_uoff,
+                     g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
+  LPA_HIP(hipGetLastError());
+  const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
+  hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, s, g->items_cc, g->hub_lcnt, g->rp,
+                     g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->ghist);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_hub_scan, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, s, listC,
+                     g->hub_lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->gcur);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, s, g->items_cc, g->hub_lcnt, g->rp,
+                     g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->gcur, g->scat);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_hub_bucket, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, s,
+                     g->items_cb, g->hub_lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
+                     g->hub_best, g->dev_err);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, s, listC,
+                     g->hub_lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown);
+  LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
+
+}  // namespace lpa

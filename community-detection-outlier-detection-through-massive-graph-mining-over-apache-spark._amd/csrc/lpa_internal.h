@@ -13,12 +13,13 @@ namespace lpa {
 
 typedef unsigned long long u64;
 typedef uint32_t u32;
+typedef int32_t v4i __attribute__((ext_vector_type(4)));  // native 16-B vector (nontemporal-capable)
 
 // ---------------------------------------------------------------------------
 // Degree bins (SURVEY.md §7 kernel inventory).  Vertices of a rank's slice are
 // sorted by degree (descending), so every bin is one contiguous range.
 // ---------------------------------------------------------------------------
-//   seg  deg > 512          block per 2048-arc segment        (k_lpa_seg + hub kernels)
+//   seg  deg > 512          wave per 512-arc unit, staged     (k_lpa_units + hub combine)
 //   w8/w4/w2  deg <= 512/256/128   wave per vertex, 8/4/2 chunks (k_lpa_wave<NC>)
 //   g64 .. g1 deg <= G          G lanes per vertex                (k_lpa_group<G>)
 enum Bin { BIN_SEG = 0, BIN_W8 = 1, BIN_W4 = 2, BIN_W2 = 3, BIN_G64 = 4, BIN_G32 = 5, BIN_G16 = 6,
@@ -28,19 +29,22 @@ static_assert(BIN_ISO + 1 == LPA_NBINS, "bin table");
 constexpr int kBinMaxDeg[LPA_NBINS] = {1 << 30, 512, 256, 128, 64, 32, 16, 8, 4, 2, 1, 0};
 
 constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 64 < deg <= 512
-constexpr int kSegArcs = 2048;        // arcs per block segment (hub path)
-constexpr int kSegCap = 4096;         // per-block LDS table entries (>= 2 * kSegArcs)
+constexpr int kSegArcs = 512;         // arcs per unit of a seg-bin row (one wave)
 constexpr int kBinEvents = LPA_NKERNELS + 2;  // event marks per timed superstep
-constexpr int kHubChunk = 2048;       // global-list entries per hub-final work item
+constexpr int kCombWords = 2048;      // expected staged words per combine bucket
+constexpr int kCombSlots = 8192;      // LDS table slots of a combine block
+constexpr int kCombDirect = 6144;     // <= this many staged words: one block, no buckets
+constexpr int kMaxBucketsLg = 12;     // at most 4096 buckets per hub
+constexpr int kMaxBuckets = 1 << kMaxBucketsLg;
 constexpr int kChunkPos = 256;        // arc positions per scatter chunk of a changed vertex
 // replicated-label refresh: scatter the changed vertices' labels while they touch at
 // most this fraction of the arcs, otherwise rebuild al[] with one gather pass
 constexpr double kRebuildFrac = 0.25;
 
-struct Segment {
+struct Segment {   // one unit of a seg-bin row
   int64_t begin;  // first arc (local CSR index)
-  int32_t len;    // arcs in the segment (<= kSegArcs)
-  int32_t v;      // local vertex index; negative-encoded when the vertex spans >1 segment: -(hub+1)
+  int32_t len;    // arcs in the unit (<= kSegArcs) | (index of the unit within its row << 10)
+  int32_t v;      // local row (slot) index
 };
 
 // thread-local last error
@@ -100,22 +104,31 @@ struct lpa_graph {
   int64_t bin_begin[LPA_NBINS + 1] = {0};
   int64_t bin_arcs[LPA_NBINS] = {0};
 
-  // hub path
+  // hub path: rows longer than one segment.  Their segment tallies are staged
+  // as tally words in stage[rp[h] .. rp[h] + wcount[h]) and merged by the hub
+  // combine (lpa_hub.hip): small runs in a wave, mid-size runs in a block, large
+  // runs partitioned into label-hash buckets (scat[], same layout as stage[]).
   lpa::Segment* segs = nullptr;
   int64_t n_segs = 0;
-  int64_t n_hub = 0;        // vertices with > kSegArcs arcs (global merge)
-  int64_t* hub_off = nullptr;     // [n_hub + 1] table offsets
-  lpa::u64* gtab = nullptr;       // global hash tables
-  int32_t* glist = nullptr;       // touched-slot lists
-  int32_t* gcnt = nullptr;        // [n_hub] list lengths
-  lpa::u64* hub_best = nullptr;   // [n_hub] reduced tally word
-  lpa::u64* hub_items = nullptr;  // hub-final work items (hub << 32 | chunk)
-  int64_t n_hub_items = 0;
-  int64_t n_hub_segs = 0;         // hub segments are segs[0, n_hub_segs)
-  int64_t* hub_seg_off = nullptr; // [n_hub + 1] first segment of each hub
-  int32_t* hub_done = nullptr;    // [n_hub] combined in LDS this superstep
-  lpa::u64* stage = nullptr;      // [hub arcs] staged segment tally words
-  int32_t* seg_wcnt = nullptr;    // [n_hub_segs * 4] staged words per segment wave
+  int64_t n_hub = 0;              // rows with > kSegArcs arcs (= the seg bin)
+  lpa::u64* stage = nullptr;      // [hub arcs] staged unit tally words (unit j of row h:
+                                  //  stage[rp[h] + j*kSegArcs ...), ucnt[hub_uoff[h] + j] words)
+  int64_t* hub_uoff = nullptr;    // [n_hub + 1] first unit of each row (units = segs[])
+  int32_t* ucnt = nullptr;        // [n_segs] staged words of each unit
+  lpa::u64* scat = nullptr;       // [hub arcs] bucket-partitioned words
+  int32_t* hub_wcount = nullptr;  // [n_hub] staged words of a queued row (0 otherwise)
+  lpa::u64* hub_best = nullptr;   // [n_hub] reduced tally word (bucketed hubs)
+  int64_t* hub_hoff = nullptr;    // [n_hub + 1] first bucket counter of each hub
+  int32_t* ghist = nullptr;       // [n_hub_buckets] words per bucket
+  int32_t* gcur = nullptr;        // [n_hub_buckets] bucket offsets / scatter cursors
+  int32_t* hub_lists = nullptr;   // [3 n_hub] queued mid-size / bucketed / wave-path rows
+  int32_t* hub_lcnt = nullptr;    // [5] queue lengths: mid, bucketed, bucket items, chunk items,
+                                  //     wave path (rows k_hub_lanes handed on)
+  int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
+  lpa::u64* items_cb = nullptr;   // [n_hub_buckets] (hub << 32 | bucket)
+  lpa::u64* items_cc = nullptr;   // [n_hub_chunks]  (hub << 32 | 8-unit chunk)
+  int64_t n_hub_buckets = 0, n_hub_chunks = 0;
+  int32_t* dev_err = nullptr;     // [1] kernel-side error flags (checked after a call)
 
   // replicated neighbour labels (GraphX ReplicatedVertexView analogue):
   // al[i] = L_cur[col[i]]; kept current by scatter (few changes) or rebuild
@@ -156,6 +169,8 @@ int bits_for(uint64_t maxval);  // bits needed to represent maxval (0 -> 0)
 int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
                 uint32_t flags);
 int init_labels(lpa_graph* g);
+int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
+int launch_hub_combine(lpa_graph* g, int32_t* Lown);         // lpa_hub.hip
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
 
 // iteration (lpa_iter.hip)

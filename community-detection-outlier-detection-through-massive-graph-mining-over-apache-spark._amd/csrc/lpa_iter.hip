@@ -70,7 +70,7 @@ namespace {
 
 constexpr int kChunks = 8;    // 64-arc chunks per wave: a wave-bin row / a quarter segment
 constexpr u32 kNone = 0xFFFFFFFFu;  // empty lane
-static_assert(kSegArcs == 4 * 64 * kChunks, "a segment block's 4 waves own 64*kChunks arcs each");
+static_assert(kSegArcs == 64 * kChunks, "a unit is one batch of chunks");
 static_assert(kWaveMaxDeg == 64 * kChunks, "a wave-bin row fits one batch of chunks");
 
 __device__ __forceinline__ u32 ld_stream(const int32_t* p) {
@@ -394,316 +394,82 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
 }
 
 // ---------------------------------------------------------------------------
-// bin seg: deg > kWaveMaxDeg, one block per segment of <= kSegArcs arcs
-// (wave w owns arcs [w * 64 * kChunks, (w + 1) * 64 * kChunks) of the segment),
-// grid-stride over segments, software-pipelined one segment ahead.
+// bin seg: deg > kWaveMaxDeg.  The row is cut into 512-arc units; one wave per
+// unit (grid-stride over units, unit descriptors prefetched two units ahead and
+// labels one unit ahead, no block barriers, no returning atomics -- those would
+// make the wave wait for its prefetched loads).  The wave tallies its unit in
+// registers (peel) + its own LDS table and writes the unit's tally words to the
+// unit's own staging slots stage[begin ...) plus their count ucnt[unit]; the hub
+// combine (lpa_hub.hip) merges a row's units.  Unit: begin arc, row,
+// len | (unit index within the row << 10).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_lpa_seg(const int32_t* __restrict__ al,
-                                                 int32_t* __restrict__ Ln,
-                                                 const Segment* __restrict__ segs, int64_t nseg,
-                                                 u64* __restrict__ stage,
-                                                 int32_t* __restrict__ seg_wcnt) {
-  __shared__ u64 tab[kSegCap];
-  __shared__ uint16_t lst_all[4][kSegArcs / 4];
-  __shared__ u64 red[4];
+__device__ __forceinline__ Segment load_unit(const Segment* __restrict__ units, int64_t u, int64_t n) {
+  Segment d;
+  d.begin = 0;
+  d.len = 0;
+  d.v = 0;
+  if (u < n) d = units[u];
+  return d;
+}
+
+__global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ al,
+                                                   const Segment* __restrict__ units, int64_t nunits,
+                                                   u64* __restrict__ stage,
+                                                   int32_t* __restrict__ ucnt) {
+  constexpr int kCap = 2 * 64 * kChunks;
+  __shared__ u64 tab_all[4][kCap];
+  __shared__ uint16_t lst_all[4][64 * kChunks];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  u64* tab = tab_all[w];
   uint16_t* lst = lst_all[w];
-  for (int i = threadIdx.x; i < kSegCap; i += 256) tab[i] = 0ull;
-  __syncthreads();
+  for (int i = lane; i < kCap; i += 64) tab[i] = 0ull;
   const u64 lt = (1ull << lane) - 1ull;
-  int64_t si = blockIdx.x;
-  if (si >= nseg) return;  // uniform over the block
-  Segment sg = segs[si];
-  const int64_t woff = (int64_t)w * 64 * kChunks;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t u = (int64_t)blockIdx.x * 4 + w;
+  if (u >= nunits) return;  // no block-level barriers in this kernel
+  Segment d0 = load_unit(units, u, nunits);
+  Segment d1 = load_unit(units, u + stride, nunits);
   u32 lab[kChunks];
-  load_labels<kChunks>(lab, al, sg.begin + woff, sg.begin + sg.len, lane);
+  load_labels<kChunks>(lab, al, d0.begin, d0.begin + (d0.len & 1023), lane);
   while (true) {
-    const int64_t sn = si + gridDim.x;
-    const bool has_next = sn < nseg;
-    Segment sgn = sg;
-    if (has_next) sgn = segs[sn];
+    const int64_t un = u + stride;
+    const Segment d2 = load_unit(units, un + stride, nunits);
     u32 labn[kChunks];
-    if (has_next) {
-      load_labels<kChunks>(labn, al, sgn.begin + woff, sgn.begin + sgn.len, lane);
+    if (un < nunits) {
+      load_labels<kChunks>(labn, al, d1.begin, d1.begin + (d1.len & 1023), lane);
     } else {
 #pragma unroll
-      for (int u = 0; u < kChunks; ++u) labn[u] = kNone;
+      for (int k = 0; k < kChunks; ++k) labn[k] = kNone;
     }
-    int lg = ceil_log2(2u * (u32)sg.len);
-    lg = lg < 6 ? 6 : lg;
-    const u32 mask = (1u << lg) - 1u;
-    const int shift = 32 - lg;
-    int cnt = 0;
-#if LPA_DIAG == 1
-    {
-      u32 acc = 0;
-#pragma unroll
-      for (int u = 0; u < kChunks; ++u) acc ^= lab[u];
-      if (acc == 0x9E3779B1u) Ln[0] = (int32_t)acc;
-    }
-#else
-    {
-      Batch<kChunks> bt;
-      const int nch = (int)min((int64_t)kChunks, (sg.len - woff + 63) / 64);
-      peel_batch<kChunks>(bt, lab, nch > 0 ? nch : 0, lane);
-      if (LPA_DIAG != 3) hash_batch<kChunks>(tab, lst, cnt, shift, mask, bt, lab, nch > 0 ? nch : 0, lane, lt);
-    }
-#endif
-    __syncthreads();  // all tallies of the segment are in `tab`
-    if (sg.v >= 0) {
-      u64 best = 0ull;
-      for (int i = lane; i < cnt; i += 64) {
-        const int s = lst[i];
-        best = umax64(best, tab[s]);
-        tab[s] = 0ull;
-      }
-      best = wave_max_u64(best);
-      if (lane == 0) red[w] = best;
-      __syncthreads();
-      if (threadIdx.x == 0)
-        Ln[sg.v] = (int32_t)(~(u32)umax64(umax64(red[0], red[1]), umax64(red[2], red[3])));
+    const int len = d0.len & 1023;
+    const int nch = (len + 63) >> 6;
+    // staging slots of this unit: stage[begin .. begin + words) (words <= len)
+    u64* st = stage + d0.begin;
+    Batch<kChunks> bt;
+    peel_batch<kChunks>(bt, lab, nch, lane);
+    if (bt.nact == 0) {
+      // every vote is in a peel group: the unit's words are the peel groups
+      if (lane < bt.npeel) st[lane] = bt.pword;
+      if (lane == 0) ucnt[u] = bt.npeel;
     } else {
-      // hub segment: stage this wave's tallies with plain stores; k_hub_small /
-      // k_hub_merge combine the segments of the hub afterwards
-      u64* st = stage + sg.begin + woff;
+      int lg = ceil_log2(2u * (u32)len);
+      lg = lg < 6 ? 6 : lg;
+      int cnt = 0;
+      hash_batch<kChunks>(tab, lst, cnt, 32 - lg, (1u << lg) - 1u, bt, lab, nch, lane, lt);
       for (int i = lane; i < cnt; i += 64) {
         const int slt = lst[i];
         st[i] = tab[slt];
         tab[slt] = 0ull;
       }
-      if (lane == 0) seg_wcnt[si * 4 + w] = cnt;
+      if (lane == 0) ucnt[u] = cnt;
     }
-    __syncthreads();  // table slots cleared before the next segment
-    if (!has_next) break;
-    si = sn;
-    sg = sgn;
+    if (un >= nunits) break;
+    u = un;
+    d0 = d1;
+    d1 = d2;
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u) lab[u] = labn[u];
-  }
-}
-
-// Hub vertices (rows split over several segments).  Segment tallies are staged
-// as tally words; per hub:
-//   k_hub_small  total staged words <= kSegCap/2: combine them in an LDS table,
-//                write the label, mark the hub done (every converged superstep)
-//   k_hub_merge  otherwise: merge each segment's words into the hub's global
-//                hash (first probes back to back, batched list appends)
-//   k_lpa_hub_final / k_lpa_hub_write: reduce the global tables in 2048-entry
-//                work items (a giant hub spreads over many blocks)
-constexpr int kUnitWin = 2048;  // hub segment-wave units combined per window in k_hub_small
-
-__global__ __launch_bounds__(256) void k_hub_small(const Segment* __restrict__ segs,
-                                                   const int64_t* __restrict__ hub_seg_off,
-                                                   const int32_t* __restrict__ seg_wcnt,
-                                                   const u64* __restrict__ stage, int64_t n_hub,
-                                                   int32_t* __restrict__ Ln,
-                                                   int32_t* __restrict__ done) {
-  __shared__ u64 tab[kSegCap];
-  __shared__ uint16_t lst[kSegCap / 2];
-  __shared__ int upre[kUnitWin + 1];  // window prefix of staged words per unit
-  __shared__ int lcount;
-  __shared__ u64 red[4];
-  __shared__ int tred[4];   // per-wave word totals of the hub
-  __shared__ int wpre[4];   // per-wave sums of a unit window
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const u64 lt = (1ull << lane) - 1ull;
-  for (int i = threadIdx.x; i < kSegCap; i += 256) tab[i] = 0ull;
-  for (int64_t h = blockIdx.x; h < n_hub; h += gridDim.x) {
-    const int64_t s0 = hub_seg_off[h], s1 = hub_seg_off[h + 1];
-    const int nunits = (int)(s1 - s0) * 4;
-    const int32_t* wc = seg_wcnt + s0 * 4;
-    int t = 0;
-    for (int k = threadIdx.x; k < nunits; k += 256) t += wc[k];
-    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-    if (lane == 0) tred[w] = t;
-    if (threadIdx.x == 0) lcount = 0;
-    __syncthreads();
-    const int T = tred[0] + tred[1] + tred[2] + tred[3];
-    if (T > kSegCap / 2) {
-      if (threadIdx.x == 0) done[h] = 0;
-      __syncthreads();
-      continue;
-    }
-    int lg = ceil_log2(2u * (u32)(T > 0 ? T : 1));
-    lg = lg < 6 ? 6 : lg;
-    const u32 mask = (1u << lg) - 1u;
-    const int shift = 32 - lg;
-    if (T <= 4 * nunits) {
-      // few words per unit (a converged hub): one thread per unit
-      for (int k = threadIdx.x; k < nunits; k += 256) {
-        const int n = wc[k];
-        const u64* st = stage + segs[s0 + k / 4].begin + (int64_t)(k % 4) * 64 * kChunks;
-        for (int i = 0; i < n; ++i) {
-          const u64 word = st[i];
-          const int slot = lds_insert(tab, shift, mask, ~(u32)word, (u32)(word >> 32));
-          if (slot >= 0) lst[atomicAdd(&lcount, 1)] = (uint16_t)slot;
-        }
-      }
-      __syncthreads();  // all inserts and list appends done before the finalize
-    } else
-    for (int k0 = 0; k0 < nunits; k0 += kUnitWin) {
-      const int nu = min(kUnitWin, nunits - k0);
-      // exclusive prefix of the window's unit counts (thread-contiguous stripes)
-      const int per = (nu + 255) / 256;
-      const int j0 = min(nu, (int)threadIdx.x * per), j1 = min(nu, j0 + per);
-      int loc = 0;
-      for (int j = j0; j < j1; ++j) loc += wc[k0 + j];
-      int incl = loc;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o;
-      }
-      if (lane == 63) wpre[w] = incl;
-      __syncthreads();
-      int run = incl - loc;
-      for (int i = 0; i < w; ++i) run += wpre[i];
-      for (int j = j0; j < j1; ++j) {
-        upre[j] = run;
-        run += wc[k0 + j];
-      }
-      if (threadIdx.x == 255) upre[nu] = run;
-      __syncthreads();
-      const int nw = upre[nu];
-      // one staged word per thread per round: find its unit by binary search
-      for (int q = threadIdx.x; q < nw; q += 256) {
-        int lo = 0, hi = nu - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (upre[mid] <= q) lo = mid; else hi = mid - 1;
-        }
-        const int k = k0 + lo;
-        const u64 word = stage[segs[s0 + k / 4].begin + (int64_t)(k % 4) * 64 * kChunks + (q - upre[lo])];
-        const int slot = lds_insert(tab, shift, mask, ~(u32)word, (u32)(word >> 32));
-        const u64 cm = __ballot(slot >= 0);
-        int basei = 0;
-        if (cm) {
-          const int first = __ffsll((unsigned long long)cm) - 1;
-          if (lane == first) basei = atomicAdd(&lcount, __popcll(cm));
-          basei = __builtin_amdgcn_readlane(basei, first);
-        }
-        if (slot >= 0) lst[basei + __popcll(cm & lt)] = (uint16_t)slot;
-      }
-      __syncthreads();
-    }
-    u64 best = 0ull;
-    for (int i = threadIdx.x; i < lcount; i += 256) {
-      const int slt = lst[i];
-      best = umax64(best, tab[slt]);
-      tab[slt] = 0ull;
-    }
-    best = wave_max_u64(best);
-    if (lane == 0) red[w] = best;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      Ln[h] = (int32_t)(~(u32)umax64(umax64(red[0], red[1]), umax64(red[2], red[3])));
-      done[h] = 1;
-    }
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(256) void k_hub_merge(const Segment* __restrict__ segs,
-                                                   int64_t n_hub_segs,
-                                                   const int32_t* __restrict__ seg_wcnt,
-                                                   const u64* __restrict__ stage,
-                                                   const int32_t* __restrict__ done,
-                                                   u64* __restrict__ gtab, int32_t* __restrict__ glist,
-                                                   int32_t* __restrict__ gcnt,
-                                                   const int64_t* __restrict__ hub_off) {
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u64 lt = (1ull << lane) - 1ull;
-  for (int64_t si = blockIdx.x; si < n_hub_segs; si += gridDim.x) {
-    const Segment sg = segs[si];
-    const int64_t h = -(int64_t)sg.v - 1;
-    if (done[h]) continue;
-    const int cnt = seg_wcnt[si * 4 + w];
-    const u64* st = stage + sg.begin + (int64_t)w * 64 * kChunks;
-    const int64_t off = hub_off[h];
-    const u32 cap = (u32)(hub_off[h + 1] - off);
-    const int gshift = 32 - ceil_log2(cap);
-    u64* gt = gtab + off;
-    u64 word[kChunks], old[kChunks];
-    u32 hs[kChunks];
-#pragma unroll
-    for (int r = 0; r < kChunks; ++r) {
-      const int i = r * 64 + lane;
-      word[r] = i < cnt ? st[i] : 0ull;
-    }
-#pragma unroll
-    for (int r = 0; r < kChunks; ++r) {
-      hs[r] = hash_slot(~(u32)word[r], gshift);
-      old[r] = 0ull;
-      if (LPA_DIAG != 2 && word[r] != 0ull) old[r] = atomicCAS(&gt[hs[r]], 0ull, word[r]);
-    }
-    int claimed[kChunks];
-    int total = 0;
-#pragma unroll
-    for (int r = 0; r < kChunks; ++r) {
-      claimed[r] = -1;
-      if (LPA_DIAG != 2 && word[r] != 0ull)
-        claimed[r] = global_resolve(gt, cap - 1u, word[r], hs[r], old[r]);
-      total += __popcll(__ballot(claimed[r] >= 0));
-    }
-    if (total > 0) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(gcnt + h, total);
-      base = __builtin_amdgcn_readlane(base, 0);
-#pragma unroll
-      for (int r = 0; r < kChunks; ++r) {
-        const u64 cm = __ballot(claimed[r] >= 0);
-        if (claimed[r] >= 0) glist[off + base + __popcll(cm & lt)] = claimed[r];
-        base += __popcll(cm);
-      }
-    }
-  }
-}
-
-// one work item per kHubChunk listed slots of a hub (items precomputed from the
-// table capacity; items past the hub's current list length exit at once)
-__global__ __launch_bounds__(256) void k_lpa_hub_final(u64* __restrict__ gtab,
-                                                       const int32_t* __restrict__ glist,
-                                                       const int32_t* __restrict__ gcnt,
-                                                       const int64_t* __restrict__ hub_off,
-                                                       const u64* __restrict__ items, int64_t n_items,
-                                                       u64* __restrict__ hbest) {
-  __shared__ u64 red[4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
-    const u64 item = items[it];
-    const int64_t h = (int64_t)(item >> 32);
-    const int begin = (int)(u32)item * kHubChunk;
-    const int n = gcnt[h];
-    if (begin >= n) continue;  // uniform over the block
-    const int end = min(n, begin + kHubChunk);
-    const int64_t off = hub_off[h];
-    u64 best = 0ull;
-    for (int i = begin + threadIdx.x; i < end; i += 256) {
-      const int32_t slt = glist[off + i];
-      best = umax64(best, gtab[off + slt]);
-      gtab[off + slt] = 0ull;
-    }
-    best = wave_max_u64(best);
-    if (lane == 0) red[w] = best;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      best = umax64(umax64(red[0], red[1]), umax64(red[2], red[3]));
-      atomicMax(&hbest[h], best);
-    }
-    __syncthreads();
-  }
-}
-
-__global__ void k_lpa_hub_write(u64* __restrict__ hbest, int32_t* __restrict__ gcnt,
-                                const int32_t* __restrict__ done, int32_t* __restrict__ Ln,
-                                int64_t n_hub) {
-  for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_hub;
-       h += (int64_t)gridDim.x * blockDim.x) {
-    if (!done[h]) Ln[h] = (int32_t)(~(u32)hbest[h]);
-    hbest[h] = 0ull;
-    gcnt[h] = 0;
+    for (int k = 0; k < kChunks; ++k) lab[k] = labn[k];
   }
 }
 
@@ -807,15 +573,38 @@ __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chun
   }
 }
 
-// many changes: al[i] = L_next[col[i]]
+// many changes: al[i] = L_next[col[i]].  Random label gathers: each thread
+// keeps 8 gathers in flight (two int4 column quads), streams col/al non-temporally.
+template <bool kIfWanted>
 __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __restrict__ counters,
                                                     const int32_t* __restrict__ col, int64_t arcs,
                                                     const int32_t* __restrict__ Ln,
                                                     int32_t* __restrict__ al) {
-  if (!rebuild_wanted(counters, arcs)) return;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < arcs;
-       i += (int64_t)gridDim.x * blockDim.x)
-    al[i] = Ln[__builtin_nontemporal_load(col + i)];
+  if (kIfWanted && !rebuild_wanted(counters, arcs)) return;
+  const int64_t n4 = arcs >> 2;
+  const v4i* __restrict__ c4 = reinterpret_cast<const v4i*>(col);
+  v4i* __restrict__ a4 = reinterpret_cast<v4i*>(al);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; q + stride < n4; q += 2 * stride) {
+    const v4i c0 = __builtin_nontemporal_load(c4 + q);
+    const v4i c1 = __builtin_nontemporal_load(c4 + q + stride);
+    v4i r0, r1;
+    r0.x = Ln[c0.x]; r0.y = Ln[c0.y]; r0.z = Ln[c0.z]; r0.w = Ln[c0.w];
+    r1.x = Ln[c1.x]; r1.y = Ln[c1.y]; r1.z = Ln[c1.z]; r1.w = Ln[c1.w];
+    __builtin_nontemporal_store(r0, a4 + q);
+    __builtin_nontemporal_store(r1, a4 + q + stride);
+  }
+  if (q < n4) {
+    const v4i c0 = __builtin_nontemporal_load(c4 + q);
+    v4i r0;
+    r0.x = Ln[c0.x]; r0.y = Ln[c0.y]; r0.z = Ln[c0.z]; r0.w = Ln[c0.w];
+    __builtin_nontemporal_store(r0, a4 + q);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (arcs & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    al[i] = Ln[col[i]];
+  }
 }
 
 __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __restrict__ new_of,
@@ -842,31 +631,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
   };
   LPA_TRY(mark(0));
   if (g->n_segs > 0) {
-    hipLaunchKernelGGL(k_lpa_seg, dim3(cap_grid(g->n_segs, 1024)), dim3(256), 0, s, g->al, Lown,
-                       g->segs, g->n_segs, g->stage, g->seg_wcnt);
+    hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
+                       g->al, g->segs, g->n_segs, g->stage, g->ucnt);
     LPA_HIP(hipGetLastError());
     LPA_TRACE_POINT("seg");
   }
   LPA_TRY(mark(1));
-  if (g->n_hub > 0) {
-    hipLaunchKernelGGL(k_hub_small, dim3(cap_grid(g->n_hub, 1024)), dim3(256), 0, s, g->segs,
-                       g->hub_seg_off, g->seg_wcnt, g->stage, g->n_hub, Lown, g->hub_done);
-    LPA_HIP(hipGetLastError());
-    LPA_TRACE_POINT("hub_small");
-    hipLaunchKernelGGL(k_hub_merge, dim3(cap_grid(g->n_hub_segs, 2048)), dim3(256), 0, s, g->segs,
-                       g->n_hub_segs, g->seg_wcnt, g->stage, g->hub_done, g->gtab, g->glist,
-                       g->gcnt, g->hub_off);
-    LPA_HIP(hipGetLastError());
-    LPA_TRACE_POINT("hub_merge");
-    hipLaunchKernelGGL(k_lpa_hub_final, dim3(cap_grid(g->n_hub_items, 2048)), dim3(256), 0, s,
-                       g->gtab, g->glist, g->gcnt, g->hub_off, g->hub_items, g->n_hub_items,
-                       g->hub_best);
-    LPA_HIP(hipGetLastError());
-    LPA_TRACE_POINT("hub_final");
-    hipLaunchKernelGGL(k_lpa_hub_write, dim3(cap_grid((g->n_hub + 255) / 256, 1024)), dim3(256), 0,
-                       s, g->hub_best, g->gcnt, g->hub_done, Lown, g->n_hub);
-    LPA_HIP(hipGetLastError());
-  }
+  LPA_TRY(launch_hub_combine(g, Lown));
+  LPA_TRACE_POINT("hub_combine");
   LPA_TRY(mark(2));
 #define LPA_WAVE_LAUNCH(BIN, NC)                                                              \
   {                                                                                           \
@@ -919,8 +691,8 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
                      g->cpos, Ln, g->al, g->arcs);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
-  hipLaunchKernelGGL(k_al_rebuild, dim3(cap_grid((g->arcs + 255) / 256, 8192)), dim3(256), 0, s,
-                     g->counters, g->col, g->arcs, Ln, g->al);
+  hipLaunchKernelGGL(k_al_rebuild<true>, dim3(cap_grid((g->arcs / 4 + 511) / 512, 8192)), dim3(256),
+                     0, s, g->counters, g->col, g->arcs, Ln, g->al);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -966,6 +738,15 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
   }
   if (timed) LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS + 1], s));
   LPA_HIP(hipStreamSynchronize(s));
+  if (n > 0) {
+    int32_t err = 0;
+    LPA_HIP(hipMemcpy(&err, g->dev_err, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) {
+      set_error("superstep kernel capacity overflow (flags 0x%x): a hub combine bucket exceeded "
+                "its LDS table", err);
+      return LPA_EOVERFLOW;
+    }
+  }
   if (timed) {
     st->iters = n;
     st->n_iter_ms = nt;
@@ -986,6 +767,14 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     LPA_HIP(hipEventElapsedTime(&tot, g->ev[2 * LPA_STATS_MAX_ITERS], g->ev[2 * LPA_STATS_MAX_ITERS + 1]));
     st->total_ms = tot;
   }
+  return LPA_OK;
+}
+
+int rebuild_arc_labels(lpa_graph* g) {
+  if (g->arcs == 0) return LPA_OK;
+  hipLaunchKernelGGL(k_al_rebuild<false>, dim3(cap_grid((g->arcs / 4 + 511) / 512, 8192)), dim3(256),
+                     0, g->stream, nullptr, g->col, g->arcs, g->lab[g->cur], g->al);
+  LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
 

@@ -35,6 +35,7 @@ extern "C" {
 #define LPA_ENODEV (-19)   /* no HIP device / bad device ordinal                */
 #define LPA_EHIP (-1000)   /* HIP runtime error                                  */
 #define LPA_ERCCL (-2000)  /* RCCL error                                         */
+#define LPA_EOVERFLOW (-75) /* kernel-side capacity overflow (hub combine table) */
 
 /* lpa_graph_create* flags */
 #define LPA_INPUT_DEVICE 0x1u /* src/dst are device pointers on `device`        */

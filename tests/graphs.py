@@ -51,3 +51,29 @@ def degree_mix(seed=0, hubs=(600, 2100, 4500, 9000), n_low=3000, extra=20000):
 def random_multigraph(V, m, seed):
     rng = np.random.default_rng(seed)
     return V, rng.integers(0, V, size=m).astype(np.int32), rng.integers(0, V, size=m).astype(np.int32)
+
+
+def comb_bucket(labels, lg):
+    """k_hub_combine's label-hash bucket (lpa_iter.hip comb_bucket)."""
+    x = (labels.astype(np.uint64) * np.uint64(0x85EBCA77)) & np.uint64(0xFFFFFFFF)
+    return (x >> np.uint64(32 - lg)).astype(np.int64) if lg else np.zeros(labels.shape, np.int64)
+
+
+def giant_hub(seed=0, n_plain=200000, n_skew=20000, lg=7):
+    """Hub 0 with n_plain + n_skew distinct neighbours (iteration 1: every staged
+    word distinct -> 2^lg combine buckets), n_skew of which hash into ONE bucket
+    (-> that bucket needs sub-bucket passes).  One skewed neighbour carries three
+    parallel edges, so the hub's mode is decided inside the overloaded bucket; two
+    plain neighbours carry two, testing the cross-bucket maximum."""
+    rng = np.random.default_rng(seed)
+    V = 4 * (n_plain + n_skew) + 1
+    ids = np.arange(1, V, dtype=np.int64)
+    b = comb_bucket(ids, lg)
+    skew = rng.permutation(ids[b == 3])[:n_skew]
+    rest = rng.permutation(ids[b != 3])[:n_plain]
+    nb = np.concatenate([skew, rest, [skew[5]] * 2, [rest[7], rest[9]]])
+    s = np.zeros(nb.size, np.int64)
+    # a sparse random background so the leaves are not all degree 1
+    bs = rng.integers(1, V, size=V // 2)
+    bd = rng.integers(1, V, size=V // 2)
+    return V, np.concatenate([s, bs]).astype(np.int32), np.concatenate([nb, bd]).astype(np.int32)

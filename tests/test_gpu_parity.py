@@ -4,7 +4,7 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from graphs import degree_mix, random_multigraph, star, two_cliques
+from graphs import degree_mix, giant_hub, random_multigraph, star, two_cliques
 
 pytestmark = pytest.mark.gpu
 
@@ -87,13 +87,26 @@ def test_degree_mix_all_bins(gfa, oracle, seed):
     V, s, d = degree_mix(seed)
     with gfa.Graph(s, d, V) as g:
         info = g.info()
-        assert info["hub_vertices"] >= 2 and info["bin_vertices"]["seg"] > info["hub_vertices"]
+        assert info["hub_vertices"] >= 2 and info["bin_vertices"]["seg"] == info["hub_vertices"]
         assert all(info["bin_vertices"][b] > 0 for b in
                    ("w8", "w4", "w2", "g64", "g32", "g16", "g8", "g4", "g2", "g1")), info["bin_vertices"]
     _, hist, _ = oracle.lpa(V, s, d, 6, per_iter=True)
     got = _per_step(gfa, V, s, d, 6)
     for t in range(6):
         assert np.array_equal(got[t], hist[t]), f"seed {seed} superstep {t + 1}"
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_hub_combine_buckets_and_subpasses(gfa, oracle, seed):
+    """A 220K-arc hub whose staged words are all distinct in superstep 1 (128
+    combine buckets, one of them overloaded -> sub-bucket passes); the mode sits
+    in the overloaded bucket.  Bit-exact per superstep."""
+    V, s, d = giant_hub(seed)
+    _, hist, _ = oracle.lpa(V, s, d, 4, per_iter=True)
+    got = _per_step(gfa, V, s, d, 4)
+    for t in range(4):
+        bad = np.flatnonzero(got[t] != hist[t])
+        assert bad.size == 0, f"superstep {t + 1}: {bad.size} differ, first {bad[:5]}"
 
 
 @pytest.mark.parametrize("V,m,seed", [(50, 2000, 3), (3000, 60000, 4), (20000, 40000, 5)])

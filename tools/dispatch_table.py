@@ -1,26 +1,36 @@
-"""Per-dispatch durations (ms) of the LPA kernels from a rocprofv3 kernel trace."""
-import csv
+"""Per-superstep kernel durations (ms) from a rocprofv3 kernel trace.
+
+A superstep starts at each k_lpa_units dispatch (the first tally kernel); every
+dispatch until the next one (hub combine, bins, diff, al refresh) belongs to it.
+Columns: one per superstep in launch order; rows: kernels; last row: sum.
+"""
 import collections
+import csv
+import re
 import sys
 
-path = sys.argv[1]
-rows = list(csv.DictReader(open(path)))
-d = collections.defaultdict(list)
-keys = ('k_lpa_seg', 'k_hub_small', 'k_hub_merge', 'k_lpa_hub_final', 'k_lpa_hub_write',
-        'k_lpa_wave<8>', 'k_lpa_wave<4>', 'k_lpa_wave<2>', 'k_lpa_group<64>', 'k_lpa_group<32>',
-        'k_lpa_group<16>', 'k_lpa_group<8>', 'k_lpa_group<4>', 'k_lpa_group<2>', 'k_lpa_group<1>',
-        'k_diff', 'k_al_scatter', 'k_al_rebuild', 'k_lpa_iter1')
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
+
+
+def short(name):
+    m = re.search(r'(k_[A-Za-z0-9_]+(<[^>]*>)?)', name)
+    return m.group(1) if m else name[:30]
+
+
+steps = []
 for r in rows:
-    name = r['Kernel_Name']
-    for k in keys:
-        if k + '(' in name or (k in name and '<' not in k):
-            d[k].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6)
-            break
-tot = None
-for k in keys:
-    if k in d:
-        v = d[k]
-        print(f"{k:18s}", ' '.join(f"{x:6.3f}" for x in v))
-        tot = v if tot is None else [a + b for a, b in zip(tot, v)]
-if tot:
-    print(f"{'sum':18s}", ' '.join(f"{x:6.3f}" for x in tot))
+    n = short(r['Kernel_Name'])
+    if n == 'k_lpa_units':
+        steps.append(collections.OrderedDict())
+    if not steps:
+        continue
+    ms = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6
+    steps[-1][n] = steps[-1].get(n, 0.0) + ms
+names = []
+for st in steps:
+    for n in st:
+        if n not in names:
+            names.append(n)
+for n in names:
+    print(f"{n:18s}", ' '.join(f"{st.get(n, 0.0):6.3f}" for st in steps))
+print(f"{'sum':18s}", ' '.join(f"{sum(st.values()):6.3f}" for st in steps))
