@@ -310,6 +310,68 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
 // software-pipelined: the next vertex's labels stream in while the current one is
 // tallied (row bounds two vertices ahead).  Per-wave LDS table of 2 * 64 * NC.
 // ---------------------------------------------------------------------------
+struct RowSpan {
+  int64_t b, e;
+};
+
+__device__ __forceinline__ RowSpan row_span(const int64_t* __restrict__ rp, int64_t v, int64_t vend) {
+  RowSpan r;
+  r.b = 0;
+  r.e = 0;
+  if (v < vend) {
+    r.b = rp[v];
+    r.e = rp[v + 1];
+  }
+  return r;
+}
+
+// unconditional loads of a row's labels (address clamped into the row)
+template <int NC>
+__device__ __forceinline__ void row_load(u32 (&raw)[NC], const int32_t* __restrict__ al,
+                                         const RowSpan& r, int lane) {
+  const int d = (int)(r.e - r.b);
+  const int last = d > 0 ? d - 1 : 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int off = c * 64 + lane;
+    raw[c] = ld_stream(al + r.b + (off < last ? off : last));
+  }
+}
+
+template <int NC>
+__device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r, int64_t v,
+                                          int32_t* __restrict__ Ln, u64* tab, uint16_t* lst, int lane,
+                                          u64 lt) {
+  const int d = (int)(r.e - r.b);
+  if (d == 0) return;
+  u32 lab[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) lab[c] = c * 64 + lane < d ? raw[c] : kNone;
+  int lg = ceil_log2(2u * (u32)d);
+  lg = lg < 6 ? 6 : lg;
+  const int nch = (d + 63) >> 6;
+  Batch<NC> bt;
+  peel_batch<NC>(bt, lab, nch, lane);
+  if (bt.nact == 0) {
+    // every vote is in a peel group: the mode is their maximum, no LDS needed
+    if (lane == 0) Ln[v] = (int32_t)(~(u32)bt.pbest);
+  } else {
+    int cnt = 0;
+    hash_batch<NC>(tab, lst, cnt, 32 - lg, (1u << lg) - 1u, bt, lab, nch, lane, lt);
+    u64 best = 0ull;
+    for (int i = lane; i < cnt; i += 64) {
+      const int sl = lst[i];
+      best = umax64(best, tab[sl]);
+      tab[sl] = 0ull;
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) Ln[v] = (int32_t)(~(u32)best);
+  }
+}
+
+// bins w2 / w4 / w8 (64 < deg <= 64 * NC): one wave per row, grid-stride; three
+// label register sets in an unrolled ring (labels two rows ahead, no set copied
+// while its loads are in flight), row bounds three rows ahead.
 template <int NC>
 __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp,
                                                   const int32_t* __restrict__ al,
@@ -327,69 +389,126 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t v = vbeg + (int64_t)blockIdx.x * 4 + w;
   if (v >= vend) return;  // no block-level barriers in this kernel
-  int64_t b = rp[v], e = rp[v + 1];
-  int64_t bn = 0, en = 0;
-  if (v + stride < vend) {
-    bn = rp[v + stride];
-    en = rp[v + stride + 1];
-  }
-  u32 lab[NC];
-  load_labels<NC>(lab, al, b, e, lane);
+  RowSpan s0 = row_span(rp, v, vend), s1 = row_span(rp, v + stride, vend),
+          s2 = row_span(rp, v + 2 * stride, vend);
+  u32 ra[NC], rb[NC], rc[NC];
+  row_load<NC>(ra, al, s0, lane);
+  row_load<NC>(rb, al, s1, lane);
   while (true) {
-    const int64_t vn = v + stride, vnn = vn + stride;
-    const bool has_next = vn < vend;
-    int64_t bnn = 0, enn = 0;
-    if (vnn < vend) {
-      bnn = rp[vnn];
-      enn = rp[vnn + 1];
-    }
-    u32 labn[NC];
-    if (has_next) {
-      load_labels<NC>(labn, al, bn, en, lane);
+    row_load<NC>(rc, al, s2, lane);
+    RowSpan s3 = row_span(rp, v + 3 * stride, vend);
+    row_tally<NC>(ra, s0, v, Ln, tab, lst, lane, lt);
+    v += stride;
+    if (v >= vend) break;
+    row_load<NC>(ra, al, s3, lane);
+    RowSpan s4 = row_span(rp, v + 3 * stride, vend);
+    row_tally<NC>(rb, s1, v, Ln, tab, lst, lane, lt);
+    v += stride;
+    if (v >= vend) break;
+    row_load<NC>(rb, al, s4, lane);
+    RowSpan s5 = row_span(rp, v + 3 * stride, vend);
+    row_tally<NC>(rc, s2, v, Ln, tab, lst, lane, lt);
+    v += stride;
+    if (v >= vend) break;
+    s0 = s3;
+    s1 = s4;
+    s2 = s5;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bins g64 .. g8 (4 < deg <= 64): persistent waves over batches of RB = 512 / G
+// consecutive rows (G lanes per row, 8 chunks of 64 lanes per batch).  Per batch
+// a wave issues ONE row-offset load (lane r holds rp[r0 + r]) and then all 8
+// label loads per lane at once; the next batch's labels and the batch after
+// next's offsets stream in while the current batch is tallied (ballot peel
+// within each G-lane group).  (A three-set unrolled ring, as in k_lpa_units,
+// measured slower here: the per-batch tally is long enough to cover one batch.)
+// ---------------------------------------------------------------------------
+template <int G>
+__device__ __forceinline__ void rows_rp(const int64_t* __restrict__ rp, int64_t r0, int64_t vend,
+                                        int lane, int64_t& rpl, int64_t& rpe) {
+  constexpr int RB = 512 / G;
+  const int64_t i = r0 + lane;
+  rpl = (lane < RB && i <= vend) ? rp[i] : 0;
+  rpe = rp[min(r0 + RB, vend)];
+}
+
+template <int G>
+__device__ __forceinline__ void rows_labels(u32 (&lab)[kChunks], const int32_t* __restrict__ al,
+                                            int64_t r0, int64_t vend, int64_t rpl, int64_t rpe,
+                                            int lane) {
+  constexpr int RB = 512 / G;
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) {
+    const int rl = c * (64 / G) + lane / G;
+    const int j = lane & (G - 1);
+    // both shuffles run on every lane (a bpermute from a lane that is masked
+    // off returns garbage), then the batch end is selected
+    const int64_t b = __shfl(rpl, rl, 64);
+    const int64_t en = __shfl(rpl, rl + 1 < 64 ? rl + 1 : 63, 64);
+    const int64_t e = rl + 1 < RB ? en : rpe;
+    lab[c] = (r0 + rl < vend && j < e - b) ? ld_stream(al + b + j) : kNone;
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp,
+                                                  const int32_t* __restrict__ al,
+                                                  int32_t* __restrict__ Ln, int64_t vbeg,
+                                                  int64_t vend) {
+  static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "lane width");
+  constexpr int RB = 512 / G;  // rows per batch
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nb = (vend - vbeg + RB - 1) / RB;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t bi = (int64_t)blockIdx.x * 4 + w;
+  if (bi >= nb) return;  // no block-level barriers in this kernel
+  int64_t rpl0, rpe0, rpl1 = 0, rpe1 = 0;
+  rows_rp<G>(rp, vbeg + bi * RB, vend, lane, rpl0, rpe0);
+  if (bi + stride < nb) rows_rp<G>(rp, vbeg + (bi + stride) * RB, vend, lane, rpl1, rpe1);
+  u32 lab[kChunks];
+  rows_labels<G>(lab, al, vbeg + bi * RB, vend, rpl0, rpe0, lane);
+  const int gbase = lane & ~(G - 1);
+  const u64 gm = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
+  while (true) {
+    const int64_t bn = bi + stride;
+    int64_t rpl2 = 0, rpe2 = 0;
+    if (bn + stride < nb) rows_rp<G>(rp, vbeg + (bn + stride) * RB, vend, lane, rpl2, rpe2);
+    u32 labn[kChunks];
+    if (bn < nb) {
+      rows_labels<G>(labn, al, vbeg + bn * RB, vend, rpl1, rpe1, lane);
     } else {
 #pragma unroll
-      for (int u = 0; u < NC; ++u) labn[u] = kNone;
+      for (int c = 0; c < kChunks; ++c) labn[c] = kNone;
     }
-    const int d = (int)(e - b);
-    int lg = ceil_log2(2u * (u32)d);
-    lg = lg < 6 ? 6 : lg;
-    const u32 mask = (1u << lg) - 1u;
-    const int shift = 32 - lg;
-    const int nch = (d + 63) >> 6;
-#if LPA_DIAG == 1
-    {
-      u32 acc = 0;
+    const int64_t r0 = vbeg + bi * RB;
 #pragma unroll
-      for (int u = 0; u < NC; ++u) acc ^= lab[u];
-      if (acc == 0x9E3779B1u) Ln[0] = (int32_t)acc;
-    }
-#else
-    Batch<NC> bt;
-    peel_batch<NC>(bt, lab, nch, lane);
-    if (bt.nact == 0 || LPA_DIAG == 3) {
-      // every vote is in a peel group: the mode is their maximum, no LDS needed
-      if (lane == 0) Ln[v] = (int32_t)(~(u32)bt.pbest);
-    } else {
-      int cnt = 0;
-      hash_batch<NC>(tab, lst, cnt, shift, mask, bt, lab, nch, lane, lt);
+    for (int c = 0; c < kChunks; ++c) {
+      const u32 lb = lab[c];
+      u64 act = __ballot(lb != kNone);
       u64 best = 0ull;
-      for (int i = lane; i < cnt; i += 64) {
-        const int s = lst[i];
-        best = umax64(best, tab[s]);
-        tab[s] = 0ull;
+      while (act) {
+        const u64 my = (act >> gbase) & gm;
+        const int lead = gbase + (my ? (__ffsll((unsigned long long)my) - 1) : 0);
+        const u32 x = (u32)__shfl((int)lb, lead, 64);
+        const u64 mm = __ballot(((act >> lane) & 1ull) && lb == x);
+        const u32 cn = (u32)__popcll((mm >> gbase) & gm);
+        if (my) best = umax64(best, tally(cn, x));
+        act &= ~mm;
       }
-      best = wave_max_u64(best);
-      if (lane == 0) Ln[v] = (int32_t)(~(u32)best);
+      const int64_t row = r0 + c * (64 / G) + lane / G;
+      if ((lane & (G - 1)) == 0 && row < vend && best) Ln[row] = (int32_t)(~(u32)best);
     }
-#endif
-    if (!has_next) break;
-    v = vn;
-    b = bn;
-    e = en;
-    bn = bnn;
-    en = enn;
+    if (bn >= nb) break;
+    bi = bn;
+    rpl0 = rpl1;
+    rpe0 = rpe1;
+    rpl1 = rpl2;
+    rpe1 = rpe2;
 #pragma unroll
-    for (int u = 0; u < NC; ++u) lab[u] = labn[u];
+    for (int c = 0; c < kChunks; ++c) lab[c] = labn[c];
   }
 }
 
@@ -412,6 +531,51 @@ __device__ __forceinline__ Segment load_unit(const Segment* __restrict__ units, 
   return d;
 }
 
+// unconditional loads (the address is clamped into the unit; lanes past the unit's
+// end are masked at use time), so the compiler can count vmcnt exactly
+__device__ __forceinline__ void unit_load(u32 (&raw)[kChunks], const int32_t* __restrict__ al,
+                                          const Segment& d, int lane) {
+  const int len = d.len & 1023;
+  const int last = len > 0 ? len - 1 : 0;
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) {
+    const int off = c * 64 + lane;
+    raw[c] = ld_stream(al + d.begin + (off < last ? off : last));
+  }
+}
+
+// tally one unit whose labels are in `raw` (loaded earlier)
+__device__ __forceinline__ void unit_tally(const u32 (&raw)[kChunks], const Segment& d, int64_t u,
+                                           u64* __restrict__ stage, int32_t* __restrict__ ucnt,
+                                           u64* tab, uint16_t* lst, int lane, u64 lt) {
+  const int len = d.len & 1023;
+  if (len == 0) return;
+  u32 lab[kChunks];
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) lab[c] = c * 64 + lane < len ? raw[c] : kNone;
+  const int nch = (len + 63) >> 6;
+  // staging slots of this unit: stage[begin .. begin + words) (words <= len)
+  u64* st = stage + d.begin;
+  Batch<kChunks> bt;
+  peel_batch<kChunks>(bt, lab, nch, lane);
+  if (bt.nact == 0) {
+    // every vote is in a peel group: the unit's words are the peel groups
+    if (lane < bt.npeel) st[lane] = bt.pword;
+    if (lane == 0) ucnt[u] = bt.npeel;
+  } else {
+    int lg = ceil_log2(2u * (u32)len);
+    lg = lg < 6 ? 6 : lg;
+    int cnt = 0;
+    hash_batch<kChunks>(tab, lst, cnt, 32 - lg, (1u << lg) - 1u, bt, lab, nch, lane, lt);
+    for (int i = lane; i < cnt; i += 64) {
+      const int slt = lst[i];
+      st[i] = tab[slt];
+      tab[slt] = 0ull;
+    }
+    if (lane == 0) ucnt[u] = cnt;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ al,
                                                    const Segment* __restrict__ units, int64_t nunits,
                                                    u64* __restrict__ stage,
@@ -428,48 +592,33 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t u = (int64_t)blockIdx.x * 4 + w;
   if (u >= nunits) return;  // no block-level barriers in this kernel
+  // three register sets in a ring, unrolled so no set is ever copied (a copy of a
+  // register with a load in flight would wait for it): labels two units ahead
   Segment d0 = load_unit(units, u, nunits);
   Segment d1 = load_unit(units, u + stride, nunits);
-  u32 lab[kChunks];
-  load_labels<kChunks>(lab, al, d0.begin, d0.begin + (d0.len & 1023), lane);
+  Segment d2 = load_unit(units, u + 2 * stride, nunits);
+  u32 ra[kChunks], rb[kChunks], rc[kChunks];
+  unit_load(ra, al, d0, lane);
+  unit_load(rb, al, d1, lane);
   while (true) {
-    const int64_t un = u + stride;
-    const Segment d2 = load_unit(units, un + stride, nunits);
-    u32 labn[kChunks];
-    if (un < nunits) {
-      load_labels<kChunks>(labn, al, d1.begin, d1.begin + (d1.len & 1023), lane);
-    } else {
-#pragma unroll
-      for (int k = 0; k < kChunks; ++k) labn[k] = kNone;
-    }
-    const int len = d0.len & 1023;
-    const int nch = (len + 63) >> 6;
-    // staging slots of this unit: stage[begin .. begin + words) (words <= len)
-    u64* st = stage + d0.begin;
-    Batch<kChunks> bt;
-    peel_batch<kChunks>(bt, lab, nch, lane);
-    if (bt.nact == 0) {
-      // every vote is in a peel group: the unit's words are the peel groups
-      if (lane < bt.npeel) st[lane] = bt.pword;
-      if (lane == 0) ucnt[u] = bt.npeel;
-    } else {
-      int lg = ceil_log2(2u * (u32)len);
-      lg = lg < 6 ? 6 : lg;
-      int cnt = 0;
-      hash_batch<kChunks>(tab, lst, cnt, 32 - lg, (1u << lg) - 1u, bt, lab, nch, lane, lt);
-      for (int i = lane; i < cnt; i += 64) {
-        const int slt = lst[i];
-        st[i] = tab[slt];
-        tab[slt] = 0ull;
-      }
-      if (lane == 0) ucnt[u] = cnt;
-    }
-    if (un >= nunits) break;
-    u = un;
-    d0 = d1;
-    d1 = d2;
-#pragma unroll
-    for (int k = 0; k < kChunks; ++k) lab[k] = labn[k];
+    unit_load(rc, al, d2, lane);
+    Segment d3 = load_unit(units, u + 3 * stride, nunits);
+    unit_tally(ra, d0, u, stage, ucnt, tab, lst, lane, lt);
+    u += stride;
+    if (u >= nunits) break;
+    unit_load(ra, al, d3, lane);
+    Segment d4 = load_unit(units, u + 3 * stride, nunits);
+    unit_tally(rb, d1, u, stage, ucnt, tab, lst, lane, lt);
+    u += stride;
+    if (u >= nunits) break;
+    unit_load(rb, al, d4, lane);
+    Segment d5 = load_unit(units, u + 3 * stride, nunits);
+    unit_tally(rc, d2, u, stage, ucnt, tab, lst, lane, lt);
+    u += stride;
+    if (u >= nunits) break;
+    d0 = d3;
+    d1 = d4;
+    d2 = d5;
   }
 }
 
@@ -662,13 +811,26 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
     }                                                                                        \
     LPA_TRY(mark(BIN + 2));                                                                  \
   }
+#define LPA_ROWS_LAUNCH(BIN, G)                                                              \
+  {                                                                                          \
+    const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
+    if (n > 0) {                                                                             \
+      const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
+      hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0, s, \
+                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                          \
+      LPA_HIP(hipGetLastError());                                                            \
+      LPA_TRACE_POINT("rows" #G);                                                            \
+    }                                                                                        \
+    LPA_TRY(mark(BIN + 2));                                                                  \
+  }
   LPA_WAVE_LAUNCH(BIN_W8, 8)
   LPA_WAVE_LAUNCH(BIN_W4, 4)
   LPA_WAVE_LAUNCH(BIN_W2, 2)
-  LPA_GROUP_LAUNCH(BIN_G64, 64)
-  LPA_GROUP_LAUNCH(BIN_G32, 32)
-  LPA_GROUP_LAUNCH(BIN_G16, 16)
-  LPA_GROUP_LAUNCH(BIN_G8, 8)
+  LPA_ROWS_LAUNCH(BIN_G64, 64)
+  LPA_ROWS_LAUNCH(BIN_G32, 32)
+  LPA_ROWS_LAUNCH(BIN_G16, 16)
+  LPA_ROWS_LAUNCH(BIN_G8, 8)
+#undef LPA_ROWS_LAUNCH
   LPA_GROUP_LAUNCH(BIN_G4, 4)
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
