@@ -12,7 +12,8 @@
 //   T <= 512            k_hub_small   one wave: words in registers, weighted
 //                                     ballot peel, residual in a per-wave LDS table
 //                                     (converged rows: one word per unit)
-//   512 < T <= 6144     k_hub_mid     one block: 8192-slot LDS table
+//   512 < T <= 6144     k_hub_mid     one block: LDS table of 2048 / 4096 / 8192
+//                                     slots for T <= 1024 / 2048 / 6144
 //   T > 6144            K = 2^ceil(log2(T / 2048)) label-hash buckets:
 //                       k_hub_count   per 8-unit chunk: bucket histogram
 //                       k_hub_scan    per hub: bucket offsets
@@ -147,17 +148,24 @@ __global__ __launch_bounds__(256) void k_hub_lanes(int64_t h_begin, int64_t h_en
   }
 }
 
-// queue row h (T staged words) for k_hub_mid or the bucket path
+// queue row h (T staged words) for k_hub_mid (three table sizes) or the bucket
+// path.  lists: [0] mid T <= 1024, [n] bucketed, [2n] wave path, [3n] mid <= 2048,
+// [4n] mid <= 6144; lcnt: 0 mid1, 1 bucketed, 2 bucket items, 3 chunk items,
+// 4 wave path, 5 mid2, 6 mid3
 __device__ __forceinline__ void queue_row(int64_t h, int T, int nu, int lane,
-                                          int32_t* __restrict__ wcount, int32_t* __restrict__ listB,
-                                          int32_t* __restrict__ listC, int32_t* __restrict__ lcnt,
+                                          int32_t* __restrict__ wcount, int32_t* __restrict__ lists,
+                                          int64_t n_hub, int32_t* __restrict__ lcnt,
                                           u64* __restrict__ itemsCB, u64* __restrict__ itemsCC) {
   if (lane == 0) {
     wcount[h] = T;
-    if (T <= kCombDirect) {
-      listB[atomicAdd(&lcnt[0], 1)] = (int32_t)h;
+    if (T <= 1024) {
+      lists[atomicAdd(&lcnt[0], 1)] = (int32_t)h;
+    } else if (T <= 2048) {
+      lists[3 * n_hub + atomicAdd(&lcnt[5], 1)] = (int32_t)h;
+    } else if (T <= kCombDirect) {
+      lists[4 * n_hub + atomicAdd(&lcnt[6], 1)] = (int32_t)h;
     } else {
-      listC[atomicAdd(&lcnt[1], 1)] = (int32_t)h;
+      lists[n_hub + atomicAdd(&lcnt[1], 1)] = (int32_t)h;
     }
   }
   if (T > kCombDirect) {
@@ -218,15 +226,14 @@ __device__ __forceinline__ int weighted_peel(const u64 (&wv)[NC], u64 (&act)[NC]
 //                                      (giant converged rows)
 //   otherwise                          queued with T in wcount[h]
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, const int64_t* __restrict__ rp,
+__global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, int64_t n_hub,
+                                                   const int64_t* __restrict__ rp,
                                                    const int64_t* __restrict__ uoff,
                                                    const int32_t* __restrict__ ucnt,
                                                    const u64* __restrict__ stage,
                                                    int32_t* __restrict__ wcount,
                                                    int32_t* __restrict__ Ln,
-                                                   const int32_t* __restrict__ listW,
-                                                   int32_t* __restrict__ listB,
-                                                   int32_t* __restrict__ listC,
+                                                   int32_t* __restrict__ lists,
                                                    int32_t* __restrict__ lcnt,
                                                    u64* __restrict__ itemsCB,
                                                    u64* __restrict__ itemsCC) {
@@ -243,7 +250,7 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, const int64_t
   const int64_t nq = h_lane + lcnt[4];
   const int64_t stride = (int64_t)gridDim.x * 4;
   for (int64_t q = (int64_t)blockIdx.x * 4 + w; q < nq; q += stride) {
-    const int64_t h = q < h_lane ? q : (int64_t)listW[q - h_lane];
+    const int64_t h = q < h_lane ? q : (int64_t)lists[2 * n_hub + (q - h_lane)];
     const RowUnits ru = row_units(rp, uoff, h);
     const int nu = ru.nu;
     const int32_t* uc = ucnt + ru.u0;
@@ -301,14 +308,14 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, const int64_t
       }
       best = wave_max_u64(best);
       if (ovf) {
-        queue_row(h, T, nu, lane, wcount, listB, listC, lcnt, itemsCB, itemsCC);
+        queue_row(h, T, nu, lane, wcount, lists, n_hub, lcnt, itemsCB, itemsCC);
       } else if (lane == 0) {
         Ln[h] = (int32_t)(~(u32)best);
       }
       continue;
     }
     if (nu > kSmallWords || T > kSmallWords) {
-      queue_row(h, T, nu, lane, wcount, listB, listC, lcnt, itemsCB, itemsCC);
+      queue_row(h, T, nu, lane, wcount, lists, n_hub, lcnt, itemsCB, itemsCC);
       continue;
     }
     u64 wv[NC];
@@ -385,12 +392,10 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, const int64_t
 
 // Tally the words of units [j0, j1) of a row whose labels pass `keep` into the
 // block's LDS table (kCombSlots slots).  Returns the block-uniform maximum.
-template <typename Keep>
+template <int kLg, typename Keep>
 __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __restrict__ uc, int j0,
                                  int j1, Keep keep, u64* tab, uint16_t* lst, int* lcount, u64* redw,
                                  int32_t* err) {
-  constexpr int kLg = 13;
-  static_assert((1 << kLg) == kCombSlots, "combine table size");
   constexpr int NC = kSegArcs / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) *lcount = 0;
@@ -499,26 +504,28 @@ __device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64
 // ---------------------------------------------------------------------------
 // 512 < T <= kCombDirect: one block per queued row (grid-stride over the queue).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_hub_mid(const int32_t* __restrict__ listB,
-                                                 const int32_t* __restrict__ lcnt,
+template <int kLg>
+__global__ __launch_bounds__(256) void k_hub_mid(const int32_t* __restrict__ list,
+                                                 const int32_t* __restrict__ lcnt, int which,
                                                  const int64_t* __restrict__ rp,
                                                  const int64_t* __restrict__ uoff,
                                                  const int32_t* __restrict__ ucnt,
                                                  const u64* __restrict__ stage,
                                                  int32_t* __restrict__ wcount,
                                                  int32_t* __restrict__ Ln, int32_t* __restrict__ err) {
-  __shared__ u64 tab[kCombSlots];
-  __shared__ uint16_t lst[kCombSlots];
+  constexpr int kSlots = 1 << kLg;
+  __shared__ u64 tab[kSlots];
+  __shared__ uint16_t lst[kSlots];
   __shared__ int lcount;
   __shared__ u64 redw[4];
-  const int nB = lcnt[0];
+  const int nB = lcnt[which];
   if ((int)blockIdx.x >= nB) return;
-  for (int i = threadIdx.x; i < kCombSlots; i += 256) tab[i] = 0ull;
+  for (int i = threadIdx.x; i < kSlots; i += 256) tab[i] = 0ull;
   for (int q = blockIdx.x; q < nB; q += gridDim.x) {
-    const int64_t h = listB[q];
+    const int64_t h = list[q];
     const RowUnits ru = row_units(rp, uoff, h);
-    const u64 best = block_tally_units(stage + ru.sbase, ucnt + ru.u0, 0, ru.nu,
-                                       [](u32) { return true; }, tab, lst, &lcount, redw, err);
+    const u64 best = block_tally_units<kLg>(stage + ru.sbase, ucnt + ru.u0, 0, ru.nu,
+                                            [](u32) { return true; }, tab, lst, &lcount, redw, err);
     if (threadIdx.x == 0) {
       Ln[h] = (int32_t)(~(u32)best);
       wcount[h] = 0;
@@ -792,8 +799,8 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   LPA_TRY(dev_alloc(g, (void**)&g->hub_best, sizeof(u64) * n));
   LPA_TRY(dev_alloc(g, (void**)&g->ghist, sizeof(int32_t) * nbk));
   LPA_TRY(dev_alloc(g, (void**)&g->gcur, sizeof(int32_t) * nbk));
-  LPA_TRY(dev_alloc(g, (void**)&g->hub_lists, sizeof(int32_t) * 3 * n));
-  LPA_TRY(dev_alloc(g, (void**)&g->hub_lcnt, sizeof(int32_t) * 5));
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_lists, sizeof(int32_t) * 5 * n));
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_lcnt, sizeof(int32_t) * 8));
   {
     // rows [hub_lane_begin, n_hub) have <= kLaneUnits units (degree-descending order)
     int64_t* d_pos = nullptr;
@@ -816,9 +823,9 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown) {
   const int64_t n = g->n_hub;
   if (n == 0) return LPA_OK;
   hipStream_t s = g->stream;
-  int32_t* listB = g->hub_lists;
+  int32_t* lists = g->hub_lists;
   int32_t* listC = g->hub_lists + n;
-  LPA_HIP(hipMemsetAsync(g->hub_lcnt, 0, sizeof(int32_t) * 5, s));
+  LPA_HIP(hipMemsetAsync(g->hub_lcnt, 0, sizeof(int32_t) * 8, s));
   const int64_t hl = g->hub_lane_begin;
   int32_t* listW = g->hub_lists + 2 * n;
   if (hl < n) {
@@ -826,13 +833,19 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown) {
                        g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, listW, g->hub_lcnt);
     LPA_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, hl, g->rp, g->hub_uoff, g->ucnt,
-                     g->stage, g->hub_wcount, Lown, listW, listB, listC, g->hub_lcnt, g->items_cb,
-                     g->items_cc);
+  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, hl, n, g->rp, g->hub_uoff, g->ucnt,
+                     g->stage, g->hub_wcount, Lown, lists, g->hub_lcnt, g->items_cb, g->items_cc);
   LPA_HIP(hipGetLastError());
-  const unsigned nbl = grid_cap(n, 1024);
-  hipLaunchKernelGGL(k_hub_mid, dim3(nbl), dim3(256), 0, s, listB, g->hub_lcnt, g->rp, g->hub_uoff,
-                     g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
+  hipLaunchKernelGGL(k_hub_mid<11>, dim3(grid_cap(n, 2048)), dim3(256), 0, s, lists, g->hub_lcnt, 0,
+                     g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_hub_mid<12>, dim3(grid_cap(n, 1024)), dim3(256), 0, s, lists + 3 * n,
+                     g->hub_lcnt, 5, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
+                     g->dev_err);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_hub_mid<13>, dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,
+                     g->hub_lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
+                     g->dev_err);
   LPA_HIP(hipGetLastError());
   const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
   hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, s, g->items_cc, g->hub_lcnt, g->rp,

@@ -8,7 +8,7 @@ i=0
 while read -r COUNTERS; do
   [ -z "$COUNTERS" ] && continue
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $COUNTERS --kernel-include-regex "k_lpa|k_hub|k_diff|k_al" -d gpurun_out/${TAG}_$i -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/${TAG}_${i}_bench.json 2> gpurun_out/${TAG}_${i}.err || { echo "pass $i failed"; tail -5 gpurun_out/${TAG}_${i}.err; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $COUNTERS --kernel-include-regex "${KREGEX:-k_lpa|k_hub|k_diff|k_al}" -d gpurun_out/${TAG}_$i -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/${TAG}_${i}_bench.json 2> gpurun_out/${TAG}_${i}.err || { echo "pass $i failed"; tail -5 gpurun_out/${TAG}_${i}.err; exit 1; }
 done <<'LIST'
 FETCH_SIZE TCC_HIT_sum
 TCC_MISS_sum WRITE_SIZE
