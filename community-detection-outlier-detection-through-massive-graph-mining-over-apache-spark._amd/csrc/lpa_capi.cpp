@@ -2,6 +2,7 @@
 // error reporting, RCCL communicator setup.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -115,6 +116,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
     return LPA_ENOMEM;
   }
   g->device = device;
+  if (const char* f = getenv("LPA_REBUILD_FRAC")) g->rebuild_frac = atof(f);
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {

@@ -139,6 +139,7 @@ struct lpa_graph {
   // per-superstep change bookkeeping (device)
   int64_t n_chunk_cap = 0;
   lpa::u64* chunks = nullptr;   // changed-vertex position chunks: (u << 32 | chunk index)
+  double rebuild_frac = lpa::kRebuildFrac;  // LPA_REBUILD_FRAC overrides (tuning experiments)
   unsigned long long* counters = nullptr;  // [0] chunk count, [1] dirty arcs, [2] changed vertices
 
   // original edge list kept for the outlier stage (device, dense ids)

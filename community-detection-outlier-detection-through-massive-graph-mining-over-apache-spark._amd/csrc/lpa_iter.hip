@@ -13,7 +13,7 @@
 //   2. exchange (P > 1) RCCL allgather of the owned label slices.
 //   3. refresh  diff L_next vs L_cur over all vertex slots; the changed vertices'
 //               new labels are scattered into al[] through the CSC position index
-//               (cptr/cpos) while they touch <= kRebuildFrac of the arcs, otherwise
+//               (cptr/cpos) while they touch <= rebuild_frac of the arcs, otherwise
 //               al[] is rebuilt with one gather pass al[i] = L_next[col[i]].
 //   Every superstep tallies every arc of every vertex; the refresh only keeps the
 //   replica exact, so labels are bit-identical to the plain gather formulation.
@@ -696,29 +696,58 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
   }
 }
 
-__device__ __forceinline__ bool rebuild_wanted(const unsigned long long* counters, int64_t arcs) {
-  return (double)counters[1] > kRebuildFrac * (double)arcs;
+// rebuild al[] when the changed vertices touch more than `thr` arcs (host-set)
+__device__ __forceinline__ bool rebuild_wanted(const unsigned long long* counters, int64_t thr) {
+  return (int64_t)counters[1] > thr;
 }
 
-// few changes: al[cpos[p]] = L_next[u] for the positions of each changed u
+// few changes: al[cpos[p]] = L_next[u] for the positions of each changed u.
+// A chunk is (u << 32 | k): positions [cptr[u] + 256 k, ...).  A wave takes 64
+// chunks, one per lane (independent loads of cptr and the label): chunks of <= 16
+// positions are written by their own lane (4 stores in flight per step), longer
+// ones by the whole wave (coalesced cpos).
 __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chunks,
                                                     const unsigned long long* __restrict__ counters,
                                                     const int64_t* __restrict__ cptr,
                                                     const uint32_t* __restrict__ cpos,
                                                     const int32_t* __restrict__ Ln,
-                                                    int32_t* __restrict__ al, int64_t arcs) {
-  if (rebuild_wanted(counters, arcs)) return;
+                                                    int32_t* __restrict__ al, int64_t thr) {
+  if (rebuild_wanted(counters, thr)) return;
   const int64_t nchunks = (int64_t)counters[0];
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t c = wid; c < nchunks; c += nw) {
-    const u64 ch = chunks[c];
-    const int64_t u = (int64_t)(ch >> 32);
-    const int64_t b = cptr[u] + (int64_t)(u32)ch * kChunkPos;
-    const int64_t e = min(cptr[u + 1], b + kChunkPos);
-    const int32_t lab = Ln[u];
-    for (int64_t p = b + lane; p < e; p += 64) al[cpos[p]] = lab;
+  for (int64_t c0 = wid * 64; c0 < nchunks; c0 += nw * 64) {
+    const int64_t c = c0 + lane;
+    int64_t b = 0;
+    int n = 0;
+    int32_t lab = 0;
+    if (c < nchunks) {
+      const u64 ch = chunks[c];
+      const int64_t u = (int64_t)(ch >> 32);
+      const int64_t rb = cptr[u], re = cptr[u + 1];
+      b = rb + (int64_t)(u32)ch * kChunkPos;
+      n = (int)min((int64_t)kChunkPos, re - b);
+      lab = Ln[u];
+    }
+    const int ns = n <= 16 ? n : 0;
+    for (int k = 0; k < ns; k += 4) {
+      uint32_t p[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) p[t] = k + t < ns ? cpos[b + k + t] : 0u;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (k + t < ns) al[p[t]] = lab;
+    }
+    u64 big = __ballot(n > 16);
+    while (big) {
+      const int bl = __ffsll((unsigned long long)big) - 1;
+      big &= big - 1ull;
+      const int64_t bb = __shfl(b, bl, 64);
+      const int bn = __shfl(n, bl, 64);
+      const int32_t bv = __shfl(lab, bl, 64);
+      for (int i = lane; i < bn; i += 64) al[cpos[bb + i]] = bv;
+    }
   }
 }
 
@@ -726,10 +755,11 @@ __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chun
 // keeps 8 gathers in flight (two int4 column quads), streams col/al non-temporally.
 template <bool kIfWanted>
 __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __restrict__ counters,
-                                                    const int32_t* __restrict__ col, int64_t arcs,
+                                                    int64_t thr, const int32_t* __restrict__ col,
+                                                    int64_t arcs,
                                                     const int32_t* __restrict__ Ln,
                                                     int32_t* __restrict__ al) {
-  if (kIfWanted && !rebuild_wanted(counters, arcs)) return;
+  if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   const int64_t n4 = arcs >> 2;
   const v4i* __restrict__ c4 = reinterpret_cast<const v4i*>(col);
   v4i* __restrict__ a4 = reinterpret_cast<v4i*>(al);
@@ -849,12 +879,13 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
                      g->counters);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("diff");
+  const int64_t thr = (int64_t)(g->rebuild_frac * (double)g->arcs);
   hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, g->counters, g->cptr,
-                     g->cpos, Ln, g->al, g->arcs);
+                     g->cpos, Ln, g->al, thr);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   hipLaunchKernelGGL(k_al_rebuild<true>, dim3(cap_grid((g->arcs / 4 + 511) / 512, 8192)), dim3(256),
-                     0, s, g->counters, g->col, g->arcs, Ln, g->al);
+                     0, s, g->counters, thr, g->col, g->arcs, Ln, g->al);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -935,7 +966,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
 int rebuild_arc_labels(lpa_graph* g) {
   if (g->arcs == 0) return LPA_OK;
   hipLaunchKernelGGL(k_al_rebuild<false>, dim3(cap_grid((g->arcs / 4 + 511) / 512, 8192)), dim3(256),
-                     0, g->stream, nullptr, g->col, g->arcs, g->lab[g->cur], g->al);
+                     0, g->stream, nullptr, (int64_t)0, g->col, g->arcs, g->lab[g->cur], g->al);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
