@@ -59,6 +59,11 @@ void destroy(lpa_graph* g) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : g->bin_ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& st : g->aux_stream)
+    if (st) (void)hipStreamDestroy(st);
+  if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
+  for (auto& e : g->ev_join)
+    if (e) (void)hipEventDestroy(e);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   if (g->own_stream) (void)hipStreamDestroy(g->own_stream);
   delete g;
@@ -117,6 +122,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   }
   g->device = device;
   if (const char* f = getenv("LPA_REBUILD_FRAC")) g->rebuild_frac = atof(f);
+  if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {
@@ -129,6 +135,19 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
       return LPA_EHIP;
     }
     g->stream = g->own_stream;
+  }
+  {
+    hipError_t e = hipSuccess;
+    for (auto& st : g->aux_stream)
+      if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming);
+    for (auto& ev : g->ev_join)
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      set_error("stream/event creation: %s", hipGetErrorString(e));
+      destroy(g);
+      return LPA_EHIP;
+    }
   }
   if (nranks > 1 && comm_id) {
     ncclUniqueId id;

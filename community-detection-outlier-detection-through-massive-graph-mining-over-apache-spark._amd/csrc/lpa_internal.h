@@ -30,7 +30,8 @@ constexpr int kBinMaxDeg[LPA_NBINS] = {1 << 30, 512, 256, 128, 64, 32, 16, 8, 4,
 
 constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 64 < deg <= 512
 constexpr int kSegArcs = 512;         // arcs per unit of a seg-bin row (one wave)
-constexpr int kBinEvents = LPA_NKERNELS + 2;  // event marks per timed superstep
+constexpr int kTallyEv = 2 * (LPA_NKERNELS - 1);  // events bracketing each tally kernel
+constexpr int kBinEvents = kTallyEv + 3;           // + join, exchange, refresh marks
 constexpr int kCombWords = 2048;      // expected staged words per combine bucket
 constexpr int kCombSlots = 8192;      // LDS table slots of a combine block
 constexpr int kCombDirect = 6144;     // <= this many staged words: one block, no buckets
@@ -80,6 +81,8 @@ struct lpa_graph {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  hipStream_t aux_stream[2] = {nullptr, nullptr};  // concurrent tally bins
+  hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   int32_t rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
 
@@ -140,6 +143,7 @@ struct lpa_graph {
   int64_t n_chunk_cap = 0;
   lpa::u64* chunks = nullptr;   // changed-vertex position chunks: (u << 32 | chunk index)
   double rebuild_frac = lpa::kRebuildFrac;  // LPA_REBUILD_FRAC overrides (tuning experiments)
+  int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   unsigned long long* counters = nullptr;  // [0] chunk count, [1] dirty arcs, [2] changed vertices
 
   // original edge list kept for the outlier stage (device, dense ids)

@@ -786,6 +786,49 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
   }
 }
 
+// Same with the labels of the kHotLabels highest-degree vertices (slots
+// [0, kHotLabels) at P = 1: 30-40 % of all arc targets on R-MAT) served from LDS:
+// the rebuild is bound by the L2 request rate of its 4-B random gathers, and every
+// gather served by the block's LDS copy is one L2 request fewer.  One 1024-thread
+// block per CU, 128 KB of LDS.
+constexpr int kHotLabels = 32768;
+template <bool kIfWanted>
+__global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long long* __restrict__ counters,
+                                                         int64_t thr, const int32_t* __restrict__ col,
+                                                         int64_t arcs, const int32_t* __restrict__ Ln,
+                                                         int32_t nhot, int32_t* __restrict__ al) {
+  if (kIfWanted && !rebuild_wanted(counters, thr)) return;
+  __shared__ int32_t hot[kHotLabels];
+  for (int i = threadIdx.x; i < nhot; i += 1024) hot[i] = Ln[i];
+  __syncthreads();
+  const u32 nh = (u32)nhot;
+  auto lab = [&](int c) -> int32_t { return (u32)c < nh ? hot[c] : Ln[c]; };
+  const int64_t n4 = arcs >> 2;
+  const v4i* __restrict__ c4 = reinterpret_cast<const v4i*>(col);
+  v4i* __restrict__ a4 = reinterpret_cast<v4i*>(al);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; q + stride < n4; q += 2 * stride) {
+    const v4i c0 = __builtin_nontemporal_load(c4 + q);
+    const v4i c1 = __builtin_nontemporal_load(c4 + q + stride);
+    v4i r0, r1;
+    r0.x = lab(c0.x); r0.y = lab(c0.y); r0.z = lab(c0.z); r0.w = lab(c0.w);
+    r1.x = lab(c1.x); r1.y = lab(c1.y); r1.z = lab(c1.z); r1.w = lab(c1.w);
+    __builtin_nontemporal_store(r0, a4 + q);
+    __builtin_nontemporal_store(r1, a4 + q + stride);
+  }
+  if (q < n4) {
+    const v4i c0 = __builtin_nontemporal_load(c4 + q);
+    v4i r0;
+    r0.x = lab(c0.x); r0.y = lab(c0.y); r0.z = lab(c0.z); r0.w = lab(c0.w);
+    __builtin_nontemporal_store(r0, a4 + q);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (arcs & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    al[i] = Ln[col[i]];
+  }
+}
+
 __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __restrict__ new_of,
                                int64_t V, int32_t* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < V;
@@ -800,58 +843,68 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
 
 // tally kernels of one superstep; bev marks: 0 start, k+1 after kernel k
 // (0 seg, 1 hub_final + hub_write, 2 wave, 3..7 g16..g1)
+// Tally kernels of one superstep on three streams (the bins write disjoint
+// label ranges and only read al[]): main = seg units -> hub combine, aux0 = the
+// wave bins, aux1 = the row/group bins; they join on the main stream.  Running
+// them concurrently hides the ~2-5 us launch gap of each dependent kernel and the
+// tails of the small bins.  bev (nullable): events 2k / 2k+1 bracket tally kernel
+// k on its own stream (0 units, 1 hub combine, 2..11 bins w8 .. g1).
 int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
-  // bev marks: 0 start, k+1 after kernel k (0 seg, 1 hub kernels, 2..11 bins w8..g1)
   hipStream_t s = g->stream;
+  hipStream_t sb = g->aux_stream[0], sc = g->aux_stream[1];
   const int64_t* bb = g->bin_begin;
-  auto mark = [&](int i) -> int {
-    if (bev) LPA_HIP(hipEventRecord(bev[i], s));
+  LPA_HIP(hipEventRecord(g->ev_fork, s));
+  LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
+  LPA_HIP(hipStreamWaitEvent(sc, g->ev_fork, 0));
+  auto mark = [&](int i, hipStream_t st) -> int {
+    if (bev) LPA_HIP(hipEventRecord(bev[i], st));
     return LPA_OK;
   };
-  LPA_TRY(mark(0));
+  LPA_TRY(mark(0, s));
   if (g->n_segs > 0) {
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
                        g->al, g->segs, g->n_segs, g->stage, g->ucnt);
     LPA_HIP(hipGetLastError());
     LPA_TRACE_POINT("seg");
   }
-  LPA_TRY(mark(1));
+  LPA_TRY(mark(1, s));
+  LPA_TRY(mark(2, s));
   LPA_TRY(launch_hub_combine(g, Lown));
   LPA_TRACE_POINT("hub_combine");
-  LPA_TRY(mark(2));
+  LPA_TRY(mark(3, s));
 #define LPA_WAVE_LAUNCH(BIN, NC)                                                              \
   {                                                                                           \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                  \
+    LPA_TRY(mark(2 * (BIN + 1), sb));                                                         \
     if (n > 0) {                                                                              \
-      hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, s,   \
+      hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, sb,  \
                          g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                          \
       LPA_HIP(hipGetLastError());                                                             \
-      LPA_TRACE_POINT("wave" #NC);                                                            \
     }                                                                                         \
-    LPA_TRY(mark(BIN + 2));                                                                   \
+    LPA_TRY(mark(2 * (BIN + 1) + 1, sb));                                                     \
   }
 #define LPA_GROUP_LAUNCH(BIN, G)                                                             \
   {                                                                                          \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
+    LPA_TRY(mark(2 * (BIN + 1), sc));                                                        \
     if (n > 0) {                                                                             \
       hipLaunchKernelGGL(k_lpa_group<G>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
-                         s, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                      \
+                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                     \
       LPA_HIP(hipGetLastError());                                                            \
-      LPA_TRACE_POINT("group" #G);                                                           \
     }                                                                                        \
-    LPA_TRY(mark(BIN + 2));                                                                  \
+    LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
   }
 #define LPA_ROWS_LAUNCH(BIN, G)                                                              \
   {                                                                                          \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
+    LPA_TRY(mark(2 * (BIN + 1), sc));                                                        \
     if (n > 0) {                                                                             \
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
-      hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0, s, \
-                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                          \
+      hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
+                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                     \
       LPA_HIP(hipGetLastError());                                                            \
-      LPA_TRACE_POINT("rows" #G);                                                            \
     }                                                                                        \
-    LPA_TRY(mark(BIN + 2));                                                                  \
+    LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
   }
   LPA_WAVE_LAUNCH(BIN_W8, 8)
   LPA_WAVE_LAUNCH(BIN_W4, 4)
@@ -860,12 +913,43 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
   LPA_ROWS_LAUNCH(BIN_G32, 32)
   LPA_ROWS_LAUNCH(BIN_G16, 16)
   LPA_ROWS_LAUNCH(BIN_G8, 8)
-#undef LPA_ROWS_LAUNCH
   LPA_GROUP_LAUNCH(BIN_G4, 4)
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
+#undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
+  LPA_HIP(hipEventRecord(g->ev_join[0], sb));
+  LPA_HIP(hipEventRecord(g->ev_join[1], sc));
+  LPA_HIP(hipStreamWaitEvent(s, g->ev_join[0], 0));
+  LPA_HIP(hipStreamWaitEvent(s, g->ev_join[1], 0));
+  return LPA_OK;
+}
+
+// al[] rebuild: the LDS hot-label kernel on a single-GPU handle (hub slots are
+// [0, kHotLabels) there), the plain one otherwise
+int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L) {
+  hipStream_t s = g->stream;
+  if (g->nranks == 1 && g->rebuild_hot) {
+    int dev_cus = 256;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
+    const int32_t nhot = (int32_t)(g->vpad < kHotLabels ? g->vpad : kHotLabels);
+    if (if_wanted)
+      hipLaunchKernelGGL(k_al_rebuild_hot<true>, dim3(dev_cus), dim3(1024), 0, s, g->counters, thr,
+                         g->col, g->arcs, L, nhot, g->al);
+    else
+      hipLaunchKernelGGL(k_al_rebuild_hot<false>, dim3(dev_cus), dim3(1024), 0, s, g->counters, thr,
+                         g->col, g->arcs, L, nhot, g->al);
+  } else {
+    const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
+    if (if_wanted)
+      hipLaunchKernelGGL(k_al_rebuild<true>, dim3(grid), dim3(256), 0, s, g->counters, thr, g->col,
+                         g->arcs, L, g->al);
+    else
+      hipLaunchKernelGGL(k_al_rebuild<false>, dim3(grid), dim3(256), 0, s, g->counters, thr, g->col,
+                         g->arcs, L, g->al);
+  }
+  LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
 
@@ -884,8 +968,7 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
                      g->cpos, Ln, g->al, thr);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
-  hipLaunchKernelGGL(k_al_rebuild<true>, dim3(cap_grid((g->arcs / 4 + 511) / 512, 8192)), dim3(256),
-                     0, s, g->counters, thr, g->col, g->arcs, Ln, g->al);
+  LPA_TRY(launch_rebuild(g, true, thr, Ln));
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -904,8 +987,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       if (!g->bin_ev[i]) LPA_HIP(hipEventCreate(&g->bin_ev[i]));
     LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS], s));
   }
-  // per timed superstep t, marks bin_ev[t*kBinEvents + i]: 0 start, k+1 after
-  // tally kernel k (k < LPA_NKERNELS - 1), then after the exchange, after the refresh
+  // per timed superstep t, bin_ev[t*kBinEvents + i]: 2k / 2k+1 around tally kernel
+  // k (k < LPA_NKERNELS - 1), then kTallyEv after the join, +1 after the exchange,
+  // +2 after the refresh
   for (int32_t t = 0; t < n; ++t) {
     const int32_t* Lc = g->lab[g->cur];
     int32_t* Ln = g->lab[g->cur ^ 1];
@@ -914,6 +998,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     hipEvent_t* bev = tt ? &g->bin_ev[t * kBinEvents] : nullptr;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
     LPA_TRY(launch_tally(g, Lown, bev));
+    if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
     if (g->nranks > 1 && g->comm) {
       ncclResult_t r = ncclAllGather(Lown, Ln, (size_t)g->slice, ncclInt32, g->comm, s);
       if (r != ncclSuccess) {
@@ -921,10 +1006,10 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
         return LPA_ERCCL;
       }
     }
-    if (tt) LPA_HIP(hipEventRecord(bev[LPA_NKERNELS], s));
+    if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
     LPA_TRY(launch_refresh(g, Lc, Ln));
     if (tt) {
-      LPA_HIP(hipEventRecord(bev[LPA_NKERNELS + 1], s));
+      LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));
       LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     }
     g->cur ^= 1;
@@ -948,12 +1033,12 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       hipEvent_t* bev = &g->bin_ev[t * kBinEvents];
       float ms;
       for (int k = 0; k < LPA_NKERNELS - 1; ++k) {
-        LPA_HIP(hipEventElapsedTime(&ms, bev[k], bev[k + 1]));
+        LPA_HIP(hipEventElapsedTime(&ms, bev[2 * k], bev[2 * k + 1]));
         st->kernel_ms[k] += ms;
       }
-      LPA_HIP(hipEventElapsedTime(&ms, bev[LPA_NKERNELS - 1], bev[LPA_NKERNELS]));
+      LPA_HIP(hipEventElapsedTime(&ms, bev[kTallyEv], bev[kTallyEv + 1]));
       st->exchange_ms += ms;
-      LPA_HIP(hipEventElapsedTime(&ms, bev[LPA_NKERNELS], bev[LPA_NKERNELS + 1]));
+      LPA_HIP(hipEventElapsedTime(&ms, bev[kTallyEv + 1], bev[kTallyEv + 2]));
       st->kernel_ms[LPA_NKERNELS - 1] += ms;
     }
     float tot;
@@ -965,10 +1050,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
 
 int rebuild_arc_labels(lpa_graph* g) {
   if (g->arcs == 0) return LPA_OK;
-  hipLaunchKernelGGL(k_al_rebuild<false>, dim3(cap_grid((g->arcs / 4 + 511) / 512, 8192)), dim3(256),
-                     0, g->stream, nullptr, (int64_t)0, g->col, g->arcs, g->lab[g->cur], g->al);
-  LPA_HIP(hipGetLastError());
-  return LPA_OK;
+  return launch_rebuild(g, false, 0, g->lab[g->cur]);
 }
 
 int gather_labels(lpa_graph* g, int32_t* out_dense_dev) {
