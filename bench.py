@@ -195,6 +195,7 @@ def main():
             "bytes": iter_bytes, "median_iter_ms": round(med_iter_ms, 4),
             "achieved_GBs": round(iter_bytes / (med_iter_ms * 1e-3) / 1e9, 1),
             "frac": round(iter_bytes / (med_iter_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "iter_ms": [round(x, 4) for x in st["iter_ms"]],
         },
         "kernel_ms_per_step": {k: round(v / ksteps, 4) for k, v in kms.items()},
         "exchange_ms_per_step": round(st["exchange_ms"] / ksteps, 4),
