@@ -23,16 +23,38 @@ __device__ __forceinline__ u64 tally(u32 cnt, u32 label) {
 
 __device__ __forceinline__ u64 umax64(u64 a, u64 b) { return a > b ? a : b; }
 
+// Wave reductions over a FULL wave (every call site has all 64 lanes active):
+// DPP within each 16-lane row (xor 1, xor 2, half-row mirror, row mirror: every
+// lane ends with its row's result, VALU only, no LDS round trip), then the four
+// row results via readlane (uniform result).
+template <int kCtrl>
+__device__ __forceinline__ u32 dpp_u32(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ u64 dpp_u64(u64 v) {
+  return ((u64)dpp_u32<kCtrl>((u32)(v >> 32)) << 32) | (u64)dpp_u32<kCtrl>((u32)v);
+}
+__device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
+  return ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l) << 32) |
+         (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, l);
+}
 __device__ __forceinline__ u64 wave_max_u64(u64 v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = umax64(v, __shfl_xor(v, off, 64));
-  return v;
+  v = umax64(v, dpp_u64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = umax64(v, dpp_u64<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = umax64(v, dpp_u64<0x141>(v));  // row_half_mirror
+  v = umax64(v, dpp_u64<0x140>(v));  // row_mirror
+  return umax64(umax64(readlane_u64(v, 0), readlane_u64(v, 16)),
+                umax64(readlane_u64(v, 32), readlane_u64(v, 48)));
 }
 
 __device__ __forceinline__ u32 wave_sum_u32(u32 v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += (u32)__shfl_xor((int)v, off, 64);
-  return v;
+  v += dpp_u32<0xB1>(v);
+  v += dpp_u32<0x4E>(v);
+  v += dpp_u32<0x141>(v);
+  v += dpp_u32<0x140>(v);
+  return (u32)__builtin_amdgcn_readlane((int)v, 0) + (u32)__builtin_amdgcn_readlane((int)v, 16) +
+         (u32)__builtin_amdgcn_readlane((int)v, 32) + (u32)__builtin_amdgcn_readlane((int)v, 48);
 }
 
 __device__ __forceinline__ u32 hash_slot(u32 label, int shift) {

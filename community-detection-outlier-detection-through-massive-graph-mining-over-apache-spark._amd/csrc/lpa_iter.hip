@@ -83,10 +83,29 @@ __device__ __forceinline__ u64 tally(u32 cnt, u32 label) {
 
 __device__ __forceinline__ u64 umax64(u64 a, u64 b) { return a > b ? a : b; }
 
+// Wave reductions over a FULL wave (every call site has all 64 lanes active):
+// DPP within each 16-lane row (xor 1, xor 2, half-row mirror, row mirror: every
+// lane ends with its row's result, VALU only, no LDS round trip), then the four
+// row results via readlane (uniform result).
+template <int kCtrl>
+__device__ __forceinline__ u32 dpp_u32(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ u64 dpp_u64(u64 v) {
+  return ((u64)dpp_u32<kCtrl>((u32)(v >> 32)) << 32) | (u64)dpp_u32<kCtrl>((u32)v);
+}
+__device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
+  return ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l) << 32) |
+         (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, l);
+}
 __device__ __forceinline__ u64 wave_max_u64(u64 v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = umax64(v, __shfl_xor(v, off, 64));
-  return v;
+  v = umax64(v, dpp_u64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = umax64(v, dpp_u64<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = umax64(v, dpp_u64<0x141>(v));  // row_half_mirror
+  v = umax64(v, dpp_u64<0x140>(v));  // row_mirror
+  return umax64(umax64(readlane_u64(v, 0), readlane_u64(v, 16)),
+                umax64(readlane_u64(v, 32), readlane_u64(v, 48)));
 }
 
 __device__ __forceinline__ u32 hash_slot(u32 label, int shift) {
@@ -425,6 +444,27 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
 // within each G-lane group).  (A three-set unrolled ring, as in k_lpa_units,
 // measured slower here: the per-batch tally is long enough to cover one batch.)
 // ---------------------------------------------------------------------------
+// label of the first active lane of this lane's G-lane group (act: the wave's
+// active mask, uniform).  G >= 16: one readlane per group (scalar lane index),
+// selected per lane -- VALU/SALU only; smaller groups use one ds_bpermute.
+template <int G>
+__device__ __forceinline__ u32 group_lead(u32 lb, u64 act, int lane, int lead) {
+  if constexpr (G >= 16) {
+    constexpr u64 gm = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
+    u32 x = 0u;
+#pragma unroll
+    for (int k = 0; k < 64 / G; ++k) {
+      const u64 mk = (act >> (k * G)) & gm;
+      const int l = k * G + (mk ? (__ffsll((unsigned long long)mk) - 1) : 0);
+      const u32 xk = (u32)__builtin_amdgcn_readlane((int)lb, l);
+      if (lane / G == k) x = xk;
+    }
+    return x;
+  } else {
+    return (u32)__shfl((int)lb, lead, 64);
+  }
+}
+
 template <int G>
 __device__ __forceinline__ void rows_rp(const int64_t* __restrict__ rp, int64_t r0, int64_t vend,
                                         int lane, int64_t& rpl, int64_t& rpe) {
@@ -492,7 +532,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       while (act) {
         const u64 my = (act >> gbase) & gm;
         const int lead = gbase + (my ? (__ffsll((unsigned long long)my) - 1) : 0);
-        const u32 x = (u32)__shfl((int)lb, lead, 64);
+        const u32 x = group_lead<G>(lb, act, lane, lead);
         const u64 mm = __ballot(((act >> lane) & 1ull) && lb == x);
         const u32 cn = (u32)__popcll((mm >> gbase) & gm);
         if (my) best = umax64(best, tally(cn, x));
