@@ -99,6 +99,85 @@ __device__ __forceinline__ int lds_insert_bounded(u64* tab, int shift, u32 mask,
   return -1;
 }
 
+// Continue the insert of tally word `word` (count << 32 | ~label) whose first
+// probe at slot h hit another key: linear probing.  Returns the claimed slot or
+// -1 (merged into an existing key).  kBounded: give up after a full sweep, raise
+// bit 2 of *err and drop the votes (tables whose load is not bounded by design).
+template <bool kBounded>
+__device__ __forceinline__ int lds_probe_word(u64* tab, u32 mask, u64 word, u32 h, int32_t* err) {
+  const u32 key = (u32)word;
+  for (u32 probe = 0; !kBounded || probe < mask; ++probe) {
+    h = (h + 1u) & mask;
+    const u64 old = atomicCAS(&tab[h], 0ull, word);
+    if (old == 0ull) return (int)h;
+    if ((u32)old == key) {
+      atomicAdd(&tab[h], word & 0xFFFFFFFF00000000ull);
+      return -1;
+    }
+  }
+  atomicOr(err, 2);
+  return -1;
+}
+
+// Batched insert of NC chunks of tally words (lane l of chunk c inserts wv[c]
+// when bit l of act[c] is set): every first-probe CAS is issued before any is
+// resolved, so NC independent LDS atomics per lane are in flight instead of one
+// dependent chain per word; a key match adds the count (no return value), a
+// collision probes on.  slot[c] = the slot this lane claimed, or -1.
+template <int NC, bool kBounded = false>
+__device__ __forceinline__ void insert_words(u64* tab, int shift, u32 mask, const u64 (&wv)[NC],
+                                             const u64 (&act)[NC], int lane, int (&slot)[NC],
+                                             int32_t* err) {
+  u64 old[NC];
+  u32 hh[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    old[c] = 0ull;
+    hh[c] = 0u;
+    if ((act[c] >> lane) & 1ull) {
+      hh[c] = hash_slot(~(u32)wv[c], shift);
+      old[c] = atomicCAS(&tab[hh[c]], 0ull, wv[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    slot[c] = -1;
+    if ((act[c] >> lane) & 1ull) {
+      if (old[c] == 0ull) {
+        slot[c] = (int)hh[c];
+      } else if ((u32)old[c] == (u32)wv[c]) {
+        atomicAdd(&tab[hh[c]], wv[c] & 0xFFFFFFFF00000000ull);
+      } else {
+        slot[c] = lds_probe_word<kBounded>(tab, mask, wv[c], hh[c], err);
+      }
+    }
+  }
+}
+
+// Append the claimed slots of NC chunks to a block-shared LDS list with ONE
+// returning LDS atomic per wave.
+template <int NC>
+__device__ __forceinline__ void list_append_n(uint16_t* lst, int* lcount, const int (&slot)[NC],
+                                              int lane) {
+  u64 cm[NC];
+  int tot = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    cm[c] = __ballot(slot[c] >= 0);
+    tot += __popcll(cm[c]);
+  }
+  if (tot == 0) return;  // uniform over the wave
+  int base = 0;
+  if (lane == 0) base = atomicAdd(lcount, tot);
+  base = __builtin_amdgcn_readfirstlane(base);
+  const u64 lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (slot[c] >= 0) lst[base + __popcll(cm[c] & lt)] = (uint16_t)slot[c];
+    base += __popcll(cm[c]);
+  }
+}
+
 // Wave-aggregated append of claimed slots to an LDS list (one LDS atomic per wave).
 __device__ __forceinline__ void list_append(uint16_t* lst, int* lcount, int slot, int lane) {
   const u64 cm = __ballot(slot >= 0);

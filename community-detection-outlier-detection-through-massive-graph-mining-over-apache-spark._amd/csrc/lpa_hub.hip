@@ -367,18 +367,20 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, int64_t n_hub
     u64 best = 0ull, pw = 0ull;
     weighted_peel<NC>(wv, act, nact, best, pw, lane);
     if (nact > 0) {
-      if (lane == 0) lc_all[w] = 0;
       int lg = ceil_log2(2u * (u32)T);
       lg = lg < 6 ? 6 : lg;
       const u32 mask = (1u << lg) - 1u;
+      int slot[NC];
+      insert_words<NC>(tab, 32 - lg, mask, wv, act, lane, slot, nullptr);
+      // the wave owns its table and list: claimed slots appended by ballot prefix
+      const u64 lt = (1ull << lane) - 1ull;
+      int n = 0;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        int slot = -1;
-        if ((act[c] >> lane) & 1ull)
-          slot = lds_insert(tab, 32 - lg, mask, ~(u32)wv[c], (u32)(wv[c] >> 32));
-        list_append(lst, &lc_all[w], slot, lane);
+        const u64 cm = __ballot(slot[c] >= 0);
+        if (slot[c] >= 0) lst[n + __popcll(cm & lt)] = (uint16_t)slot[c];
+        n += __popcll(cm);
       }
-      const int n = lc_all[w];
       for (int i = lane; i < n; i += 64) {
         const int sl = lst[i];
         best = umax64(best, tab[sl]);
@@ -410,9 +412,14 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
     u64 fv[kFirst];
 #pragma unroll
     for (int k = 0; k < kFirst; ++k) fv[k] = k < nj ? src[k] : 0ull;
+    {
+      u64 fa[kFirst];
+      int sl[kFirst];
 #pragma unroll
-    for (int k = 0; k < kFirst; ++k)
-      insert_word(fv[k], fv[k] != 0ull && keep(~(u32)fv[k]), tab, lst, lcount, kLg, lane, err);
+      for (int k = 0; k < kFirst; ++k) fa[k] = __ballot(fv[k] != 0ull && keep(~(u32)fv[k]));
+      insert_words<kFirst>(tab, 32 - kLg, (1u << kLg) - 1u, fv, fa, lane, sl, err);
+      list_append_n<kFirst>(lst, lcount, sl, lane);
+    }
     // longer units one at a time, the next one's words loading meanwhile
     u64 big = __ballot(nj > kFirst);
     u64 wv[NC];
@@ -437,10 +444,13 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
       u64 wn[NC];
       int nn = 0;
       load_big(big, wn, nn);
+      {
+        u64 wa[NC];
+        int sl[NC];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        if (kFirst + c * 64 >= n) break;  // uniform over the wave
-        insert_word(wv[c], wv[c] != 0ull && keep(~(u32)wv[c]), tab, lst, lcount, kLg, lane, err);
+        for (int c = 0; c < NC; ++c) wa[c] = __ballot(wv[c] != 0ull && keep(~(u32)wv[c]));
+        insert_words<NC>(tab, 32 - kLg, (1u << kLg) - 1u, wv, wa, lane, sl, err);
+        list_append_n<NC>(lst, lcount, sl, lane);
       }
 #pragma unroll
       for (int c = 0; c < NC; ++c) wv[c] = wn[c];
