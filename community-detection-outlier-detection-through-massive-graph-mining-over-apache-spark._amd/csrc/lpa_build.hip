@@ -186,6 +186,7 @@ int init_labels(lpa_graph* g) {
                      g->vpad, g->lab[0], g->lab[1]);
   LPA_HIP(hipGetLastError());
   g->cur = 0;
+  g->since_reset = 0;
   return rebuild_arc_labels(g);
 }
 

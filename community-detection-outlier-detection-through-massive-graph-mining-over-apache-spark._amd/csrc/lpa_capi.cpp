@@ -61,8 +61,8 @@ void destroy(lpa_graph* g) {
     if (e) (void)hipEventDestroy(e);
   for (auto& st : g->aux_stream)
     if (st) (void)hipStreamDestroy(st);
-  if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
-  for (auto& e : g->ev_join)
+  for (hipEvent_t e : {g->ev_fork, g->ev_join[0], g->ev_join[1], g->ev_fork2, g->ev_join2[0],
+                       g->ev_join2[1]})
     if (e) (void)hipEventDestroy(e);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   if (g->own_stream) (void)hipStreamDestroy(g->own_stream);
@@ -140,9 +140,9 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
     hipError_t e = hipSuccess;
     for (auto& st : g->aux_stream)
       if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming);
-    for (auto& ev : g->ev_join)
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    for (hipEvent_t* ev : {&g->ev_fork, &g->ev_join[0], &g->ev_join[1], &g->ev_fork2, &g->ev_join2[0],
+                           &g->ev_join2[1]})
+      if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       set_error("stream/event creation: %s", hipGetErrorString(e));
       destroy(g);

@@ -829,7 +829,7 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   return LPA_OK;
 }
 
-int launch_hub_combine(lpa_graph* g, int32_t* Lown) {
+int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   const int64_t n = g->n_hub;
   if (n == 0) return LPA_OK;
   hipStream_t s = g->stream;
@@ -846,34 +846,49 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown) {
   hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, hl, n, g->rp, g->hub_uoff, g->ucnt,
                      g->stage, g->hub_wcount, Lown, lists, g->hub_lcnt, g->items_cb, g->items_cc);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_mid<11>, dim3(grid_cap(n, 2048)), dim3(256), 0, s, lists, g->hub_lcnt, 0,
-                     g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
+  // the mid tiers and the bucket path are independent.  fork: the 8192- and
+  // 4096-slot tiers run on the main stream, the 2048-slot tier and the bucket path
+  // on their own stream (not behind the tally bins of the other aux streams).  The
+  // caller forks only while the labels are still high-cardinality (the first
+  // supersteps after L0): converged supersteps queue ~5 us kernels here, and the
+  // extra cross-stream event pair costs more than their overlap saves.
+  hipStream_t sd = fork ? g->aux_stream[2] : s;
+  if (fork) {
+    LPA_HIP(hipEventRecord(g->ev_fork2, s));
+    LPA_HIP(hipStreamWaitEvent(sd, g->ev_fork2, 0));
+  }
+  hipLaunchKernelGGL(k_hub_mid<13>, dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,
+                     g->hub_lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
+                     g->dev_err);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_hub_mid<12>, dim3(grid_cap(n, 1024)), dim3(256), 0, s, lists + 3 * n,
                      g->hub_lcnt, 5, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
                      g->dev_err);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_mid<13>, dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,
-                     g->hub_lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
-                     g->dev_err);
+  hipLaunchKernelGGL(k_hub_mid<11>, dim3(grid_cap(n, 2048)), dim3(256), 0, sd, lists, g->hub_lcnt, 0,
+                     g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
   LPA_HIP(hipGetLastError());
   const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
-  hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, s, g->items_cc, g->hub_lcnt, g->rp,
+  hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, sd, g->items_cc, g->hub_lcnt, g->rp,
                      g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->ghist);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_scan, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, s, listC,
+  hipLaunchKernelGGL(k_hub_scan, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
                      g->hub_lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->gcur);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, s, g->items_cc, g->hub_lcnt, g->rp,
+  hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, sd, g->items_cc, g->hub_lcnt, g->rp,
                      g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->gcur, g->scat);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_bucket, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_hub_bucket, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, sd,
                      g->items_cb, g->hub_lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
                      g->hub_best, g->dev_err);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, s, listC,
+  hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
                      g->hub_lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown);
   LPA_HIP(hipGetLastError());
+  if (fork) {
+    LPA_HIP(hipEventRecord(g->ev_join2[0], sd));
+    LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[0], 0));
+  }
   return LPA_OK;
 }
 

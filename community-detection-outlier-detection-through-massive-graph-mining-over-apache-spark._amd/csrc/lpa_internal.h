@@ -81,8 +81,11 @@ struct lpa_graph {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  hipStream_t aux_stream[2] = {nullptr, nullptr};  // concurrent tally bins
+  // concurrent tally bins (0: wave bins, 1: row/group bins) and the hub combine's
+  // bucket path (2); 4 streams = the 4 hardware queues of a process
+  hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork2 = nullptr, ev_join2[2] = {nullptr, nullptr};  // hub combine tail (join2[0] used)
   int32_t rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
 
@@ -102,6 +105,7 @@ struct lpa_graph {
   int32_t* deg = nullptr;     // [V] symmetrised degree by dense id
   int32_t* lab[2] = {nullptr, nullptr};  // [vpad] ping-pong label vectors (replicated)
   int cur = 0;                // index of the current label vector
+  int64_t since_reset = 0;    // supersteps run since the labels were last L0
 
   // degree bins over the owned slice
   int64_t bin_begin[LPA_NBINS + 1] = {0};
@@ -176,7 +180,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
                 uint32_t flags);
 int init_labels(lpa_graph* g);
 int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
-int launch_hub_combine(lpa_graph* g, int32_t* Lown);         // lpa_hub.hip
+int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork);  // lpa_hub.hip
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
 
 // iteration (lpa_iter.hip)

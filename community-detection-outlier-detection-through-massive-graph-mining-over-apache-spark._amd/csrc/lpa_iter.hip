@@ -68,6 +68,10 @@ namespace {
 #define LPA_DIAG 0
 #endif
 
+// supersteps after L0 whose hub combine runs forked over two streams (see
+// launch_hub_combine)
+constexpr int kDenseSupersteps = 2;
+
 constexpr int kChunks = 8;    // 64-arc chunks per wave: a wave-bin row / a quarter segment
 constexpr u32 kNone = 0xFFFFFFFFu;  // empty lane
 static_assert(kSegArcs == 64 * kChunks, "a unit is one batch of chunks");
@@ -908,10 +912,6 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
     LPA_TRACE_POINT("seg");
   }
   LPA_TRY(mark(1, s));
-  LPA_TRY(mark(2, s));
-  LPA_TRY(launch_hub_combine(g, Lown));
-  LPA_TRACE_POINT("hub_combine");
-  LPA_TRY(mark(3, s));
 #define LPA_WAVE_LAUNCH(BIN, NC)                                                              \
   {                                                                                           \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                  \
@@ -959,6 +959,12 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
+  // hub combine after the bins are queued: its tail kernels on the aux streams
+  // run after those streams' bins
+  LPA_TRY(mark(2, s));
+  LPA_TRY(launch_hub_combine(g, Lown, g->since_reset < kDenseSupersteps));
+  LPA_TRACE_POINT("hub_combine");
+  LPA_TRY(mark(3, s));
   LPA_HIP(hipEventRecord(g->ev_join[0], sb));
   LPA_HIP(hipEventRecord(g->ev_join[1], sc));
   LPA_HIP(hipStreamWaitEvent(s, g->ev_join[0], 0));
@@ -1053,6 +1059,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     }
     g->cur ^= 1;
+    ++g->since_reset;
   }
   if (timed) LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS + 1], s));
   LPA_HIP(hipStreamSynchronize(s));
