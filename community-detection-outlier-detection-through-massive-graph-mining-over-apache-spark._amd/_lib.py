@@ -99,6 +99,8 @@ SIGNATURES = {
     "lpa_degrees": (ctypes.c_int, [_vp, _i32p]),
     "lpa_exchange_get": (ctypes.c_int, [_vp, _i32p]),
     "lpa_exchange_put": (ctypes.c_int, [_vp, _i32p]),
+    "lpa_exchange_get_delta": (ctypes.c_int, [_vp, _vp, _i64p]),
+    "lpa_exchange_put_delta": (ctypes.c_int, [_vp, _vp, _i64p, ctypes.c_int64]),
     "lpa_graph_get_info": (ctypes.c_int, [_vp, ctypes.POINTER(LpaGraphInfo)]),
     "lpa_graph_destroy": (None, [_vp]),
     "lpa_last_error": (ctypes.c_char_p, []),

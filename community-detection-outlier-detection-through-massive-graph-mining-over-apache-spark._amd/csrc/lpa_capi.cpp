@@ -46,6 +46,7 @@ int gen_sbm(int32_t V, int32_t blocks, int64_t m, uint32_t p_in_q32, uint64_t se
             int32_t* d_dst, hipStream_t s);
 
 void destroy(lpa_graph* g) {
+  if (g) exchange_free(g);
   if (!g) return;
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
@@ -161,6 +162,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
     }
   }
   int rc = build_graph(g, src, dst, m, V, flags);
+  if (rc == LPA_OK) rc = exchange_alloc(g);
   if (rc != LPA_OK) {
     destroy(g);
     return rc;
@@ -231,6 +233,53 @@ int lpa_exchange_put(lpa_graph* g, const int32_t* full_in) {
                          g->stream));
   LPA_TRY(rebuild_arc_labels(g));
   LPA_HIP(hipStreamSynchronize(g->stream));
+  return LPA_OK;
+}
+
+int lpa_exchange_get_delta(lpa_graph* g, uint64_t* entries_out, int64_t* count_out) {
+  if (!g || !entries_out || !count_out || g->nranks <= 1) {
+    set_error("lpa_exchange_get_delta: null argument or single-rank handle");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  // after lpa_step the current vector holds this rank's new owned labels, the other
+  // one the labels they replace
+  LPA_TRY(exchange_compact(g, g->lab[g->cur ^ 1], g->lab[g->cur]));
+  unsigned long long n = 0;
+  LPA_HIP(hipMemcpyAsync(&n, g->dcount, sizeof(n), hipMemcpyDeviceToHost, g->stream));
+  LPA_HIP(hipStreamSynchronize(g->stream));
+  if (n > 0)
+    LPA_HIP(hipMemcpyAsync(entries_out, g->dsend, sizeof(uint64_t) * n, hipMemcpyDeviceToHost,
+                           g->stream));
+  LPA_HIP(hipStreamSynchronize(g->stream));
+  *count_out = (int64_t)n;
+  return LPA_OK;
+}
+
+int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t* counts, int64_t cap) {
+  if (!g || !counts || (cap > 0 && !entries) || g->nranks <= 1 || cap < 0) {
+    set_error("lpa_exchange_put_delta: null argument or single-rank handle");
+    return LPA_EINVAL;
+  }
+  if (cap > g->dcap) {
+    set_error("lpa_exchange_put_delta: %lld entries per rank exceed the delta capacity %lld "
+              "(use lpa_exchange_put)", (long long)cap, (long long)g->dcap);
+    return LPA_EINVAL;
+  }
+  for (int r = 0; r < g->nranks; ++r)
+    if (counts[r] < 0 || counts[r] > cap) {
+      set_error("lpa_exchange_put_delta: count of rank %d out of [0, cap]", r);
+      return LPA_EINVAL;
+    }
+  LPA_HIP(hipSetDevice(g->device));
+  hipStream_t s = g->stream;
+  if (cap > 0)
+    LPA_HIP(hipMemcpyAsync(g->drecv, entries, sizeof(uint64_t) * cap * g->nranks,
+                           hipMemcpyHostToDevice, s));
+  LPA_HIP(hipMemcpyAsync(g->dcount + 1, counts, sizeof(int64_t) * g->nranks, hipMemcpyHostToDevice, s));
+  LPA_TRY(exchange_apply(g, g->lab[g->cur ^ 1], g->lab[g->cur], g->dcount + 1, cap));
+  LPA_TRY(rebuild_arc_labels(g));
+  LPA_HIP(hipStreamSynchronize(s));
   return LPA_OK;
 }
 

@@ -1,0 +1,173 @@
+// Multi-GPU label exchange: after each superstep's tally every
+// rank holds the new labels of its own slice; every replica must receive them.
+//
+//   full   ncclAllGather of the owned slices (4 V (P-1)/P bytes received per
+//          rank): the label-dense supersteps right after L0, where most labels
+//          change anyway.
+//   delta  each rank compacts the (slot, label) pairs of its CHANGED owned
+//          vertices; the per-rank counts are allgathered and read on the host,
+//          then ncclAllGather moves max-count entries per rank (8 B each).  Every
+//          rank copies the other ranks' slices of the current labels into the
+//          next-label buffer and applies the gathered changes.  Converged
+//          supersteps change ~0.3 % of the vertices (R-MAT-24, superstep 4+), so
+//          the exchange shrinks by ~2 orders of magnitude.  Chosen when the
+//          largest delta is < 1/4 of a slice (its bytes < 1/2 of the full slice).
+// Both give the identical full label vector, so the mode never affects labels.
+#include "lpa_internal.h"
+
+namespace lpa {
+
+namespace {
+
+// changed owned slots -> dsend[] = (local slot << 32 | new label); dcount = count.
+// Block-aggregated: one global atomic per block.
+__global__ __launch_bounds__(256) void k_delta_compact(const int32_t* __restrict__ Lc_own,
+                                                       const int32_t* __restrict__ Ln_own,
+                                                       int64_t slice, u64* __restrict__ dsend,
+                                                       unsigned long long* __restrict__ dcount) {
+  __shared__ int wsum[4];
+  __shared__ unsigned long long base_s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t i0 = (int64_t)blockIdx.x * 256; i0 < slice; i0 += (int64_t)gridDim.x * 256) {
+    const int64_t i = i0 + threadIdx.x;
+    int32_t nv = 0;
+    bool chg = false;
+    if (i < slice) {
+      nv = Ln_own[i];
+      chg = nv != Lc_own[i];
+    }
+    const u64 m = __ballot(chg);
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k < w) before += wsum[k];
+      tot += wsum[k];
+    }
+    if (threadIdx.x == 0 && tot) base_s = atomicAdd(dcount, (unsigned long long)tot);
+    __syncthreads();
+    if (chg) {
+      const u64 pos = base_s + before + __popcll(m & ((1ull << lane) - 1ull));
+      dsend[pos] = ((u64)(uint32_t)i << 32) | (u64)(uint32_t)nv;
+    }
+    __syncthreads();  // wsum / base_s reused by the next tile
+  }
+}
+
+// Ln[i] = Lc[i] for every slot outside [own_begin, own_begin + slice) (int4; slices
+// are multiples of 64 slots)
+__global__ void k_copy_other(const int4* __restrict__ Lc, int4* __restrict__ Ln, int64_t n4,
+                             int64_t own4_begin, int64_t own4_end) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+       q += (int64_t)gridDim.x * blockDim.x)
+    if (q < own4_begin || q >= own4_end) Ln[q] = Lc[q];
+}
+
+// apply the gathered changes: rank r's entries are drecv[r * cap, r * cap + counts[r])
+__global__ void k_delta_apply(const u64* __restrict__ drecv, const unsigned long long* __restrict__ counts,
+                              int64_t cap, int32_t P, int64_t slice, int32_t* __restrict__ Ln) {
+  const int64_t tot = cap * P;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = k / cap, j = k - r * cap;
+    if (j < (int64_t)counts[r]) {
+      const u64 e = drecv[k];
+      Ln[r * slice + (int64_t)(e >> 32)] = (int32_t)(uint32_t)e;
+    }
+  }
+}
+
+inline unsigned grid_of(int64_t n, int64_t cap) {
+  int64_t b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  return (unsigned)(b < cap ? b : cap);
+}
+
+}  // namespace
+
+int exchange_alloc(lpa_graph* g) {
+  if (g->nranks <= 1) return LPA_OK;
+  g->dcap = g->slice / 4;
+  if (g->dcap < 1) g->dcap = 1;
+  LPA_TRY(dev_alloc(g, (void**)&g->dsend, sizeof(u64) * g->slice));
+  LPA_TRY(dev_alloc(g, (void**)&g->drecv, sizeof(u64) * g->dcap * g->nranks));
+  LPA_TRY(dev_alloc(g, (void**)&g->dcount, sizeof(unsigned long long) * (1 + g->nranks)));
+  LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * g->nranks,
+                        hipHostMallocDefault));
+  return LPA_OK;
+}
+
+void exchange_free(lpa_graph* g) {
+  if (g->h_dcounts) (void)hipHostFree(g->h_dcounts);
+  g->h_dcounts = nullptr;
+}
+
+// compact this rank's changed owned labels (Lc -> Ln) into dsend; count -> dcount[0]
+int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
+  hipStream_t s = g->stream;
+  LPA_HIP(hipMemsetAsync(g->dcount, 0, sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(k_delta_compact, dim3(grid_of(g->slice, 4096)), dim3(256), 0, s,
+                     Lc + g->own_begin, Ln + g->own_begin, g->slice, g->dsend, g->dcount);
+  LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
+
+// Ln := Lc outside the own slice, then the gathered changes (drecv, cap entries per
+// rank, counts on the device)
+int exchange_apply(lpa_graph* g, const int32_t* Lc, int32_t* Ln, const unsigned long long* counts,
+                   int64_t cap) {
+  hipStream_t s = g->stream;
+  const int64_t n4 = g->vpad / 4;
+  hipLaunchKernelGGL(k_copy_other, dim3(grid_of(n4, 8192)), dim3(256), 0, s, (const int4*)Lc,
+                     (int4*)Ln, n4, g->own_begin / 4, (g->own_begin + g->slice) / 4);
+  LPA_HIP(hipGetLastError());
+  if (cap > 0) {
+    hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(cap * g->nranks, 8192)), dim3(256), 0, s,
+                       g->drecv, counts, cap, g->nranks, g->slice, Ln);
+    LPA_HIP(hipGetLastError());
+  }
+  return LPA_OK;
+}
+
+// In-library RCCL exchange of one superstep (P > 1, comm set): Lown = Ln + own_begin
+// holds the new owned labels; on return Ln holds the full new label vector.
+int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense) {
+  hipStream_t s = g->stream;
+  int32_t* Lown = Ln + g->own_begin;
+  if (!dense) {
+    LPA_TRY(exchange_compact(g, Lc, Ln));
+    unsigned long long* counts = g->dcount + 1;
+    ncclResult_t r = ncclAllGather(g->dcount, counts, 1, ncclUint64, g->comm, s);
+    if (r != ncclSuccess) {
+      set_error("ncclAllGather (delta counts): %s", ncclGetErrorString(r));
+      return LPA_ERCCL;
+    }
+    LPA_HIP(hipMemcpyAsync(g->h_dcounts, counts, sizeof(unsigned long long) * g->nranks,
+                           hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    int64_t cap = 0;
+    for (int k = 0; k < g->nranks; ++k)
+      if ((int64_t)g->h_dcounts[k] > cap) cap = (int64_t)g->h_dcounts[k];
+    if (cap <= g->dcap) {
+      if (cap > 0) {
+        r = ncclAllGather(g->dsend, g->drecv, (size_t)cap, ncclUint64, g->comm, s);
+        if (r != ncclSuccess) {
+          set_error("ncclAllGather (delta): %s", ncclGetErrorString(r));
+          return LPA_ERCCL;
+        }
+      }
+      g->last_exchange_delta = cap;
+      return exchange_apply(g, Lc, Ln, counts, cap);
+    }
+  }
+  ncclResult_t r = ncclAllGather(Lown, Ln, (size_t)g->slice, ncclInt32, g->comm, s);
+  if (r != ncclSuccess) {
+    set_error("ncclAllGather: %s", ncclGetErrorString(r));
+    return LPA_ERCCL;
+  }
+  g->last_exchange_delta = -1;
+  return LPA_OK;
+}
+
+}  // namespace lpa

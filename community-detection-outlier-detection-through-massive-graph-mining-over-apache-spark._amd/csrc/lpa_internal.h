@@ -150,6 +150,14 @@ struct lpa_graph {
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   unsigned long long* counters = nullptr;  // [0] chunk count, [1] dirty arcs, [2] changed vertices
 
+  // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
+  lpa::u64* dsend = nullptr;                 // [slice] this rank's (slot << 32 | label)
+  lpa::u64* drecv = nullptr;                 // [nranks * dcap] gathered deltas
+  unsigned long long* dcount = nullptr;      // [1 + nranks] own count, then every rank's
+  unsigned long long* h_dcounts = nullptr;   // [nranks] pinned host copy
+  int64_t dcap = 0;                          // delta entries per rank (slice / 4)
+  int64_t last_exchange_delta = -1;          // entries per rank of the last exchange (-1 full)
+
   // original edge list kept for the outlier stage (device, dense ids)
   int32_t* e_src = nullptr;
   int32_t* e_dst = nullptr;
@@ -186,6 +194,14 @@ int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
 // iteration (lpa_iter.hip)
 int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st);
 int gather_labels(lpa_graph* g, int32_t* out_dense_dev);
+
+// label exchange (lpa_exchange.hip)
+int exchange_alloc(lpa_graph* g);
+void exchange_free(lpa_graph* g);
+int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln);
+int exchange_apply(lpa_graph* g, const int32_t* Lc, int32_t* Ln, const unsigned long long* counts,
+                   int64_t cap);
+int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense);
 
 // outlier (lpa_outlier.hip)
 int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,

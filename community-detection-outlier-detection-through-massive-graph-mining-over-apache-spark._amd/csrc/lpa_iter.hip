@@ -1045,13 +1045,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
     LPA_TRY(launch_tally(g, Lown, bev));
     if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
-    if (g->nranks > 1 && g->comm) {
-      ncclResult_t r = ncclAllGather(Lown, Ln, (size_t)g->slice, ncclInt32, g->comm, s);
-      if (r != ncclSuccess) {
-        set_error("ncclAllGather: %s", ncclGetErrorString(r));
-        return LPA_ERCCL;
-      }
-    }
+    if (g->nranks > 1 && g->comm)
+      LPA_TRY(exchange_rccl(g, Lc, Ln, g->since_reset < kDenseSupersteps));
     if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
     LPA_TRY(launch_refresh(g, Lc, Ln));
     if (tt) {

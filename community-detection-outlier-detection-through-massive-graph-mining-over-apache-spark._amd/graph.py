@@ -144,6 +144,26 @@ class Graph:
         full = np.ascontiguousarray(full, dtype=np.int32)
         _lib.check(self._lib.lpa_exchange_put(self._handle(), full.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
 
+    def exchange_get_delta(self) -> np.ndarray:
+        """This rank's changed owned labels as (local slot << 32 | label) entries."""
+        buf = np.empty(max(self.info()["slice"], 1), dtype=np.uint64)
+        n = ctypes.c_int64(0)
+        _lib.check(self._lib.lpa_exchange_get_delta(self._handle(), buf.ctypes.data_as(ctypes.c_void_p),
+                                                    ctypes.byref(n)))
+        return buf[: n.value].copy()
+
+    def exchange_put_delta(self, per_rank):
+        """Apply every rank's delta entries (list in rank order)."""
+        cap = max((e.size for e in per_rank), default=0)
+        P = len(per_rank)
+        table = np.zeros((P, max(cap, 1)), dtype=np.uint64)
+        for r, e in enumerate(per_rank):
+            table[r, : e.size] = e
+        counts = np.array([e.size for e in per_rank], dtype=np.int64)
+        _lib.check(self._lib.lpa_exchange_put_delta(self._handle(), table.ctypes.data_as(ctypes.c_void_p),
+                                                    counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                    cap))
+
     # -- outlier stage --------------------------------------------------------
     def outlier(self, labels, mode="L1", sub_iter: int = 5):
         """Appendix B outlier stage.  Returns dict(size, incident, sub_labels, flags, summary)."""

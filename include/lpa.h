@@ -121,6 +121,17 @@ int lpa_graph_create_dist(const int32_t* src, const int32_t* dst, int64_t m, int
  */
 int lpa_exchange_get(lpa_graph* g, int32_t* slice_out);
 int lpa_exchange_put(lpa_graph* g, const int32_t* full_in);
+/*
+ * Delta form of the caller-driven exchange (the protocol the in-library RCCL
+ * exchange uses in converged supersteps, lpa_exchange.hip): after lpa_step(g, 1)
+ * lpa_exchange_get_delta returns this rank's CHANGED owned labels as
+ * (local slot << 32 | label) entries (entries_out: room for `slice` entries) and
+ * their count; the caller lays every rank's entries out as [nranks][cap]
+ * (cap >= every count, cap <= slice / 4) and passes them with the counts to
+ * lpa_exchange_put_delta on every rank.  Host buffers.
+ */
+int lpa_exchange_get_delta(lpa_graph* g, uint64_t* entries_out, int64_t* count_out);
+int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t* counts, int64_t cap);
 
 /* Run on a caller-provided hipStream_t (NULL = the handle's own stream). */
 int lpa_set_stream(lpa_graph* g, void* hip_stream);

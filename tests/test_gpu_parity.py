@@ -169,6 +169,40 @@ def test_virtual_partitions_bit_exact(gfa, oracle, P):
             g.close()
 
 
+@pytest.mark.parametrize("P", [2, 4])
+def test_virtual_partitions_delta_exchange(gfa, oracle, P):
+    """The changed-label delta exchange (the converged-superstep protocol of the
+    in-library RCCL exchange, lpa_exchange.hip) with P virtual ranks: full
+    exchange while a delta exceeds slice / 4, deltas after; bit-exact per superstep."""
+    V, s, d = degree_mix(11)
+    ranks = [gfa.Graph(s, d, V, rank=r, nranks=P) for r in range(P)]
+    try:
+        slice_ = ranks[0].info()["slice"]
+        _, hist, _ = oracle.lpa(V, s, d, 8, per_iter=True)
+        modes = []
+        for t in range(8):
+            for g in ranks:
+                g.step(1)
+            deltas = [g.exchange_get_delta() for g in ranks]
+            for r, e in enumerate(deltas):  # entries: owned local slots, in range
+                assert e.size == 0 or int((e >> np.uint64(32)).max()) < slice_
+            if max(e.size for e in deltas) <= slice_ // 4:
+                for g in ranks:
+                    g.exchange_put_delta(deltas)
+                modes.append("delta")
+            else:
+                full = np.concatenate([g.exchange_get() for g in ranks])
+                for g in ranks:
+                    g.exchange_put(full)
+                modes.append("full")
+            for g in ranks:
+                assert np.array_equal(g.labels(), hist[t]), f"P={P} superstep {t + 1} ({modes[-1]})"
+        assert "delta" in modes and modes[0] == "full", modes
+    finally:
+        for g in ranks:
+            g.close()
+
+
 def test_outlier_l1_l2_golden(gfa, golden):
     V = golden["ids"].size
     with gfa.Graph(golden["src"], golden["dst"], V) as g:
