@@ -29,6 +29,22 @@ sys.path.insert(0, ROOT)
 
 METRIC = "LPA GTEPS per iteration at 1/2/4/8 MI355X; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
+# measured HBM traffic per launch of the dominant kernel: rocprofv3 --pmc FETCH_SIZE /
+# WRITE_SIZE passes over this same bench command (tools/pmc_traffic.sh; FETCH doubled
+# per the gfx950 correction, cross-checked on k_diff's known byte count)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "e_traffic", "pmc_traffic.json")
+
+
+def measured_traffic(kernel, scale):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (C3 only)."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if scale != 24 or kernel not in t:
+        return None, None
+    return t[kernel]["traffic_bytes"], os.path.relpath(TRAFFIC_FILE, ROOT)
 
 
 def kernel_bytes(info, name):
@@ -165,6 +181,7 @@ def main():
     dom_ms = kms[dom] / ksteps
     dom_bytes = kernel_bytes(info, dom)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    traffic, traffic_src = measured_traffic(dom, scale)
     it_ms = sorted(st["iter_ms"])
     med_iter_ms = it_ms[len(it_ms) // 2]
     iter_bytes = 8 * info["arcs"] + 12 * info["slice"] + 8
@@ -196,7 +213,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "bytes_per_launch": dom_bytes,
             "avg_launch_ms": round(dom_ms, 4),
         },
