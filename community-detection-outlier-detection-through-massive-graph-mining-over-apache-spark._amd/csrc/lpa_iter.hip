@@ -112,6 +112,15 @@ __device__ __forceinline__ u64 wave_max_u64(u64 v) {
                 umax64(readlane_u64(v, 32), readlane_u64(v, 48)));
 }
 
+__device__ __forceinline__ u32 wave_sum_u32(u32 v) {
+  v += dpp_u32<0xB1>(v);
+  v += dpp_u32<0x4E>(v);
+  v += dpp_u32<0x141>(v);
+  v += dpp_u32<0x140>(v);
+  return (u32)__builtin_amdgcn_readlane((int)v, 0) + (u32)__builtin_amdgcn_readlane((int)v, 16) +
+         (u32)__builtin_amdgcn_readlane((int)v, 32) + (u32)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 __device__ __forceinline__ u32 hash_slot(u32 label, int shift) {
   return (label * 0x9E3779B1u) >> shift;
 }
@@ -179,10 +188,15 @@ __device__ __forceinline__ int lds_probe(u64* tab, u32 mask, u64 word, u32 h) {
 // ---------------------------------------------------------------------------
 constexpr int kPeelMax = 8;
 
+// The peel keeps its state per LANE in VGPRs (bit u of `mask` = this lane's label of
+// chunk u is not yet tallied) and counts with VALU compares + a DPP wave sum: a
+// compute unit issues one scalar instruction per cycle for all its waves but one
+// vector instruction per SIMD, and per-chunk ballot/and/popcount chains made the
+// steady-state tally kernels scalar-issue bound (SQ_INSTS_SALU 2.4x SQ_INSTS_VALU).
 template <int NC>
 struct Batch {
-  u64 act[NC];
-  int nact;
+  u32 mask;    // per lane: chunks whose label is still untallied
+  bool any;    // uniform: some lane still has an untallied label
   u64 pword;   // lane p: tally word of peel group p
   int npeel;   // uniform
   u64 pbest;   // uniform
@@ -190,43 +204,38 @@ struct Batch {
 
 template <int NC>
 __device__ __forceinline__ void peel_batch(Batch<NC>& bt, const u32 (&lab)[NC], int nch, int lane) {
-  bt.nact = 0;
+  u32 mask = 0u;
 #pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    bt.act[u] = u < nch ? __ballot(lab[u] != kNone) : 0ull;
-    bt.nact += __popcll(bt.act[u]);
-  }
+  for (int u = 0; u < NC; ++u)
+    if (u < nch && lab[u] != kNone) mask |= 1u << u;
   bt.pword = 0ull;
   bt.npeel = 0;
   bt.pbest = 0ull;
-#pragma unroll
+#pragma unroll 1
   for (int p = 0; p < kPeelMax; ++p) {
-    if (bt.nact == 0) break;
-    u32 x = 0u;
-    bool found = false;
+    const u64 live = __ballot(mask != 0u);
+    if (live == 0ull) break;
+    // candidate: the first untallied label of the first lane that has one
+    u32 cand = 0u;
 #pragma unroll
-    for (int u = 0; u < NC; ++u) {
-      if (!found && bt.act[u] != 0ull) {
-        x = (u32)__builtin_amdgcn_readlane((int)lab[u], __ffsll((unsigned long long)bt.act[u]) - 1);
-        found = true;
-      }
-    }
-    int c = 0;
+    for (int u = NC - 1; u >= 0; --u)
+      if ((mask >> u) & 1u) cand = lab[u];
+    const u32 x = (u32)__builtin_amdgcn_readlane((int)cand, __ffsll((unsigned long long)live) - 1);
+    u32 m = 0u;
 #pragma unroll
-    for (int u = 0; u < NC; ++u) {
-      if (u < nch) {
-        const u64 mm = __ballot(lab[u] == x) & bt.act[u];
-        bt.act[u] &= ~mm;
-        c += __popcll(mm);
-      }
-    }
-    bt.nact -= c;
-    const u64 word = tally((u32)c, x);
+    for (int u = 0; u < NC; ++u)
+      if (lab[u] == x) m |= 1u << u;
+    m &= mask;
+    mask &= ~m;
+    const u32 c = wave_sum_u32((u32)__popc(m));
+    const u64 word = tally(c, x);
     if (lane == p) bt.pword = word;
     bt.pbest = umax64(bt.pbest, word);
     bt.npeel = p + 1;
     if (c < 2) break;
   }
+  bt.mask = mask;
+  bt.any = __ballot(mask != 0u) != 0ull;
 }
 
 template <int NC>
@@ -241,7 +250,7 @@ __device__ __forceinline__ void hash_batch(u64* tab, uint16_t* lst, int& cnt, in
   for (int u = 0; u < NC; ++u) {
     old[u] = 0ull;
     hh[u] = 0u;
-    if (u < nch && ((bt.act[u] >> lane) & 1ull)) {
+    if (u < nch && ((bt.mask >> u) & 1u)) {
       hh[u] = hash_slot(lab[u], shift);
       old[u] = atomicCAS(&tab[hh[u]], 0ull, (1ull << 32) | (u64)(u32)(~lab[u]));
     }
@@ -250,7 +259,7 @@ __device__ __forceinline__ void hash_batch(u64* tab, uint16_t* lst, int& cnt, in
 #pragma unroll
   for (int u = 0; u < NC; ++u) {
     slot[u] = -1;
-    if (u < nch && ((bt.act[u] >> lane) & 1ull)) {
+    if (u < nch && ((bt.mask >> u) & 1u)) {
       const u64 word = (1ull << 32) | (u64)(u32)(~lab[u]);
       if (old[u] == 0ull) {
         slot[u] = (int)hh[u];
@@ -375,7 +384,7 @@ __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r
   const int nch = (d + 63) >> 6;
   Batch<NC> bt;
   peel_batch<NC>(bt, lab, nch, lane);
-  if (bt.nact == 0) {
+  if (!bt.any) {
     // every vote is in a peel group: the mode is their maximum, no LDS needed
     if (lane == 0) Ln[v] = (int32_t)(~(u32)bt.pbest);
   } else {
@@ -602,7 +611,7 @@ __device__ __forceinline__ void unit_tally(const u32 (&raw)[kChunks], const Segm
   u64* st = stage + d.begin;
   Batch<kChunks> bt;
   peel_batch<kChunks>(bt, lab, nch, lane);
-  if (bt.nact == 0) {
+  if (!bt.any) {
     // every vote is in a peel group: the unit's words are the peel groups
     if (lane < bt.npeel) st[lane] = bt.pword;
     if (lane == 0) ucnt[u] = bt.npeel;
