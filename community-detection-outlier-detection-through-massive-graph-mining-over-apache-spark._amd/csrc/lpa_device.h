@@ -119,22 +119,21 @@ __device__ __forceinline__ int lds_probe_word(u64* tab, u32 mask, u64 word, u32 
   return -1;
 }
 
-// Batched insert of NC chunks of tally words (lane l of chunk c inserts wv[c]
-// when bit l of act[c] is set): every first-probe CAS is issued before any is
-// resolved, so NC independent LDS atomics per lane are in flight instead of one
-// dependent chain per word; a key match adds the count (no return value), a
-// collision probes on.  slot[c] = the slot this lane claimed, or -1.
+// Batched insert of NC chunks of tally words (this lane inserts wv[c] when bit c of
+// its `lmask` is set): every first-probe CAS is issued before any is resolved, so
+// NC independent LDS atomics per lane are in flight instead of one dependent chain
+// per word; a key match adds the count (no return value), a collision probes on.
+// slot[c] = the slot this lane claimed, or -1.
 template <int NC, bool kBounded = false>
 __device__ __forceinline__ void insert_words(u64* tab, int shift, u32 mask, const u64 (&wv)[NC],
-                                             const u64 (&act)[NC], int lane, int (&slot)[NC],
-                                             int32_t* err) {
+                                             u32 lmask, int (&slot)[NC], int32_t* err) {
   u64 old[NC];
   u32 hh[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     old[c] = 0ull;
     hh[c] = 0u;
-    if ((act[c] >> lane) & 1ull) {
+    if ((lmask >> c) & 1u) {
       hh[c] = hash_slot(~(u32)wv[c], shift);
       old[c] = atomicCAS(&tab[hh[c]], 0ull, wv[c]);
     }
@@ -142,7 +141,7 @@ __device__ __forceinline__ void insert_words(u64* tab, int shift, u32 mask, cons
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     slot[c] = -1;
-    if ((act[c] >> lane) & 1ull) {
+    if ((lmask >> c) & 1u) {
       if (old[c] == 0ull) {
         slot[c] = (int)hh[c];
       } else if ((u32)old[c] == (u32)wv[c]) {
@@ -152,6 +151,44 @@ __device__ __forceinline__ void insert_words(u64* tab, int shift, u32 mask, cons
       }
     }
   }
+}
+
+// Weighted peel over NC chunks of tally words with per-lane state (bit c of
+// `lmask`: word c still untallied): each round takes the first untallied label of
+// the first lane holding one, sums its words' counts (VALU + DPP wave sums, no
+// per-chunk scalar mask chains) and retires them; repeated while a round retires
+// >= 2 words, up to `rounds`.  Round p's tally word ends in lane p's *pw; *best is
+// the maximum; returns the number of rounds.
+template <int NC>
+__device__ __forceinline__ int peel_words(const u64 (&wv)[NC], u32& lmask, u64& best, u64& pw,
+                                          int lane, int rounds) {
+  int np = 0;
+#pragma unroll 1
+  for (int p = 0; p < rounds; ++p) {
+    const u64 live = __ballot(lmask != 0u);
+    if (live == 0ull) break;
+    u32 cand = 0u;
+#pragma unroll
+    for (int c = NC - 1; c >= 0; --c)
+      if ((lmask >> c) & 1u) cand = ~(u32)wv[c];
+    const u32 x = (u32)__builtin_amdgcn_readlane((int)cand, __ffsll((unsigned long long)live) - 1);
+    u32 m = 0u, cs = 0u;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (((lmask >> c) & 1u) && ~(u32)wv[c] == x) {
+        m |= 1u << c;
+        cs += (u32)(wv[c] >> 32);
+      }
+    }
+    lmask &= ~m;
+    const u32 k = wave_sum_u32((u32)__popc(m));
+    const u64 tw = tally(wave_sum_u32(cs), x);
+    best = umax64(best, tw);
+    if (lane == p) pw = tw;
+    np = p + 1;
+    if (k < 2) break;
+  }
+  return np;
 }
 
 // Append the claimed slots of NC chunks to a block-shared LDS list with ONE

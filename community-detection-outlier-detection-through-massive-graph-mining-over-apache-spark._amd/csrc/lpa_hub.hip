@@ -357,21 +357,18 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, int64_t n_hub
         }
       }
     }
-    u64 act[NC];
-    int nact = 0;
+    u32 lmask = 0u;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      act[c] = __ballot(wv[c] != 0ull);
-      nact += __popcll(act[c]);
-    }
+    for (int c = 0; c < NC; ++c)
+      if (wv[c] != 0ull) lmask |= 1u << c;
     u64 best = 0ull, pw = 0ull;
-    weighted_peel<NC>(wv, act, nact, best, pw, lane);
-    if (nact > 0) {
+    peel_words<NC>(wv, lmask, best, pw, lane, kPeelRounds);
+    if (__ballot(lmask != 0u)) {
       int lg = ceil_log2(2u * (u32)T);
       lg = lg < 6 ? 6 : lg;
       const u32 mask = (1u << lg) - 1u;
       int slot[NC];
-      insert_words<NC>(tab, 32 - lg, mask, wv, act, lane, slot, nullptr);
+      insert_words<NC>(tab, 32 - lg, mask, wv, lmask, slot, nullptr);
       // the wave owns its table and list: claimed slots appended by ballot prefix
       const u64 lt = (1ull << lane) - 1ull;
       int n = 0;
@@ -413,11 +410,12 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
 #pragma unroll
     for (int k = 0; k < kFirst; ++k) fv[k] = k < nj ? src[k] : 0ull;
     {
-      u64 fa[kFirst];
+      u32 fa = 0u;
       int sl[kFirst];
 #pragma unroll
-      for (int k = 0; k < kFirst; ++k) fa[k] = __ballot(fv[k] != 0ull && keep(~(u32)fv[k]));
-      insert_words<kFirst>(tab, 32 - kLg, (1u << kLg) - 1u, fv, fa, lane, sl, err);
+      for (int k = 0; k < kFirst; ++k)
+        if (fv[k] != 0ull && keep(~(u32)fv[k])) fa |= 1u << k;
+      insert_words<kFirst>(tab, 32 - kLg, (1u << kLg) - 1u, fv, fa, sl, err);
       list_append_n<kFirst>(lst, lcount, sl, lane);
     }
     // longer units one at a time, the next one's words loading meanwhile
@@ -445,11 +443,12 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
       int nn = 0;
       load_big(big, wn, nn);
       {
-        u64 wa[NC];
+        u32 wa = 0u;
         int sl[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) wa[c] = __ballot(wv[c] != 0ull && keep(~(u32)wv[c]));
-        insert_words<NC>(tab, 32 - kLg, (1u << kLg) - 1u, wv, wa, lane, sl, err);
+        for (int c = 0; c < NC; ++c)
+          if (wv[c] != 0ull && keep(~(u32)wv[c])) wa |= 1u << c;
+        insert_words<NC>(tab, 32 - kLg, (1u << kLg) - 1u, wv, wa, sl, err);
         list_append_n<NC>(lst, lcount, sl, lane);
       }
 #pragma unroll
