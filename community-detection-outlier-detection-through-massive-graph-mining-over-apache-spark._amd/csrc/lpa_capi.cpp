@@ -124,6 +124,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   g->device = device;
   if (const char* f = getenv("LPA_REBUILD_FRAC")) g->rebuild_frac = atof(f);
   if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
+  if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {

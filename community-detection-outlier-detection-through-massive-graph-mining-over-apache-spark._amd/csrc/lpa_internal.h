@@ -147,6 +147,7 @@ struct lpa_graph {
   int64_t n_chunk_cap = 0;
   lpa::u64* chunks = nullptr;   // changed-vertex position chunks: (u << 32 | chunk index)
   double rebuild_frac = lpa::kRebuildFrac;  // LPA_REBUILD_FRAC overrides (tuning experiments)
+  int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   unsigned long long* counters = nullptr;  // [0] chunk count, [1] dirty arcs, [2] changed vertices
 

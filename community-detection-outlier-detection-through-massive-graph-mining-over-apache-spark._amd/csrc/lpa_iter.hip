@@ -904,11 +904,15 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
 // k on its own stream (0 units, 1 hub combine, 2..11 bins w8 .. g1).
 int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
   hipStream_t s = g->stream;
-  hipStream_t sb = g->aux_stream[0], sc = g->aux_stream[1];
+  // LPA_SERIAL=1 (profiling only): every tally kernel on the main stream, so a
+  // kernel trace shows each kernel's standalone duration
+  hipStream_t sb = g->serial ? s : g->aux_stream[0], sc = g->serial ? s : g->aux_stream[1];
   const int64_t* bb = g->bin_begin;
-  LPA_HIP(hipEventRecord(g->ev_fork, s));
-  LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
-  LPA_HIP(hipStreamWaitEvent(sc, g->ev_fork, 0));
+  if (!g->serial) {
+    LPA_HIP(hipEventRecord(g->ev_fork, s));
+    LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
+    LPA_HIP(hipStreamWaitEvent(sc, g->ev_fork, 0));
+  }
   auto mark = [&](int i, hipStream_t st) -> int {
     if (bev) LPA_HIP(hipEventRecord(bev[i], st));
     return LPA_OK;
@@ -971,13 +975,15 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
   // hub combine after the bins are queued: its tail kernels on the aux streams
   // run after those streams' bins
   LPA_TRY(mark(2, s));
-  LPA_TRY(launch_hub_combine(g, Lown, g->since_reset < kDenseSupersteps));
+  LPA_TRY(launch_hub_combine(g, Lown, !g->serial && g->since_reset < kDenseSupersteps));
   LPA_TRACE_POINT("hub_combine");
   LPA_TRY(mark(3, s));
-  LPA_HIP(hipEventRecord(g->ev_join[0], sb));
-  LPA_HIP(hipEventRecord(g->ev_join[1], sc));
-  LPA_HIP(hipStreamWaitEvent(s, g->ev_join[0], 0));
-  LPA_HIP(hipStreamWaitEvent(s, g->ev_join[1], 0));
+  if (!g->serial) {
+    LPA_HIP(hipEventRecord(g->ev_join[0], sb));
+    LPA_HIP(hipEventRecord(g->ev_join[1], sc));
+    LPA_HIP(hipStreamWaitEvent(s, g->ev_join[0], 0));
+    LPA_HIP(hipStreamWaitEvent(s, g->ev_join[1], 0));
+  }
   return LPA_OK;
 }
 
