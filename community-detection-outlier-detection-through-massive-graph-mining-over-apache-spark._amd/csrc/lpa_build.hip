@@ -337,7 +337,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     // the last entry finds the hubs (rows longer than one segment)
     int32_t thr_h[LPA_NBINS];
     for (int b = 1; b < LPA_NBINS; ++b) thr_h[b - 1] = kBinMaxDeg[b];
-    thr_h[LPA_NBINS - 1] = kSegArcs;
+    thr_h[LPA_NBINS - 1] = kWideMaxDeg;
     int32_t* d_thr = nullptr;
     int64_t* d_bb = nullptr;
     LPA_HIP(hipMalloc((void**)&d_thr, sizeof(thr_h)));

@@ -19,16 +19,17 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));  // native 16-B vector 
 // Degree bins (SURVEY.md §7 kernel inventory).  Vertices of a rank's slice are
 // sorted by degree (descending), so every bin is one contiguous range.
 // ---------------------------------------------------------------------------
-//   seg  deg > 512          wave per 512-arc unit, staged     (k_lpa_units + hub combine)
-//   w8/w4/w2  deg <= 512/256/128   wave per vertex, 8/4/2 chunks (k_lpa_wave<NC>)
+//   seg  deg > 1024         wave per 512-arc unit, staged     (k_lpa_units + hub combine)
+//   w16/w8/w4/w2  deg <= 1024/512/256/128   wave per vertex, NC chunks (k_lpa_wave<NC>)
 //   g64 .. g1 deg <= G          G lanes per vertex                (k_lpa_group<G>)
-enum Bin { BIN_SEG = 0, BIN_W8 = 1, BIN_W4 = 2, BIN_W2 = 3, BIN_G64 = 4, BIN_G32 = 5, BIN_G16 = 6,
-           BIN_G8 = 7, BIN_G4 = 8, BIN_G2 = 9, BIN_G1 = 10, BIN_ISO = 11 };
+enum Bin { BIN_SEG = 0, BIN_W16 = 1, BIN_W8 = 2, BIN_W4 = 3, BIN_W2 = 4, BIN_G64 = 5, BIN_G32 = 6,
+           BIN_G16 = 7, BIN_G8 = 8, BIN_G4 = 9, BIN_G2 = 10, BIN_G1 = 11, BIN_ISO = 12 };
 static_assert(BIN_ISO + 1 == LPA_NBINS, "bin table");
 // upper degree bound of each bin (bin b holds bin_max[b+1] < deg <= bin_max[b])
-constexpr int kBinMaxDeg[LPA_NBINS] = {1 << 30, 512, 256, 128, 64, 32, 16, 8, 4, 2, 1, 0};
+constexpr int kBinMaxDeg[LPA_NBINS] = {1 << 30, 1024, 512, 256, 128, 64, 32, 16, 8, 4, 2, 1, 0};
 
 constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 64 < deg <= 512
+constexpr int kWideMaxDeg = 1024;     // ... and (w16, 16 chunks, 2048-slot table) up to 1024
 constexpr int kSegArcs = 512;         // arcs per unit of a seg-bin row (one wave)
 constexpr int kTallyEv = 2 * (LPA_NKERNELS - 1);  // events bracketing each tally kernel
 constexpr int kBinEvents = kTallyEv + 3;           // + join, exchange, refresh marks
@@ -117,7 +118,7 @@ struct lpa_graph {
   // runs partitioned into label-hash buckets (scat[], same layout as stage[]).
   lpa::Segment* segs = nullptr;
   int64_t n_segs = 0;
-  int64_t n_hub = 0;              // rows with > kSegArcs arcs (= the seg bin)
+  int64_t n_hub = 0;              // rows with > kWideMaxDeg arcs (= the seg bin)
   lpa::u64* stage = nullptr;      // [hub arcs] staged unit tally words (unit j of row h:
                                   //  stage[rp[h] + j*kSegArcs ...), ucnt[hub_uoff[h] + j] words)
   int64_t* hub_uoff = nullptr;    // [n_hub + 1] first unit of each row (units = segs[])

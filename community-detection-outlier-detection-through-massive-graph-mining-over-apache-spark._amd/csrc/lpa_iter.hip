@@ -76,6 +76,7 @@ constexpr int kChunks = 8;    // 64-arc chunks per wave: a wave-bin row / a quar
 constexpr u32 kNone = 0xFFFFFFFFu;  // empty lane
 static_assert(kSegArcs == 64 * kChunks, "a unit is one batch of chunks");
 static_assert(kWaveMaxDeg == 64 * kChunks, "a wave-bin row fits one batch of chunks");
+static_assert(kWideMaxDeg == 2 * kWaveMaxDeg, "w16 rows: 16 chunks");
 
 __device__ __forceinline__ u32 ld_stream(const int32_t* p) {
   return (u32)__builtin_nontemporal_load(p);
@@ -244,43 +245,51 @@ __device__ __forceinline__ void hash_batch(u64* tab, uint16_t* lst, int& cnt, in
                                            int lane, u64 lt) {
   int pslot = -1;
   if (lane < bt.npeel) pslot = lds_insert(tab, shift, mask, ~(u32)bt.pword, (u32)(bt.pword >> 32));
-  u64 old[NC];
-  u32 hh[NC];
-#pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    old[u] = 0ull;
-    hh[u] = 0u;
-    if (u < nch && ((bt.mask >> u) & 1u)) {
-      hh[u] = hash_slot(lab[u], shift);
-      old[u] = atomicCAS(&tab[hh[u]], 0ull, (1ull << 32) | (u64)(u32)(~lab[u]));
-    }
-  }
-  int slot[NC];
-#pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    slot[u] = -1;
-    if (u < nch && ((bt.mask >> u) & 1u)) {
-      const u64 word = (1ull << 32) | (u64)(u32)(~lab[u]);
-      if (old[u] == 0ull) {
-        slot[u] = (int)hh[u];
-      } else if ((u32)old[u] == (u32)word) {
-        atomicAdd(&tab[hh[u]], 1ull << 32);
-      } else {
-        slot[u] = lds_probe(tab, mask, word, hh[u]);
-      }
-    }
-  }
   {
     const u64 cm = __ballot(pslot >= 0);
     if (pslot >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)pslot;
     cnt += __popcll(cm);
   }
+  // chunks in groups of up to 8 (bounded registers for the in-flight CAS results)
+  constexpr int H = NC < 8 ? NC : 8;
 #pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    if (u < nch) {
-      const u64 cm = __ballot(slot[u] >= 0);
-      if (slot[u] >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)slot[u];
-      cnt += __popcll(cm);
+  for (int h0 = 0; h0 < NC; h0 += H) {
+    if (h0 >= nch) break;  // uniform
+    u64 old[H];
+    u32 hh[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const int u = h0 + k;
+      old[k] = 0ull;
+      hh[k] = 0u;
+      if (u < nch && ((bt.mask >> u) & 1u)) {
+        hh[k] = hash_slot(lab[u], shift);
+        old[k] = atomicCAS(&tab[hh[k]], 0ull, (1ull << 32) | (u64)(u32)(~lab[u]));
+      }
+    }
+    int slot[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const int u = h0 + k;
+      slot[k] = -1;
+      if (u < nch && ((bt.mask >> u) & 1u)) {
+        const u64 word = (1ull << 32) | (u64)(u32)(~lab[u]);
+        if (old[k] == 0ull) {
+          slot[k] = (int)hh[k];
+        } else if ((u32)old[k] == (u32)word) {
+          atomicAdd(&tab[hh[k]], 1ull << 32);
+        } else {
+          slot[k] = lds_probe(tab, mask, word, hh[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      if (h0 + k < nch) {
+        const u64 cm = __ballot(slot[k] >= 0);
+        if (slot[k] >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)slot[k];
+        cnt += __popcll(cm);
+      }
     }
   }
 }
@@ -959,6 +968,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
   }
+  LPA_WAVE_LAUNCH(BIN_W16, 16)
   LPA_WAVE_LAUNCH(BIN_W8, 8)
   LPA_WAVE_LAUNCH(BIN_W4, 4)
   LPA_WAVE_LAUNCH(BIN_W2, 2)

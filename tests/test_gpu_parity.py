@@ -89,7 +89,7 @@ def test_degree_mix_all_bins(gfa, oracle, seed):
         info = g.info()
         assert info["hub_vertices"] >= 2 and info["bin_vertices"]["seg"] == info["hub_vertices"]
         assert all(info["bin_vertices"][b] > 0 for b in
-                   ("w8", "w4", "w2", "g64", "g32", "g16", "g8", "g4", "g2", "g1")), info["bin_vertices"]
+                   ("w16", "w8", "w4", "w2", "g64", "g32", "g16", "g8", "g4", "g2", "g1")), info["bin_vertices"]
     _, hist, _ = oracle.lpa(V, s, d, 6, per_iter=True)
     got = _per_step(gfa, V, s, d, 6)
     for t in range(6):
