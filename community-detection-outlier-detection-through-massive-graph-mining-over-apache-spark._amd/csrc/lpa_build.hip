@@ -328,8 +328,8 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   LPA_TRY(dev_alloc(g, (void**)&g->al, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
   g->n_chunk_cap = arcs / kChunkPos + g->vpad + 1;
   LPA_TRY(dev_alloc(g, (void**)&g->chunks, sizeof(u64) * g->n_chunk_cap));
-  LPA_TRY(dev_alloc(g, (void**)&g->counters, sizeof(unsigned long long) * 4));
-  LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 4, s));
+  LPA_TRY(dev_alloc(g, (void**)&g->counters, sizeof(unsigned long long) * 8));  // 2 parities
+  LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 8, s));
 
   // ---- 4. degree bins (contiguous slot ranges) ----
   {

@@ -722,8 +722,11 @@ __global__ __launch_bounds__(256) void k_hub_final(const int32_t* __restrict__ l
                                                    const int64_t* __restrict__ hoff,
                                                    int32_t* __restrict__ ghist,
                                                    u64* __restrict__ hub_best,
-                                                   int32_t* __restrict__ Ln) {
+                                                   int32_t* __restrict__ Ln,
+                                                   int32_t* __restrict__ lcnt_next) {
   const int lane = threadIdx.x & 63;
+  // the next superstep's queue counters (the other parity; no memset launch)
+  if (blockIdx.x == 0 && threadIdx.x < 8) lcnt_next[threadIdx.x] = 0;
   const int nC = lcnt[1];
   for (int q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nC; q += gridDim.x * 4) {
     const int64_t h = listC[q];
@@ -809,7 +812,8 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   LPA_TRY(dev_alloc(g, (void**)&g->ghist, sizeof(int32_t) * nbk));
   LPA_TRY(dev_alloc(g, (void**)&g->gcur, sizeof(int32_t) * nbk));
   LPA_TRY(dev_alloc(g, (void**)&g->hub_lists, sizeof(int32_t) * 5 * n));
-  LPA_TRY(dev_alloc(g, (void**)&g->hub_lcnt, sizeof(int32_t) * 8));
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_lcnt, sizeof(int32_t) * 16));
+  LPA_HIP(hipMemsetAsync(g->hub_lcnt, 0, sizeof(int32_t) * 16, s));
   {
     // rows [hub_lane_begin, n_hub) have <= kLaneUnits units (degree-descending order)
     int64_t* d_pos = nullptr;
@@ -834,16 +838,17 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   hipStream_t s = g->stream;
   int32_t* lists = g->hub_lists;
   int32_t* listC = g->hub_lists + n;
-  LPA_HIP(hipMemsetAsync(g->hub_lcnt, 0, sizeof(int32_t) * 8, s));
+  // queue counters of this superstep's parity (zeroed by the previous k_hub_final)
+  int32_t* lcnt = g->hub_lcnt + 8 * g->par;
   const int64_t hl = g->hub_lane_begin;
   int32_t* listW = g->hub_lists + 2 * n;
   if (hl < n) {
     hipLaunchKernelGGL(k_hub_lanes, dim3(grid_cap((n - hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
-                       g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, listW, g->hub_lcnt);
+                       g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, listW, lcnt);
     LPA_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, hl, n, g->rp, g->hub_uoff, g->ucnt,
-                     g->stage, g->hub_wcount, Lown, lists, g->hub_lcnt, g->items_cb, g->items_cc);
+                     g->stage, g->hub_wcount, Lown, lists, lcnt, g->items_cb, g->items_cc);
   LPA_HIP(hipGetLastError());
   // the mid tiers and the bucket path are independent.  fork: the 8192- and
   // 4096-slot tiers run on the main stream, the 2048-slot tier and the bucket path
@@ -857,32 +862,33 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
     LPA_HIP(hipStreamWaitEvent(sd, g->ev_fork2, 0));
   }
   hipLaunchKernelGGL(k_hub_mid<13>, dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,
-                     g->hub_lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
+                     lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
                      g->dev_err);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_hub_mid<12>, dim3(grid_cap(n, 1024)), dim3(256), 0, s, lists + 3 * n,
-                     g->hub_lcnt, 5, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
+                     lcnt, 5, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
                      g->dev_err);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_mid<11>, dim3(grid_cap(n, 2048)), dim3(256), 0, sd, lists, g->hub_lcnt, 0,
+  hipLaunchKernelGGL(k_hub_mid<11>, dim3(grid_cap(n, 2048)), dim3(256), 0, sd, lists, lcnt, 0,
                      g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
   LPA_HIP(hipGetLastError());
   const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
-  hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, sd, g->items_cc, g->hub_lcnt, g->rp,
+  hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
                      g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->ghist);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_hub_scan, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
-                     g->hub_lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->gcur);
+                     lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->gcur);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, sd, g->items_cc, g->hub_lcnt, g->rp,
+  hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
                      g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->gcur, g->scat);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_hub_bucket, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, sd,
-                     g->items_cb, g->hub_lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
+                     g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
                      g->hub_best, g->dev_err);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
-                     g->hub_lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown);
+                     lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown,
+                     g->hub_lcnt + 8 * (g->par ^ 1));
   LPA_HIP(hipGetLastError());
   if (fork) {
     LPA_HIP(hipEventRecord(g->ev_join2[0], sd));

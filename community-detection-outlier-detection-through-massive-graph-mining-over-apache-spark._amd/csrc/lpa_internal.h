@@ -106,6 +106,7 @@ struct lpa_graph {
   int32_t* deg = nullptr;     // [V] symmetrised degree by dense id
   int32_t* lab[2] = {nullptr, nullptr};  // [vpad] ping-pong label vectors (replicated)
   int cur = 0;                // index of the current label vector
+  int par = 0;                // superstep parity: which counter / queue-count set is live
   int64_t since_reset = 0;    // supersteps run since the labels were last L0
 
   // degree bins over the owned slice
@@ -131,7 +132,7 @@ struct lpa_graph {
   int32_t* gcur = nullptr;        // [n_hub_buckets] bucket offsets / scatter cursors
   int32_t* hub_lists = nullptr;   // [5 n_hub] queued rows: mid (T <= 1024), bucketed, wave path,
                                   //   mid (T <= 2048), mid (T <= 6144)
-  int32_t* hub_lcnt = nullptr;    // [8] queue lengths: mid1, bucketed, bucket items, chunk items,
+  int32_t* hub_lcnt = nullptr;    // [2][8] per parity, queue lengths: mid1, bucketed, bucket items, chunk items,
                                   //     wave path, mid2, mid3
   int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
   lpa::u64* items_cb = nullptr;   // [n_hub_buckets] (hub << 32 | bucket)
@@ -150,7 +151,7 @@ struct lpa_graph {
   double rebuild_frac = lpa::kRebuildFrac;  // LPA_REBUILD_FRAC overrides (tuning experiments)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
-  unsigned long long* counters = nullptr;  // [0] chunk count, [1] dirty arcs, [2] changed vertices
+  unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
   lpa::u64* dsend = nullptr;                 // [slice] this rank's (slot << 32 | label)

@@ -770,10 +770,13 @@ __device__ __forceinline__ bool rebuild_wanted(const unsigned long long* counter
 // ones by the whole wave (coalesced cpos).
 __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chunks,
                                                     const unsigned long long* __restrict__ counters,
+                                                    unsigned long long* __restrict__ counters_next,
                                                     const int64_t* __restrict__ cptr,
                                                     const uint32_t* __restrict__ cpos,
                                                     const int32_t* __restrict__ Ln,
                                                     int32_t* __restrict__ al, int64_t thr) {
+  // the next superstep's counters (the other parity; no memset launch)
+  if (blockIdx.x == 0 && threadIdx.x < 2) counters_next[threadIdx.x] = 0ull;
   if (rebuild_wanted(counters, thr)) return;
   const int64_t nchunks = (int64_t)counters[0];
   const int lane = threadIdx.x & 63;
@@ -934,16 +937,16 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
     LPA_TRACE_POINT("seg");
   }
   LPA_TRY(mark(1, s));
-#define LPA_WAVE_LAUNCH(BIN, NC)                                                              \
+#define LPA_WAVE_LAUNCH(BIN, NC, ST)                                                              \
   {                                                                                           \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                  \
-    LPA_TRY(mark(2 * (BIN + 1), sb));                                                         \
+    LPA_TRY(mark(2 * (BIN + 1), ST));                                                         \
     if (n > 0) {                                                                              \
-      hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, sb,  \
+      hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, ST,  \
                          g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                          \
       LPA_HIP(hipGetLastError());                                                             \
     }                                                                                         \
-    LPA_TRY(mark(2 * (BIN + 1) + 1, sb));                                                     \
+    LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                     \
   }
 #define LPA_GROUP_LAUNCH(BIN, G)                                                             \
   {                                                                                          \
@@ -968,10 +971,12 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
   }
-  LPA_WAVE_LAUNCH(BIN_W16, 16)
-  LPA_WAVE_LAUNCH(BIN_W8, 8)
-  LPA_WAVE_LAUNCH(BIN_W4, 4)
-  LPA_WAVE_LAUNCH(BIN_W2, 2)
+  // stream balance (measured steady superstep): aux0 w16 + w8 + w4, aux1 w2 + the
+  // row/group bins
+  LPA_WAVE_LAUNCH(BIN_W16, 16, sb)
+  LPA_WAVE_LAUNCH(BIN_W8, 8, sb)
+  LPA_WAVE_LAUNCH(BIN_W4, 4, sb)
+  LPA_WAVE_LAUNCH(BIN_W2, 2, sc)
   LPA_ROWS_LAUNCH(BIN_G64, 64)
   LPA_ROWS_LAUNCH(BIN_G32, 32)
   LPA_ROWS_LAUNCH(BIN_G16, 16)
@@ -999,25 +1004,26 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
 
 // al[] rebuild: the LDS hot-label kernel on a single-GPU handle (hub slots are
 // [0, kHotLabels) there), the plain one otherwise
-int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L) {
+int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
+                   const unsigned long long* ctr) {
   hipStream_t s = g->stream;
   if (g->nranks == 1 && g->rebuild_hot) {
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
     const int32_t nhot = (int32_t)(g->vpad < kHotLabels ? g->vpad : kHotLabels);
     if (if_wanted)
-      hipLaunchKernelGGL(k_al_rebuild_hot<true>, dim3(dev_cus), dim3(1024), 0, s, g->counters, thr,
+      hipLaunchKernelGGL(k_al_rebuild_hot<true>, dim3(dev_cus), dim3(1024), 0, s, ctr, thr,
                          g->col, g->arcs, L, nhot, g->al);
     else
-      hipLaunchKernelGGL(k_al_rebuild_hot<false>, dim3(dev_cus), dim3(1024), 0, s, g->counters, thr,
+      hipLaunchKernelGGL(k_al_rebuild_hot<false>, dim3(dev_cus), dim3(1024), 0, s, ctr, thr,
                          g->col, g->arcs, L, nhot, g->al);
   } else {
     const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
     if (if_wanted)
-      hipLaunchKernelGGL(k_al_rebuild<true>, dim3(grid), dim3(256), 0, s, g->counters, thr, g->col,
+      hipLaunchKernelGGL(k_al_rebuild<true>, dim3(grid), dim3(256), 0, s, ctr, thr, g->col,
                          g->arcs, L, g->al);
     else
-      hipLaunchKernelGGL(k_al_rebuild<false>, dim3(grid), dim3(256), 0, s, g->counters, thr, g->col,
+      hipLaunchKernelGGL(k_al_rebuild<false>, dim3(grid), dim3(256), 0, s, ctr, thr, g->col,
                          g->arcs, L, g->al);
   }
   LPA_HIP(hipGetLastError());
@@ -1028,18 +1034,20 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L) 
 int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
   if (g->arcs == 0) return LPA_OK;
   hipStream_t s = g->stream;
-  LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 2, s));
+  // this superstep's counters (zeroed by the previous k_al_scatter or at build)
+  unsigned long long* ctr = g->counters + 4 * g->par;
   hipLaunchKernelGGL(k_diff, dim3((unsigned)((g->vpad / 4 + kDiffQuads - 1) / kDiffQuads)), dim3(256),
                      0, s, (const int4*)Lc, (const int4*)Ln, g->vpad / 4, g->cptr, g->chunks,
-                     g->counters);
+                     ctr);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("diff");
   const int64_t thr = (int64_t)(g->rebuild_frac * (double)g->arcs);
-  hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, g->counters, g->cptr,
+  hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, ctr,
+                     g->counters + 4 * (g->par ^ 1), g->cptr,
                      g->cpos, Ln, g->al, thr);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
-  LPA_TRY(launch_rebuild(g, true, thr, Ln));
+  LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -1079,6 +1087,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     }
     g->cur ^= 1;
+    g->par ^= 1;
     ++g->since_reset;
   }
   if (timed) LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS + 1], s));
@@ -1117,7 +1126,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
 
 int rebuild_arc_labels(lpa_graph* g) {
   if (g->arcs == 0) return LPA_OK;
-  return launch_rebuild(g, false, 0, g->lab[g->cur]);
+  return launch_rebuild(g, false, 0, g->lab[g->cur], g->counters);
 }
 
 int gather_labels(lpa_graph* g, int32_t* out_dense_dev) {
