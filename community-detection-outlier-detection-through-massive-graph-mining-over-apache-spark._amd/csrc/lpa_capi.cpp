@@ -284,6 +284,15 @@ int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t*
   return LPA_OK;
 }
 
+int lpa_set_serial(lpa_graph* g, int32_t serial) {
+  if (!g) {
+    set_error("null handle");
+    return LPA_EINVAL;
+  }
+  g->serial = serial ? 1 : 0;
+  return LPA_OK;
+}
+
 int lpa_set_stream(lpa_graph* g, void* hip_stream) {
   if (!g) {
     set_error("null handle");

@@ -134,6 +134,10 @@ class Graph:
         _lib.check(self._lib.lpa_degrees(self._handle(), deg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return deg
 
+    def set_serial(self, serial: bool = True):
+        """Profiling: queue every tally kernel on one stream (standalone kernel times)."""
+        _lib.check(self._lib.lpa_set_serial(self._handle(), int(bool(serial))))
+
     # -- caller-driven exchange (virtual ranks) -------------------------------
     def exchange_get(self) -> np.ndarray:
         sl = np.empty(self.info()["slice"], dtype=np.int32)

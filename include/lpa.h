@@ -133,6 +133,10 @@ int lpa_exchange_put(lpa_graph* g, const int32_t* full_in);
 int lpa_exchange_get_delta(lpa_graph* g, uint64_t* entries_out, int64_t* count_out);
 int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t* counts, int64_t cap);
 
+/* Profiling control: serial != 0 queues every tally kernel on the handle's main
+ * stream (no concurrent bins), so per-kernel times in lpa_stats are standalone
+ * durations.  Labels are identical either way. */
+int lpa_set_serial(lpa_graph* g, int32_t serial);
 /* Run on a caller-provided hipStream_t (NULL = the handle's own stream). */
 int lpa_set_stream(lpa_graph* g, void* hip_stream);
 

@@ -20,7 +20,7 @@ def per_kernel(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            m = re.search(r"(k_[A-Za-z0-9_]+)", r["Kernel_Name"])
+            m = re.search(r"(k_[A-Za-z0-9_]+(<[^>]*>)?)", r["Kernel_Name"])
             k = m.group(1) if m else r["Kernel_Name"]
             out.setdefault(k, []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     for k in out:
@@ -35,7 +35,7 @@ W, K = bench["warmup"], bench["steps"]
 lo, hi = 1 + W, 1 + W + K  # timed dispatches of a once-per-superstep kernel
 res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py --no-cpu-baseline",
        "timed_dispatches": [lo, hi - 1]}
-for k in ("k_lpa_units", "k_diff"):
+for k in sorted(fetch):
     f = [v for _, v in fetch.get(k, [])][lo:hi]
     w = [v for _, v in write.get(k, [])][lo:hi]
     if not f:
