@@ -183,6 +183,39 @@ __device__ __forceinline__ void queue_row(int64_t h, int T, int nu, int lane,
   }
 }
 
+// Label-dense supersteps: classify the rows of > kLaneUnits units right after the
+// unit tallies, so the bucket path (count / scan / scatter / bucket, complete once
+// these rows are queued: rows of <= kLaneUnits units never exceed kCombDirect words)
+// can start on its own stream while k_hub_small works through the rest.  Rows of
+// <= kSmallWords units and words go to list S for k_hub_small; the others are
+// queued with their word count as k_hub_small would.
+__global__ __launch_bounds__(256) void k_hub_classify(int64_t h_lane, int64_t n_hub,
+                                                      const int64_t* __restrict__ rp,
+                                                      const int64_t* __restrict__ uoff,
+                                                      const int32_t* __restrict__ ucnt,
+                                                      int32_t* __restrict__ wcount,
+                                                      int32_t* __restrict__ lists,
+                                                      int32_t* __restrict__ lcnt,
+                                                      u64* __restrict__ itemsCB,
+                                                      u64* __restrict__ itemsCC) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < h_lane; h += stride) {
+    const RowUnits ru = row_units(rp, uoff, h);
+    const int nu = ru.nu;
+    const int32_t* uc = ucnt + ru.u0;
+    int T = 0;
+    for (int j = lane; j < nu; j += 64) T += uc[j];
+    T = (int)wave_sum_u32((u32)T);
+    if (nu <= kSmallWords && T <= kSmallWords) {
+      if (lane == 0) lists[5 * n_hub + atomicAdd(&lcnt[7], 1)] = (int32_t)h;
+    } else {
+      queue_row(h, T, nu, lane, wcount, lists, n_hub, lcnt, itemsCB, itemsCC);
+    }
+  }
+}
+
 // weighted ballot peel over NC word chunks: rounds retire the first unretired
 // label's words; lane p ends with round p's tally word in *pw, returns rounds.
 template <int NC>
@@ -226,7 +259,7 @@ __device__ __forceinline__ int weighted_peel(const u64 (&wv)[NC], u64 (&act)[NC]
 //                                      (giant converged rows)
 //   otherwise                          queued with T in wcount[h]
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, int64_t n_hub,
+__global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
                                                    const int64_t* __restrict__ rp,
                                                    const int64_t* __restrict__ uoff,
                                                    const int32_t* __restrict__ ucnt,
@@ -247,10 +280,15 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t h_lane, int64_t n_hub
   int32_t* pre = aux_all[w];
   uint16_t* lst = reinterpret_cast<uint16_t*>(aux_all[w]);
   for (int i = lane; i < kSmallSlots; i += 64) tab[i] = 0ull;
-  const int64_t nq = h_lane + lcnt[4];
+  // rows: [0, nd) directly, then list S (pre-classified by k_hub_classify), then
+  // list W (from k_hub_lanes)
+  const int64_t nS = lcnt[7];
+  const int64_t nq = nd + nS + lcnt[4];
   const int64_t stride = (int64_t)gridDim.x * 4;
   for (int64_t q = (int64_t)blockIdx.x * 4 + w; q < nq; q += stride) {
-    const int64_t h = q < h_lane ? q : (int64_t)lists[2 * n_hub + (q - h_lane)];
+    const int64_t h = q < nd ? q
+                             : (q < nd + nS ? (int64_t)lists[5 * n_hub + (q - nd)]
+                                            : (int64_t)lists[2 * n_hub + (q - nd - nS)]);
     const RowUnits ru = row_units(rp, uoff, h);
     const int nu = ru.nu;
     const int32_t* uc = ucnt + ru.u0;
@@ -811,7 +849,7 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   LPA_TRY(dev_alloc(g, (void**)&g->hub_best, sizeof(u64) * n));
   LPA_TRY(dev_alloc(g, (void**)&g->ghist, sizeof(int32_t) * nbk));
   LPA_TRY(dev_alloc(g, (void**)&g->gcur, sizeof(int32_t) * nbk));
-  LPA_TRY(dev_alloc(g, (void**)&g->hub_lists, sizeof(int32_t) * 5 * n));
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_lists, sizeof(int32_t) * 6 * n));
   LPA_TRY(dev_alloc(g, (void**)&g->hub_lcnt, sizeof(int32_t) * 16));
   LPA_HIP(hipMemsetAsync(g->hub_lcnt, 0, sizeof(int32_t) * 16, s));
   {
@@ -842,25 +880,51 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   int32_t* lcnt = g->hub_lcnt + 8 * g->par;
   const int64_t hl = g->hub_lane_begin;
   int32_t* listW = g->hub_lists + 2 * n;
+  // fork (label-dense supersteps): classify the > 8-unit rows first and start the
+  // bucket path on its own stream; the mid tiers follow k_hub_small on the main
+  // stream.  Otherwise everything runs in order on the main stream.
+  hipStream_t sd = fork ? g->aux_stream[2] : s;
+  const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
+  auto bucket_path = [&]() -> int {
+    hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
+                       g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->ghist);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_scan, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
+                       lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->gcur);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
+                       g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->gcur, g->scat);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_bucket, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, sd,
+                       g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
+                       g->hub_best, g->dev_err);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
+                       lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown,
+                       g->hub_lcnt + 8 * (g->par ^ 1));
+    LPA_HIP(hipGetLastError());
+    return LPA_OK;
+  };
+  if (fork) {
+    if (hl > 0) {
+      hipLaunchKernelGGL(k_hub_classify, dim3(grid_cap((hl + 3) / 4, 2048)), dim3(256), 0, s, hl, n,
+                         g->rp, g->hub_uoff, g->ucnt, g->hub_wcount, lists, lcnt, g->items_cb,
+                         g->items_cc);
+      LPA_HIP(hipGetLastError());
+    }
+    LPA_HIP(hipEventRecord(g->ev_fork2, s));
+    LPA_HIP(hipStreamWaitEvent(sd, g->ev_fork2, 0));
+    LPA_TRY(bucket_path());
+  }
   if (hl < n) {
     hipLaunchKernelGGL(k_hub_lanes, dim3(grid_cap((n - hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
                        g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, listW, lcnt);
     LPA_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, hl, n, g->rp, g->hub_uoff, g->ucnt,
-                     g->stage, g->hub_wcount, Lown, lists, lcnt, g->items_cb, g->items_cc);
+  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, fork ? (int64_t)0 : hl, n, g->rp,
+                     g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, lists, lcnt, g->items_cb,
+                     g->items_cc);
   LPA_HIP(hipGetLastError());
-  // the mid tiers and the bucket path are independent.  fork: the 8192- and
-  // 4096-slot tiers run on the main stream, the 2048-slot tier and the bucket path
-  // on their own stream (not behind the tally bins of the other aux streams).  The
-  // caller forks only while the labels are still high-cardinality (the first
-  // supersteps after L0): converged supersteps queue ~5 us kernels here, and the
-  // extra cross-stream event pair costs more than their overlap saves.
-  hipStream_t sd = fork ? g->aux_stream[2] : s;
-  if (fork) {
-    LPA_HIP(hipEventRecord(g->ev_fork2, s));
-    LPA_HIP(hipStreamWaitEvent(sd, g->ev_fork2, 0));
-  }
   hipLaunchKernelGGL(k_hub_mid<13>, dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,
                      lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
                      g->dev_err);
@@ -869,27 +933,10 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
                      lcnt, 5, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
                      g->dev_err);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_mid<11>, dim3(grid_cap(n, 2048)), dim3(256), 0, sd, lists, lcnt, 0,
+  hipLaunchKernelGGL(k_hub_mid<11>, dim3(grid_cap(n, 2048)), dim3(256), 0, s, lists, lcnt, 0,
                      g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
   LPA_HIP(hipGetLastError());
-  const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
-  hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
-                     g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->ghist);
-  LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_scan, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
-                     lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->gcur);
-  LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
-                     g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->gcur, g->scat);
-  LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_bucket, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, sd,
-                     g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
-                     g->hub_best, g->dev_err);
-  LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
-                     lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown,
-                     g->hub_lcnt + 8 * (g->par ^ 1));
-  LPA_HIP(hipGetLastError());
+  if (!fork) LPA_TRY(bucket_path());
   if (fork) {
     LPA_HIP(hipEventRecord(g->ev_join2[0], sd));
     LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[0], 0));

@@ -130,10 +130,10 @@ struct lpa_graph {
   int64_t* hub_hoff = nullptr;    // [n_hub + 1] first bucket counter of each hub
   int32_t* ghist = nullptr;       // [n_hub_buckets] words per bucket
   int32_t* gcur = nullptr;        // [n_hub_buckets] bucket offsets / scatter cursors
-  int32_t* hub_lists = nullptr;   // [5 n_hub] queued rows: mid (T <= 1024), bucketed, wave path,
-                                  //   mid (T <= 2048), mid (T <= 6144)
-  int32_t* hub_lcnt = nullptr;    // [2][8] per parity, queue lengths: mid1, bucketed, bucket items, chunk items,
-                                  //     wave path, mid2, mid3
+  int32_t* hub_lists = nullptr;   // [6 n_hub] queued rows: mid (T <= 1024), bucketed, wave path,
+                                  //   mid (T <= 2048), mid (T <= 6144), small (list S)
+  int32_t* hub_lcnt = nullptr;    // [2][8] per parity, queue lengths: mid1, bucketed, bucket items,
+                                  //   chunk items, wave path, mid2, mid3, small (list S)
   int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
   lpa::u64* items_cb = nullptr;   // [n_hub_buckets] (hub << 32 | bucket)
   lpa::u64* items_cc = nullptr;   // [n_hub_chunks]  (hub << 32 | 8-unit chunk)
