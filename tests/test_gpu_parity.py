@@ -126,7 +126,7 @@ def test_generators_match_cpu_restatement(gfa, oracle):
     assert np.array_equal(s.cpu().numpy(), cs) and np.array_equal(d.cpu().numpy(), cd)
 
 
-@pytest.mark.parametrize("scale", [12, 16])
+@pytest.mark.parametrize("scale", [12, 16, 18])
 def test_rmat_bit_exact(gfa, oracle, scale):
     s, d = gfa.gen_rmat(scale, 16, seed=1)
     V = 1 << scale
@@ -138,6 +138,20 @@ def test_rmat_bit_exact(gfa, oracle, scale):
     _, hist, _ = oracle.lpa(V, s.cpu().numpy(), d.cpu().numpy(), 10, per_iter=True)
     for t in range(10):
         assert np.array_equal(got[t], hist[t]), f"R-MAT {scale} superstep {t + 1}"
+
+
+def test_schedules_identical(gfa):
+    """The concurrent four-stream schedule (forked hub combine in the label-dense
+    supersteps) and the serialized profiling schedule give identical labels."""
+    s, d = gfa.gen_rmat(17, 16, seed=3)
+    V = 1 << 17
+    with gfa.Graph(s, d, V) as g:
+        conc = [g.labels() for _ in range(6) if g.step(1) is not None or True]
+        g.reset()
+        g.set_serial(True)
+        ser = [g.labels() for _ in range(6) if g.step(1) is not None or True]
+    for t in range(6):
+        assert np.array_equal(conc[t], ser[t]), f"superstep {t + 1}"
 
 
 def test_sbm_bit_exact(gfa, oracle):
