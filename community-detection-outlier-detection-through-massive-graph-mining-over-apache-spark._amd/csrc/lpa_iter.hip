@@ -693,7 +693,7 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
 // with ONE global atomic (a global counter hit by every wave serialises).
 constexpr int kDiffQuads = 2048;  // quads (8192 slots) per block
 __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
-                                              const int4* __restrict__ Ln4, int64_t n4,
+                                              const int4* __restrict__ Ln4, int64_t s0, int64_t s1,
                                               const int64_t* __restrict__ cptr,
                                               u64* __restrict__ chunks,
                                               unsigned long long* __restrict__ counters) {
@@ -705,12 +705,19 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) qn = 0;
   __syncthreads();
-  const int64_t q0 = (int64_t)blockIdx.x * kDiffQuads;
-  const int64_t q1 = min(n4, q0 + kDiffQuads);
+  // slot range [s0, s1): quads [s0 / 4, ceil(s1 / 4)), lanes outside the range masked
+  // (the neighbouring slots may belong to a bin another stream is still computing)
+  const int64_t q0 = s0 / 4 + (int64_t)blockIdx.x * kDiffQuads;
+  const int64_t q1 = min((s1 + 3) / 4, q0 + kDiffQuads);
   unsigned long long dirty = 0;
   for (int64_t q = q0 + threadIdx.x; q < q1; q += 256) {
     const int4 a = Lc4[q], b = Ln4[q];
-    const int chg = (a.x != b.x) | ((a.y != b.y) << 1) | ((a.z != b.z) << 2) | ((a.w != b.w) << 3);
+    int chg = (a.x != b.x) | ((a.y != b.y) << 1) | ((a.z != b.z) << 2) | ((a.w != b.w) << 3);
+    if (q * 4 < s0 || q * 4 + 4 > s1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (q * 4 + k < s0 || q * 4 + k >= s1) chg &= ~(1 << k);
+    }
     if (chg) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -914,7 +921,14 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
 // them concurrently hides the ~2-5 us launch gap of each dependent kernel and the
 // tails of the small bins.  bev (nullable): events 2k / 2k+1 bracket tally kernel
 // k on its own stream (0 units, 1 hub combine, 2..11 bins w8 .. g1).
-int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
+int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* Ln, int64_t s0,
+                int64_t s1);
+
+// diff (P = 1, concurrent schedule): each stream diffs the slots its own bins
+// produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
+// rows after the hub combine), overlapping most of the diff with the tally tail
+int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc,
+                 const int32_t* Ln, bool diff) {
   hipStream_t s = g->stream;
   // LPA_SERIAL=1 (profiling only): every tally kernel on the main stream, so a
   // kernel trace shows each kernel's standalone duration
@@ -993,6 +1007,11 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev) {
   LPA_TRY(launch_hub_combine(g, Lown, !g->serial && g->since_reset < kDenseSupersteps));
   LPA_TRACE_POINT("hub_combine");
   LPA_TRY(mark(3, s));
+  if (diff) {
+    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2]));
+    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], g->vpad));
+    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16]));
+  }
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_join[0], sb));
     LPA_HIP(hipEventRecord(g->ev_join[1], sc));
@@ -1030,16 +1049,27 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
   return LPA_OK;
 }
 
-// refresh al[] for L_next (after the exchange, so every rank sees all changes)
-int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
+// changed slots in [s0, s1) -> position chunks + dirty-arc count (counters of this
+// superstep's parity)
+int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* Ln, int64_t s0,
+                int64_t s1) {
+  if (s1 <= s0) return LPA_OK;
+  const int64_t nq = (s1 + 3) / 4 - s0 / 4;
+  hipLaunchKernelGGL(k_diff, dim3((unsigned)((nq + kDiffQuads - 1) / kDiffQuads)), dim3(256), 0, st,
+                     (const int4*)Lc, (const int4*)Ln, s0, s1, g->cptr, g->chunks,
+                     g->counters + 4 * g->par);
+  LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
+
+// refresh al[] for L_next (after the exchange, so every rank sees all changes);
+// diff_done: the tally schedule already ran the diff per stream (launch_tally)
+int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done) {
   if (g->arcs == 0) return LPA_OK;
   hipStream_t s = g->stream;
   // this superstep's counters (zeroed by the previous k_al_scatter or at build)
   unsigned long long* ctr = g->counters + 4 * g->par;
-  hipLaunchKernelGGL(k_diff, dim3((unsigned)((g->vpad / 4 + kDiffQuads - 1) / kDiffQuads)), dim3(256),
-                     0, s, (const int4*)Lc, (const int4*)Ln, g->vpad / 4, g->cptr, g->chunks,
-                     ctr);
-  LPA_HIP(hipGetLastError());
+  if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, g->vpad));
   LPA_TRACE_POINT("diff");
   const int64_t thr = (int64_t)(g->rebuild_frac * (double)g->arcs);
   hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, ctr,
@@ -1076,12 +1106,13 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     const bool tt = timed && t < nt;
     hipEvent_t* bev = tt ? &g->bin_ev[t * kBinEvents] : nullptr;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
-    LPA_TRY(launch_tally(g, Lown, bev));
+    const bool diff_in_tally = g->nranks == 1 && !g->serial;
+    LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
     if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
     if (g->nranks > 1 && g->comm)
       LPA_TRY(exchange_rccl(g, Lc, Ln, g->since_reset < kDenseSupersteps));
     if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
-    LPA_TRY(launch_refresh(g, Lc, Ln));
+    LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally));
     if (tt) {
       LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));
       LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
