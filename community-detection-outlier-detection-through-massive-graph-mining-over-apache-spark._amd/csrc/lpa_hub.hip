@@ -526,10 +526,22 @@ __device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64
       const int i = b0 + r * 256 + threadIdx.x;
       wv[r] = i < n ? wd[i] : 0ull;
     }
+    // batched inserts, 8 words per lane in flight (bounded probing: a bucket's
+    // table load is not guaranteed by construction)
+    static_assert(R % 8 == 0, "insert groups of 8");
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (b0 + r * 256 >= n) break;  // uniform over the block
-      insert_word(wv[r], wv[r] != 0ull && keep(~(u32)wv[r]), tab, lst, lcount, kLg, lane, err);
+    for (int r0 = 0; r0 < R; r0 += 8) {
+      if (b0 + r0 * 256 >= n) break;  // uniform over the block
+      u64 grp[8];
+      u32 m = 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        grp[k] = wv[r0 + k];
+        if (grp[k] != 0ull && keep(~(u32)grp[k])) m |= 1u << k;
+      }
+      int sl[8];
+      insert_words<8, true>(tab, 32 - kLg, (1u << kLg) - 1u, grp, m, sl, err);
+      list_append_n<8>(lst, lcount, sl, lane);
     }
   }
   __syncthreads();
