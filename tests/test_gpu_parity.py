@@ -140,6 +140,21 @@ def test_rmat_bit_exact(gfa, oracle, scale):
         assert np.array_equal(got[t], hist[t]), f"R-MAT {scale} superstep {t + 1}"
 
 
+def test_c2_sbm_full_size(gfa, oracle):
+    """Config C2: planted partition, 1 M vertices / 20 M edges /
+    100 blocks, maxIter 10: bit-exact vs the oracle, and the communities recover the
+    planted blocks (NMI vs ground truth; oracle value at seed 20261015: 0.916)."""
+    from sklearn.metrics import normalized_mutual_info_score as nmi
+    V, B, m = 1_000_000, 100, 20_000_000
+    s, d = gfa.gen_sbm(V, B, m)
+    with gfa.Graph(s, d, V) as g:
+        lab = g.run(10)
+    ref = oracle.lpa(V, s.cpu().numpy(), d.cpu().numpy(), 10)
+    assert np.array_equal(lab, ref)
+    truth = np.minimum(np.arange(V) // (V // B), B - 1)
+    assert nmi(truth, lab) > 0.9
+
+
 def test_schedules_identical(gfa):
     """The concurrent four-stream schedule (forked hub combine in the label-dense
     supersteps) and the serialized profiling schedule give identical labels."""
