@@ -187,6 +187,7 @@ int init_labels(lpa_graph* g) {
   LPA_HIP(hipGetLastError());
   g->cur = 0;
   g->since_reset = 0;
+  g->prev_delta_ok = false;  // the exchange's delta chain restarts from L0
   return rebuild_arc_labels(g);
 }
 

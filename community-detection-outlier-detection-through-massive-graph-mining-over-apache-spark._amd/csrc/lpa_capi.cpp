@@ -232,6 +232,7 @@ int lpa_exchange_put(lpa_graph* g, const int32_t* full_in) {
   LPA_HIP(hipSetDevice(g->device));
   LPA_HIP(hipMemcpyAsync(g->lab[g->cur], full_in, sizeof(int32_t) * g->vpad, hipMemcpyHostToDevice,
                          g->stream));
+  g->prev_delta_ok = false;
   LPA_TRY(rebuild_arc_labels(g));
   LPA_HIP(hipStreamSynchronize(g->stream));
   return LPA_OK;
@@ -274,12 +275,19 @@ int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t*
     }
   LPA_HIP(hipSetDevice(g->device));
   hipStream_t s = g->stream;
+  // the receive buffer lays entries out as [nranks][cap] like the RCCL allgather
   if (cap > 0)
-    LPA_HIP(hipMemcpyAsync(g->drecv, entries, sizeof(uint64_t) * cap * g->nranks,
+    LPA_HIP(hipMemcpyAsync(exchange_recv_buf(g), entries, sizeof(uint64_t) * cap * g->nranks,
                            hipMemcpyHostToDevice, s));
-  LPA_HIP(hipMemcpyAsync(g->dcount + 1, counts, sizeof(int64_t) * g->nranks, hipMemcpyHostToDevice, s));
-  LPA_TRY(exchange_apply(g, g->lab[g->cur ^ 1], g->lab[g->cur], g->dcount + 1, cap));
-  LPA_TRY(rebuild_arc_labels(g));
+  LPA_HIP(hipMemcpyAsync(exchange_recv_counts(g), counts, sizeof(int64_t) * g->nranks,
+                         hipMemcpyHostToDevice, s));
+  // the refresh's counters of this parity (a full put between two deltas runs no
+  // scatter, which would otherwise have zeroed them)
+  LPA_HIP(hipMemsetAsync(g->counters + 4 * g->par, 0, sizeof(unsigned long long) * 2, s));
+  const int32_t* Lc = g->lab[g->cur ^ 1];
+  int32_t* Ln = g->lab[g->cur];
+  LPA_TRY(exchange_finish_delta(g, Lc, Ln, cap));
+  LPA_TRY(launch_refresh_ext(g, Lc, Ln, true));
   LPA_HIP(hipStreamSynchronize(s));
   return LPA_OK;
 }

@@ -6,13 +6,20 @@
 //          change anyway.
 //   delta  each rank compacts the (slot, label) pairs of its CHANGED owned
 //          vertices; the per-rank counts are allgathered and read on the host,
-//          then ncclAllGather moves max-count entries per rank (8 B each).  Every
-//          rank copies the other ranks' slices of the current labels into the
-//          next-label buffer and applies the gathered changes.  Converged
-//          supersteps change ~0.3 % of the vertices (R-MAT-24, superstep 4+), so
-//          the exchange shrinks by ~2 orders of magnitude.  Chosen when the
-//          largest delta is < 1/4 of a slice (its bytes < 1/2 of the full slice).
+//          then ncclAllGather moves max-count entries per rank (8 B each).
+//          Converged supersteps change ~0.3 % of the vertices (R-MAT-24,
+//          superstep 4+), so the exchange shrinks by ~2 orders of magnitude.
+//          Chosen when the largest delta is <= slice / 4 (its bytes <= 1/2 of the
+//          full slice).
 // Both give the identical full label vector, so the mode never affects labels.
+//
+// Completing the next-label buffer Ln after a delta exchange.  Ln (the ping-pong
+// partner of the current vector Lc = L_t) still holds L_{t-1} outside the own
+// slice.  If the previous superstep also exchanged deltas (E_t: L_{t-1} -> L_t),
+// applying E_t and then the new E_{t+1} gives L_{t+1} without touching the rest of
+// the vector; otherwise the other slices are first copied from Lc.  The gathered
+// E_{t+1} is also the list of changed vertices, so the al[] refresh takes its
+// position chunks from it instead of diffing the whole vector.
 #include "lpa_internal.h"
 
 namespace lpa {
@@ -64,17 +71,61 @@ __global__ void k_copy_other(const int4* __restrict__ Lc, int4* __restrict__ Ln,
     if (q < own4_begin || q >= own4_end) Ln[q] = Lc[q];
 }
 
-// apply the gathered changes: rank r's entries are drecv[r * cap, r * cap + counts[r])
+// apply gathered changes (rank r's entries: drecv[r * cap, r * cap + counts[r])),
+// except those of rank `skip` (its slice of Ln is the tally output already)
 __global__ void k_delta_apply(const u64* __restrict__ drecv, const unsigned long long* __restrict__ counts,
-                              int64_t cap, int32_t P, int64_t slice, int32_t* __restrict__ Ln) {
+                              int64_t cap, int32_t P, int32_t skip, int64_t slice,
+                              int32_t* __restrict__ Ln) {
   const int64_t tot = cap * P;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot;
        k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = k / cap, j = k - r * cap;
-    if (j < (int64_t)counts[r]) {
+    if (r != skip && j < (int64_t)counts[r]) {
       const u64 e = drecv[k];
       Ln[r * slice + (int64_t)(e >> 32)] = (int32_t)(uint32_t)e;
     }
+  }
+}
+
+// the gathered changes as al[] position chunks (u << 32 | k) + the dirty-arc count:
+// k_diff's output, from the change list instead of a scan of the whole vector
+__global__ __launch_bounds__(256) void k_delta_chunks(const u64* __restrict__ drecv,
+                                                      const unsigned long long* __restrict__ counts,
+                                                      int64_t cap, int32_t P, int64_t slice,
+                                                      const int64_t* __restrict__ cptr,
+                                                      u64* __restrict__ chunks,
+                                                      unsigned long long* __restrict__ counters) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tot = cap * P;
+  for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = k0 + threadIdx.x;
+    int nch = 0;
+    int64_t u = 0, cnt = 0;
+    if (k < tot) {
+      const int64_t r = k / cap, j = k - r * cap;
+      if (j < (int64_t)counts[r]) {
+        u = r * slice + (int64_t)(drecv[k] >> 32);
+        cnt = cptr[u + 1] - cptr[u];
+        nch = (int)((cnt + kChunkPos - 1) / kChunkPos);
+      }
+    }
+    // wave-aggregated reservation of chunk slots and dirty-arc count
+    int incl = nch;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    const int wtot = __shfl(incl, 63, 64);
+    unsigned long long dirty = (unsigned long long)cnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dirty += __shfl_xor(dirty, off, 64);
+    unsigned long long base = 0;
+    if (lane == 0 && wtot) base = atomicAdd(&counters[0], (unsigned long long)wtot);
+    if (lane == 0 && dirty) atomicAdd(&counters[1], dirty);
+    base = __shfl(base, 0, 64);
+    u64 pos = base + (u64)(incl - nch);
+    for (int c = 0; c < nch; ++c) chunks[pos++] = ((u64)u << 32) | (u64)c;
   }
 }
 
@@ -90,11 +141,13 @@ int exchange_alloc(lpa_graph* g) {
   if (g->nranks <= 1) return LPA_OK;
   g->dcap = g->slice / 4;
   if (g->dcap < 1) g->dcap = 1;
+  const int64_t P = g->nranks;
   LPA_TRY(dev_alloc(g, (void**)&g->dsend, sizeof(u64) * g->slice));
-  LPA_TRY(dev_alloc(g, (void**)&g->drecv, sizeof(u64) * g->dcap * g->nranks));
-  LPA_TRY(dev_alloc(g, (void**)&g->dcount, sizeof(unsigned long long) * (1 + g->nranks)));
-  LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * g->nranks,
-                        hipHostMallocDefault));
+  LPA_TRY(dev_alloc(g, (void**)&g->drecv, sizeof(u64) * g->dcap * P * 2));
+  LPA_TRY(dev_alloc(g, (void**)&g->dcount, sizeof(unsigned long long) * (1 + 2 * P)));
+  LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * P, hipHostMallocDefault));
+  g->dbuf = 0;
+  g->prev_delta_ok = false;
   return LPA_OK;
 }
 
@@ -102,6 +155,9 @@ void exchange_free(lpa_graph* g) {
   if (g->h_dcounts) (void)hipHostFree(g->h_dcounts);
   g->h_dcounts = nullptr;
 }
+
+u64* exchange_recv_buf(lpa_graph* g) { return g->drecv + (int64_t)g->dbuf * g->dcap * g->nranks; }
+unsigned long long* exchange_recv_counts(lpa_graph* g) { return g->dcount + 1 + (int64_t)g->dbuf * g->nranks; }
 
 // compact this rank's changed owned labels (Lc -> Ln) into dsend; count -> dcount[0]
 int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
@@ -113,31 +169,51 @@ int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
   return LPA_OK;
 }
 
-// Ln := Lc outside the own slice, then the gathered changes (drecv, cap entries per
-// rank, counts on the device)
-int exchange_apply(lpa_graph* g, const int32_t* Lc, int32_t* Ln, const unsigned long long* counts,
-                   int64_t cap) {
+// Ln := L_{t+1} from the gathered changes in the current receive buffer (cap entries
+// per rank) -- see the header; also queues the al[] position chunks of the changes
+// (counters of this superstep's parity).  Flips the receive buffer.
+int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap) {
   hipStream_t s = g->stream;
+  const int P = g->nranks;
   const int64_t n4 = g->vpad / 4;
-  hipLaunchKernelGGL(k_copy_other, dim3(grid_of(n4, 8192)), dim3(256), 0, s, (const int4*)Lc,
-                     (int4*)Ln, n4, g->own_begin / 4, (g->own_begin + g->slice) / 4);
-  LPA_HIP(hipGetLastError());
-  if (cap > 0) {
-    hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(cap * g->nranks, 8192)), dim3(256), 0, s,
-                       g->drecv, counts, cap, g->nranks, g->slice, Ln);
+  if (g->prev_delta_ok) {
+    const int pb = g->dbuf ^ 1;
+    if (g->prev_cap > 0) {
+      hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(g->prev_cap * P, 8192)), dim3(256), 0, s,
+                         g->drecv + (int64_t)pb * g->dcap * P, g->dcount + 1 + (int64_t)pb * P,
+                         g->prev_cap, P, g->rank, g->slice, Ln);
+      LPA_HIP(hipGetLastError());
+    }
+  } else {
+    hipLaunchKernelGGL(k_copy_other, dim3(grid_of(n4, 8192)), dim3(256), 0, s, (const int4*)Lc,
+                       (int4*)Ln, n4, g->own_begin / 4, (g->own_begin + g->slice) / 4);
     LPA_HIP(hipGetLastError());
   }
+  if (cap > 0) {
+    hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(cap * P, 8192)), dim3(256), 0, s,
+                       exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->rank, g->slice, Ln);
+    LPA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_delta_chunks, dim3(grid_of(cap * P, 4096)), dim3(256), 0, s,
+                       exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->slice, g->cptr,
+                       g->chunks, g->counters + 4 * g->par);
+    LPA_HIP(hipGetLastError());
+  }
+  g->prev_cap = cap;
+  g->prev_delta_ok = true;
+  g->dbuf ^= 1;
   return LPA_OK;
 }
 
 // In-library RCCL exchange of one superstep (P > 1, comm set): Lown = Ln + own_begin
 // holds the new owned labels; on return Ln holds the full new label vector.
-int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense) {
+// *changes_listed: the refresh's position chunks were queued from the delta.
+int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed) {
   hipStream_t s = g->stream;
   int32_t* Lown = Ln + g->own_begin;
+  *changes_listed = false;
   if (!dense) {
     LPA_TRY(exchange_compact(g, Lc, Ln));
-    unsigned long long* counts = g->dcount + 1;
+    unsigned long long* counts = exchange_recv_counts(g);
     ncclResult_t r = ncclAllGather(g->dcount, counts, 1, ncclUint64, g->comm, s);
     if (r != ncclSuccess) {
       set_error("ncclAllGather (delta counts): %s", ncclGetErrorString(r));
@@ -151,14 +227,15 @@ int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense) {
       if ((int64_t)g->h_dcounts[k] > cap) cap = (int64_t)g->h_dcounts[k];
     if (cap <= g->dcap) {
       if (cap > 0) {
-        r = ncclAllGather(g->dsend, g->drecv, (size_t)cap, ncclUint64, g->comm, s);
+        r = ncclAllGather(g->dsend, exchange_recv_buf(g), (size_t)cap, ncclUint64, g->comm, s);
         if (r != ncclSuccess) {
           set_error("ncclAllGather (delta): %s", ncclGetErrorString(r));
           return LPA_ERCCL;
         }
       }
       g->last_exchange_delta = cap;
-      return exchange_apply(g, Lc, Ln, counts, cap);
+      *changes_listed = true;
+      return exchange_finish_delta(g, Lc, Ln, cap);
     }
   }
   ncclResult_t r = ncclAllGather(Lown, Ln, (size_t)g->slice, ncclInt32, g->comm, s);
@@ -167,6 +244,7 @@ int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense) {
     return LPA_ERCCL;
   }
   g->last_exchange_delta = -1;
+  g->prev_delta_ok = false;
   return LPA_OK;
 }
 

@@ -155,11 +155,15 @@ struct lpa_graph {
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
   lpa::u64* dsend = nullptr;                 // [slice] this rank's (slot << 32 | label)
-  lpa::u64* drecv = nullptr;                 // [nranks * dcap] gathered deltas
-  unsigned long long* dcount = nullptr;      // [1 + nranks] own count, then every rank's
+  lpa::u64* drecv = nullptr;                 // [2][nranks * dcap] gathered deltas
+  unsigned long long* dcount = nullptr;      // [1 + 2 nranks] own count, then every rank's (x2)
   unsigned long long* h_dcounts = nullptr;   // [nranks] pinned host copy
   int64_t dcap = 0;                          // delta entries per rank (slice / 4)
   int64_t last_exchange_delta = -1;          // entries per rank of the last exchange (-1 full)
+  int dbuf = 0;                              // receive buffer of the next delta (ping-pong)
+  bool prev_delta_ok = false;                // the other receive buffer holds the previous
+                                             //   superstep's delta (L_{t-1} -> L_t)
+  int64_t prev_cap = 0;                      // its entries per rank
 
   // original edge list kept for the outlier stage (device, dense ids)
   int32_t* e_src = nullptr;
@@ -202,9 +206,11 @@ int gather_labels(lpa_graph* g, int32_t* out_dense_dev);
 int exchange_alloc(lpa_graph* g);
 void exchange_free(lpa_graph* g);
 int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln);
-int exchange_apply(lpa_graph* g, const int32_t* Lc, int32_t* Ln, const unsigned long long* counts,
-                   int64_t cap);
-int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense);
+lpa::u64* exchange_recv_buf(lpa_graph* g);
+unsigned long long* exchange_recv_counts(lpa_graph* g);
+int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap);
+int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed);
+int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done);
 
 // outlier (lpa_outlier.hip)
 int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,

@@ -1084,6 +1084,10 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
 
 }  // namespace
 
+int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done) {
+  return launch_refresh(g, Lc, Ln, diff_done);
+}
+
 int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
   hipStream_t s = g->stream;
   const bool timed = st != nullptr;
@@ -1109,10 +1113,14 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     const bool diff_in_tally = g->nranks == 1 && !g->serial;
     LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
     if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
+    bool changes_listed = false;
     if (g->nranks > 1 && g->comm)
-      LPA_TRY(exchange_rccl(g, Lc, Ln, g->since_reset < kDenseSupersteps));
+      LPA_TRY(exchange_rccl(g, Lc, Ln, g->since_reset < kDenseSupersteps, &changes_listed));
     if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
-    LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally));
+    // P > 1 without a communicator: the caller completes the superstep with
+    // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
+    // (changes + refresh); a refresh here would see a partial vector
+    if (g->nranks == 1 || g->comm) LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed));
     if (tt) {
       LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));
       LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));

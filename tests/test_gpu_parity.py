@@ -226,7 +226,9 @@ def test_virtual_partitions_delta_exchange(gfa, oracle, P):
                 modes.append("full")
             for g in ranks:
                 assert np.array_equal(g.labels(), hist[t]), f"P={P} superstep {t + 1} ({modes[-1]})"
-        assert "delta" in modes and modes[0] == "full", modes
+        # consecutive deltas exercise the double application (previous + new change
+        # list) that replaces the copy of the other slices
+        assert modes[0] == "full" and any(a == b == "delta" for a, b in zip(modes, modes[1:])), modes
     finally:
         for g in ranks:
             g.close()
