@@ -864,17 +864,31 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
 // gather served by the block's LDS copy is one L2 request fewer.  One 1024-thread
 // block per CU, 128 KB of LDS.
 constexpr int kHotLabels = 32768;
-template <bool kIfWanted>
+// kRanked (P > 1, power-of-two slices and rank count): the hottest vertices of rank
+// r's slice are its first slots (degree rank k lives at slot (k mod P) S + k / P),
+// so the global top kHotLabels are the first H = kHotLabels / P slots of every
+// slice: slot c is hot iff (c mod S) < H, at LDS index (c / S) H + c mod S.
+template <bool kIfWanted, bool kRanked>
 __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long long* __restrict__ counters,
                                                          int64_t thr, const int32_t* __restrict__ col,
                                                          int64_t arcs, const int32_t* __restrict__ Ln,
-                                                         int32_t nhot, int32_t* __restrict__ al) {
+                                                         int32_t nhot, int32_t* __restrict__ al,
+                                                         int slice_lg, int hot_lg) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   __shared__ int32_t hot[kHotLabels];
-  for (int i = threadIdx.x; i < nhot; i += 1024) hot[i] = Ln[i];
+  for (int i = threadIdx.x; i < nhot; i += 1024)
+    hot[i] = kRanked ? Ln[((int64_t)(i >> hot_lg) << slice_lg) + (i & ((1 << hot_lg) - 1))] : Ln[i];
   __syncthreads();
   const u32 nh = (u32)nhot;
-  auto lab = [&](int c) -> int32_t { return (u32)c < nh ? hot[c] : Ln[c]; };
+  const u32 smask = kRanked ? (1u << slice_lg) - 1u : 0u, hcap = 1u << hot_lg;
+  auto lab = [&](int c) -> int32_t {
+    if constexpr (kRanked) {
+      const u32 j = (u32)c & smask;
+      return j < hcap ? hot[(((u32)c >> slice_lg) << hot_lg) + j] : Ln[c];
+    } else {
+      return (u32)c < nh ? hot[c] : Ln[c];
+    }
+  };
   const int64_t n4 = arcs >> 2;
   const v4i* __restrict__ c4 = reinterpret_cast<const v4i*>(col);
   v4i* __restrict__ a4 = reinterpret_cast<v4i*>(al);
@@ -1026,16 +1040,28 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
 int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
                    const unsigned long long* ctr) {
   hipStream_t s = g->stream;
-  if (g->nranks == 1 && g->rebuild_hot) {
+  const auto pow2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
+  const bool ranked = g->nranks > 1 && pow2(g->nranks) && pow2(g->slice) && g->nranks <= kHotLabels &&
+                      g->slice >= kHotLabels / g->nranks;
+  if (g->rebuild_hot && (g->nranks == 1 || ranked)) {
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
-    const int32_t nhot = (int32_t)(g->vpad < kHotLabels ? g->vpad : kHotLabels);
-    if (if_wanted)
-      hipLaunchKernelGGL(k_al_rebuild_hot<true>, dim3(dev_cus), dim3(1024), 0, s, ctr, thr,
-                         g->col, g->arcs, L, nhot, g->al);
-    else
-      hipLaunchKernelGGL(k_al_rebuild_hot<false>, dim3(dev_cus), dim3(1024), 0, s, ctr, thr,
-                         g->col, g->arcs, L, nhot, g->al);
+    int slice_lg = 0, hot_lg = 0;
+    int32_t nhot = (int32_t)(g->vpad < kHotLabels ? g->vpad : kHotLabels);
+    if (ranked) {
+      while ((int64_t(1) << slice_lg) < g->slice) ++slice_lg;
+      while ((int64_t(1) << hot_lg) < kHotLabels / g->nranks) ++hot_lg;
+      nhot = (int32_t)(g->nranks << hot_lg);
+    }
+#define LPA_HOT_LAUNCH(W, R)                                                                     \
+  hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
+                     g->arcs, L, nhot, g->al, slice_lg, hot_lg)
+    if (if_wanted) {
+      if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
+    } else {
+      if (ranked) LPA_HOT_LAUNCH(false, true); else LPA_HOT_LAUNCH(false, false);
+    }
+#undef LPA_HOT_LAUNCH
   } else {
     const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
     if (if_wanted)

@@ -199,6 +199,29 @@ def test_virtual_partitions_bit_exact(gfa, oracle, P):
 
 
 @pytest.mark.parametrize("P", [2, 4])
+def test_virtual_partitions_rmat_power_of_two(gfa, oracle, P):
+    """Power-of-two slices: the al[] rebuild serves the hottest vertices of every
+    slice from LDS (rank-strided hot set); bit-exact per superstep (R-MAT scale 16)."""
+    s, d = gfa.gen_rmat(16, 16, seed=2)
+    V = 1 << 16
+    s, d = s.cpu().numpy(), d.cpu().numpy()
+    ranks = [gfa.Graph(s, d, V, rank=r, nranks=P) for r in range(P)]
+    try:
+        assert ranks[0].info()["slice"] == V // P
+        _, hist, _ = oracle.lpa(V, s, d, 5, per_iter=True)
+        for t in range(5):
+            for g in ranks:
+                g.step(1)
+            full = np.concatenate([g.exchange_get() for g in ranks])
+            for g in ranks:
+                g.exchange_put(full)
+            assert np.array_equal(ranks[-1].labels(), hist[t]), f"P={P} superstep {t + 1}"
+    finally:
+        for g in ranks:
+            g.close()
+
+
+@pytest.mark.parametrize("P", [2, 4])
 def test_virtual_partitions_delta_exchange(gfa, oracle, P):
     """The changed-label delta exchange (the converged-superstep protocol of the
     in-library RCCL exchange, lpa_exchange.hip) with P virtual ranks: full
