@@ -47,6 +47,9 @@ int gen_sbm(int32_t V, int32_t blocks, int64_t m, uint32_t p_in_q32, uint64_t se
 
 void destroy(lpa_graph* g) {
   if (g) exchange_free(g);
+  if (g)
+    for (auto& ge : g->gexec)
+      if (ge) (void)hipGraphExecDestroy(ge);
   if (!g) return;
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
@@ -125,6 +128,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_REBUILD_FRAC")) g->rebuild_frac = atof(f);
   if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
   if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
+  if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {

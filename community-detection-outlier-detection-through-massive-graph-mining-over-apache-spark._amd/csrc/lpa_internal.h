@@ -150,6 +150,8 @@ struct lpa_graph {
   lpa::u64* chunks = nullptr;   // changed-vertex position chunks: (u << 32 | chunk index)
   double rebuild_frac = lpa::kRebuildFrac;  // LPA_REBUILD_FRAC overrides (tuning experiments)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
+  int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
+  hipGraphExec_t gexec[4] = {};             // captured converged superstep per (cur, par)
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 
