@@ -109,6 +109,8 @@ SIGNATURES = {
                                     _vp, _vp, ctypes.c_int32, _vp]),
     "lpa_gen_sbm": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
                                    ctypes.c_uint64, _vp, _vp, ctypes.c_int32, _vp]),
+    "lpa_gen_chunglu": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_uint64, _vp, _vp, ctypes.c_int32, _vp]),
 }
 
 _lib = None

@@ -44,6 +44,8 @@ int gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t do_scramble, int32
              int32_t* d_dst, hipStream_t s);
 int gen_sbm(int32_t V, int32_t blocks, int64_t m, uint32_t p_in_q32, uint64_t seed, int32_t* d_src,
             int32_t* d_dst, hipStream_t s);
+int gen_chunglu(int32_t V, int64_t m, double gamma, double max_deg, uint64_t seed, int32_t* d_src,
+                int32_t* d_dst, hipStream_t s);
 
 void destroy(lpa_graph* g) {
   if (g) exchange_free(g);
@@ -461,6 +463,20 @@ int lpa_gen_sbm(int32_t V, int32_t blocks, int64_t m, uint32_t p_in_q32, uint64_
   }
   hipStream_t s = (hipStream_t)hip_stream;
   LPA_TRY(gen_sbm(V, blocks, m, p_in_q32, seed, d_src, d_dst, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  return LPA_OK;
+}
+
+int lpa_gen_chunglu(int32_t V, int64_t m, double gamma, double max_deg, uint64_t seed,
+                    int32_t* d_src, int32_t* d_dst, int32_t device, void* hip_stream) {
+  LPA_TRY(check_device(device));
+  LPA_HIP(hipSetDevice(device));
+  if (m > 0 && (!d_src || !d_dst)) {
+    set_error("d_src/d_dst must be non-null");
+    return LPA_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)hip_stream;
+  LPA_TRY(gen_chunglu(V, m, gamma, max_deg, seed, d_src, d_dst, s));
   LPA_HIP(hipStreamSynchronize(s));
   return LPA_OK;
 }

@@ -1,7 +1,11 @@
-// Synthetic inputs generated in HBM: R-MAT (configs C3/C4)
-// and the planted-partition SBM (C2).  Every draw is a pure function of
+// Synthetic inputs generated in HBM: R-MAT (configs C3/C4),
+// the planted-partition SBM (C2) and the Chung-Lu power-law graph (C5).  Every draw is a pure function of
 // (seed, edge index, slot) through a splitmix64 counter RNG, so the device
 // output is bit-identical to the CPU restatement in oracle/lpa_oracle.c.
+#include <math.h>
+
+#include <vector>
+
 #include "lpa_internal.h"
 
 namespace lpa {
@@ -82,6 +86,31 @@ __global__ void k_sbm(u32 V, u32 blocks, int64_t m, u32 p_in, u64 seed_mixed,
   }
 }
 
+// Chung-Lu (C5): both endpoints of an edge drawn independently with P(i) ~ w_i =
+// (i + i0)^(-1/(gamma-1)) over weight ranks i, then mapped to vertex ids by the
+// seeded affine permutation id = (mul i + add) mod V.  The sampler is integer-only
+// on the device: a 62-bit uniform draw, binary search of the quantized cumulative
+// weight table Q[0..V] (Q[0] = 0, Q[V] = 2^62, built on the host).
+__global__ void k_chunglu(const u64* __restrict__ Q, u32 V, int64_t m, u64 seed_mixed, u64 mul,
+                          u64 add, int32_t* __restrict__ src, int32_t* __restrict__ dst) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    u32 id[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const u64 r = sm64(seed_mixed + (u64)e * 32ull + (u64)k) >> 2;
+      u32 lo = 0, hi = V;  // Q[lo] <= r < Q[hi]
+      while (hi - lo > 1) {
+        const u32 mid = lo + ((hi - lo) >> 1);
+        if (Q[mid] <= r) lo = mid; else hi = mid;
+      }
+      id[k] = (u32)((mul * (u64)lo + add) % (u64)V);
+    }
+    src[e] = (int32_t)id[0];
+    dst[e] = (int32_t)id[1];
+  }
+}
+
 inline unsigned gen_grid(int64_t m) {
   int64_t b = (m + 255) / 256;
   if (b < 1) b = 1;
@@ -104,6 +133,74 @@ int gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t do_scramble, int32
   hipLaunchKernelGGL(k_rmat, dim3(gen_grid(m)), dim3(256), 0, s, scale, m, sm64_h(seed),
                      do_scramble, m1, m2, c1, d_src, d_dst);
   LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
+
+// Host half of the Chung-Lu sampler (restated in oracle/lpa_oracle.c: the same
+// double arithmetic in the same order, so both build the identical table).
+// i0 is set by bisection so that the expected maximum degree 2 m w_0 / W equals
+// max_deg, with W from the integral approximation; the table itself uses the
+// exact sequential sum.
+void chunglu_table(int32_t V, int64_t m, double gamma, double max_deg, uint64_t seed, u64* Q,
+                   u64* mul_out, u64* add_out) {
+  const double a = 1.0 / (gamma - 1.0);
+  double i0 = 1.0;
+  if (max_deg > 0.0) {
+    auto expmax = [&](double x) {
+      const double S = (pow((double)V + x, 1.0 - a) - pow(x, 1.0 - a)) / (1.0 - a) + 0.5 * pow(x, -a);
+      return 2.0 * (double)m * pow(x, -a) / S;
+    };
+    double lo = log(1e-3), hi = log((double)V);
+    for (int it = 0; it < 200; ++it) {
+      const double mid = 0.5 * (lo + hi);
+      if (expmax(exp(mid)) > max_deg) lo = mid; else hi = mid;
+    }
+    i0 = exp(0.5 * (lo + hi));
+  }
+  double W = 0.0;
+  for (int32_t i = 0; i < V; ++i) W += pow((double)i + i0, -a);
+  const double two62 = 4611686018427387904.0;
+  double c = 0.0;
+  for (int32_t i = 0; i < V; ++i) {
+    Q[i] = (u64)(c / W * two62);
+    c += pow((double)i + i0, -a);
+  }
+  Q[V] = 1ull << 62;
+  u64 mul = V > 1 ? sm64_h(seed ^ 0xC0FFEEull) % (u64)V : 1ull;
+  auto gcd = [](u64 x, u64 y) { while (y) { u64 t = x % y; x = y; y = t; } return x; };
+  if (mul == 0) mul = 1;
+  while (V > 1 && gcd(mul, (u64)V) != 1) mul = mul + 1 == (u64)V ? 1 : mul + 1;
+  *mul_out = mul;
+  *add_out = V > 1 ? sm64_h(seed ^ 0xADDull) % (u64)V : 0ull;
+}
+
+int gen_chunglu(int32_t V, int64_t m, double gamma, double max_deg, uint64_t seed, int32_t* d_src,
+                int32_t* d_dst, hipStream_t s) {
+  if (V < 1 || m < 0 || !(gamma > 1.0 && gamma < 10.0)) {
+    set_error("gen_chunglu: need V >= 1, m >= 0 and 1 < gamma < 10");
+    return LPA_EINVAL;
+  }
+  if (m == 0) return LPA_OK;
+  std::vector<u64> Q;
+  try {
+    Q.resize((size_t)V + 1);
+  } catch (...) {
+    set_error("gen_chunglu: host table allocation failed");
+    return LPA_ENOMEM;
+  }
+  u64 mul = 1, add = 0;
+  chunglu_table(V, m, gamma, max_deg, seed, Q.data(), &mul, &add);
+  u64* dQ = nullptr;
+  LPA_HIP(hipMalloc(&dQ, Q.size() * sizeof(u64)));
+  hipError_t e = hipMemcpyAsync(dQ, Q.data(), Q.size() * sizeof(u64), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_chunglu, dim3(gen_grid(m)), dim3(256), 0, s, dQ, (u32)V, m, sm64_h(seed),
+                       mul, add, d_src, d_dst);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(dQ);
+  LPA_HIP(e);
   return LPA_OK;
 }
 

@@ -226,3 +226,17 @@ def gen_sbm(num_vertices: int, blocks: int, m: int, seed: int = 20261015,
     _lib.check(_lib.load().lpa_gen_sbm(num_vertices, blocks, m, p_in_q32, seed, src.data_ptr(),
                                        dst.data_ptr(), device, None))
     return src, dst
+
+
+def gen_chunglu(num_vertices: int, m: int, gamma: float = 2.1, max_deg: float = 0.0, seed: int = 7,
+                device: int = 0):
+    """Chung-Lu power-law edge list generated in HBM (config C5: heavy hubs)."""
+    import torch
+
+    dev = torch.device("cuda", device)
+    src = torch.empty(m, dtype=torch.int32, device=dev)
+    dst = torch.empty(m, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    _lib.check(_lib.load().lpa_gen_chunglu(num_vertices, m, gamma, max_deg, seed, src.data_ptr(),
+                                           dst.data_ptr(), device, None))
+    return src, dst

@@ -187,6 +187,12 @@ int lpa_gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t scramble, int3
 /* planted-partition SBM: V vertices in `blocks` equal blocks, p_in as a Q32 fraction. */
 int lpa_gen_sbm(int32_t V, int32_t blocks, int64_t m, uint32_t p_in_q32, uint64_t seed,
                 int32_t* d_src, int32_t* d_dst, int32_t device, void* hip_stream);
+/* Chung-Lu power-law (config C5: "Twitter-shaped", heavy hubs): both endpoints drawn
+ * with P(i) ~ (i + i0)^(-1/(gamma-1)), i0 chosen so the expected maximum degree is
+ * max_deg (<= 0: i0 = 1), ranks mapped to ids by a seeded affine permutation mod V;
+ * duplicates and self-loops kept.  Builds a (V+1) x 8 B weight table on the host. */
+int lpa_gen_chunglu(int32_t V, int64_t m, double gamma, double max_deg, uint64_t seed,
+                    int32_t* d_src, int32_t* d_dst, int32_t device, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,7 @@
  */
 #include <stdint.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -84,6 +85,60 @@ void oracle_gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t scramble_i
     src[e] = (int32_t)u;
     dst[e] = (int32_t)v;
   }
+}
+
+/* Chung-Lu power-law (config C5): P(i) ~ (i + i0)^(-1/(gamma-1))
+ * over weight ranks, i0 by bisection so that the expected maximum degree is max_deg,
+ * a quantized cumulative table Q[0..V] (Q[V] = 2^62), one 62-bit draw per endpoint,
+ * rank -> id by the seeded affine permutation (mul * i + add) mod V.  Restates the
+ * generator of csrc/lpa_gen.hip with the same double arithmetic in the same order. */
+static uint64_t gcd_u64(uint64_t x, uint64_t y) {
+  while (y) { uint64_t t = x % y; x = y; y = t; }
+  return x;
+}
+static double cl_expmax(double x, int32_t V, int64_t m, double a) {
+  double S = (pow((double)V + x, 1.0 - a) - pow(x, 1.0 - a)) / (1.0 - a) + 0.5 * pow(x, -a);
+  return 2.0 * (double)m * pow(x, -a) / S;
+}
+int oracle_gen_chunglu(int32_t V, int64_t m, double gamma, double max_deg, uint64_t seed,
+                       int32_t* src, int32_t* dst) {
+  double a = 1.0 / (gamma - 1.0), i0 = 1.0;
+  if (max_deg > 0.0) {
+    double lo = log(1e-3), hi = log((double)V);
+    for (int it = 0; it < 200; ++it) {
+      double mid = 0.5 * (lo + hi);
+      if (cl_expmax(exp(mid), V, m, a) > max_deg) lo = mid; else hi = mid;
+    }
+    i0 = exp(0.5 * (lo + hi));
+  }
+  uint64_t* Q = (uint64_t*)malloc(((size_t)V + 1) * sizeof(uint64_t));
+  if (!Q) return -1;
+  double W = 0.0, c = 0.0;
+  for (int32_t i = 0; i < V; ++i) W += pow((double)i + i0, -a);
+  for (int32_t i = 0; i < V; ++i) {
+    Q[i] = (uint64_t)(c / W * 4611686018427387904.0);
+    c += pow((double)i + i0, -a);
+  }
+  Q[V] = 1ull << 62;
+  uint64_t mul = V > 1 ? sm64(seed ^ 0xC0FFEEull) % (uint64_t)V : 1ull;
+  if (mul == 0) mul = 1;
+  while (V > 1 && gcd_u64(mul, (uint64_t)V) != 1) mul = (mul + 1 == (uint64_t)V) ? 1 : mul + 1;
+  uint64_t add = V > 1 ? sm64(seed ^ 0xADDull) % (uint64_t)V : 0ull;
+#pragma omp parallel for schedule(static)
+  for (int64_t e = 0; e < m; ++e) {
+    for (int k = 0; k < 2; ++k) {
+      uint64_t r = draw(seed, (uint64_t)e, (uint32_t)k) >> 2;
+      uint32_t lo = 0, hi = (uint32_t)V;
+      while (hi - lo > 1) {
+        uint32_t mid = lo + ((hi - lo) >> 1);
+        if (Q[mid] <= r) lo = mid; else hi = mid;
+      }
+      int32_t id = (int32_t)((mul * (uint64_t)lo + add) % (uint64_t)V);
+      if (k == 0) src[e] = id; else dst[e] = id;
+    }
+  }
+  free(Q);
+  return 0;
 }
 
 /* planted-partition SBM: u uniform; with p_in v uniform inside u's block,

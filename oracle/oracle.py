@@ -71,6 +71,9 @@ def _load():
     lib.oracle_gen_sbm.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                    ctypes.c_uint32, ctypes.c_uint64, i32p, i32p]
     lib.oracle_gen_sbm.restype = None
+    lib.oracle_gen_chunglu.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    lib.oracle_gen_chunglu.restype = ctypes.c_int
     lib.oracle_num_threads.argtypes = []
     lib.oracle_num_threads.restype = ctypes.c_int
     _lib = lib
@@ -189,6 +192,16 @@ def gen_sbm(V: int, blocks: int, m: int, seed: int = 20261015, p_in_q32: int = P
     s = np.empty(m, dtype=np.int32)
     d = np.empty(m, dtype=np.int32)
     lib.oracle_gen_sbm(V, blocks, m, p_in_q32, seed, _p(s, ctypes.c_int32), _p(d, ctypes.c_int32))
+    return s, d
+
+
+def gen_chunglu(V: int, m: int, gamma: float = 2.1, max_deg: float = 0.0, seed: int = 7):
+    """CPU restatement of the GPU Chung-Lu generator (config C5; bit-identical)."""
+    lib = _load()
+    s = np.empty(m, dtype=np.int32)
+    d = np.empty(m, dtype=np.int32)
+    if lib.oracle_gen_chunglu(V, m, gamma, max_deg, seed, s.ctypes.data, d.ctypes.data) != 0:
+        raise MemoryError("oracle_gen_chunglu: table allocation failed")
     return s, d
 
 

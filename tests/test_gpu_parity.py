@@ -169,6 +169,27 @@ def test_schedules_identical(gfa):
         assert np.array_equal(conc[t], ser[t]), f"superstep {t + 1}"
 
 
+def test_chunglu_generator_matches_oracle(gfa, oracle):
+    s, d = gfa.gen_chunglu(100_000, 1_000_000, 2.1, 30_000.0, seed=7)
+    cs, cd = oracle.gen_chunglu(100_000, 1_000_000, 2.1, 30_000.0, 7)
+    assert np.array_equal(s.cpu().numpy(), cs) and np.array_equal(d.cpu().numpy(), cd)
+
+
+def test_chunglu_heavy_hub_every_superstep(gfa, oracle):
+    """Config C5's shape scaled down (Chung-Lu exponent 2.1): a hub
+    of ~250 K arcs among 300 K vertices -- the superstep-1 combine sees ~200 K
+    distinct labels in one row (bucket path, sub-bucket passes).  Bit-exact per superstep."""
+    V, m = 300_000, 3_000_000
+    s, d = gfa.gen_chunglu(V, m, 2.1, 250_000.0, seed=7)
+    sn, dn = s.cpu().numpy(), d.cpu().numpy()
+    deg = np.bincount(sn, minlength=V) + np.bincount(dn, minlength=V)
+    assert deg.max() > 200_000
+    got = _per_step(gfa, V, s, d, 10)
+    _, hist, _ = oracle.lpa(V, sn, dn, 10, per_iter=True)
+    for t in range(10):
+        assert np.array_equal(got[t], hist[t]), f"Chung-Lu superstep {t + 1}"
+
+
 def test_sbm_bit_exact(gfa, oracle):
     s, d = gfa.gen_sbm(20000, 20, 400000)
     with gfa.Graph(s, d, 20000) as g:

@@ -132,3 +132,20 @@ def test_generators_deterministic(oracle):
     s, d = oracle.gen_sbm(1000, 10, 50000)
     same = (s // 100) == (d // 100)
     assert abs(same.mean() - 0.9) < 0.01
+
+
+def test_chunglu_generator(oracle):
+    """Config C5's generator (Chung-Lu, exponent 2.1, seed 7):
+    deterministic, ids in range, the requested expected maximum degree, a heavy tail."""
+    V, m = 200_000, 2_000_000
+    s1, d1 = oracle.gen_chunglu(V, m, 2.1, 20_000.0, 7)
+    s2, d2 = oracle.gen_chunglu(V, m, 2.1, 20_000.0, 7)
+    assert np.array_equal(s1, s2) and np.array_equal(d1, d2)
+    assert s1.min() >= 0 and max(s1.max(), d1.max()) < V
+    s3, _ = oracle.gen_chunglu(V, m, 2.1, 20_000.0, 8)
+    assert not np.array_equal(s1, s3)
+    deg = np.bincount(s1, minlength=V) + np.bincount(d1, minlength=V)
+    assert 0.9 * 20_000 < deg.max() < 1.1 * 20_000
+    top = np.sort(deg)[::-1]
+    # power-law tail: the top 1 % of vertices hold far more than 1 % of the arcs
+    assert top[: V // 100].sum() > 0.2 * deg.sum()
