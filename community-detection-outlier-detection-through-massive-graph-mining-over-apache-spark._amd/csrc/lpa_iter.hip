@@ -889,29 +889,26 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
       return (u32)c < nh ? hot[c] : Ln[c];
     }
   };
-  const int64_t n4 = arcs >> 2;
-  const v4i* __restrict__ c4 = reinterpret_cast<const v4i*>(col);
-  v4i* __restrict__ a4 = reinterpret_cast<v4i*>(al);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; q + stride < n4; q += 2 * stride) {
-    const v4i c0 = __builtin_nontemporal_load(c4 + q);
-    const v4i c1 = __builtin_nontemporal_load(c4 + q + stride);
-    v4i r0, r1;
-    r0.x = lab(c0.x); r0.y = lab(c0.y); r0.z = lab(c0.z); r0.w = lab(c0.w);
-    r1.x = lab(c1.x); r1.y = lab(c1.y); r1.z = lab(c1.z); r1.w = lab(c1.w);
-    __builtin_nontemporal_store(r0, a4 + q);
-    __builtin_nontemporal_store(r1, a4 + q + stride);
-  }
-  if (q < n4) {
-    const v4i c0 = __builtin_nontemporal_load(c4 + q);
-    v4i r0;
-    r0.x = lab(c0.x); r0.y = lab(c0.y); r0.z = lab(c0.z); r0.w = lab(c0.w);
-    __builtin_nontemporal_store(r0, a4 + q);
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (arcs & 3)) {
-    const int64_t i = (n4 << 2) + threadIdx.x;
-    al[i] = Ln[col[i]];
+  // lane-consecutive arcs: one gather instruction covers 64 consecutive arcs of
+  // a row, whose sorted columns often share lines (hub rows) -> fewer L2 requests
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512;
+       base < arcs; base += nw * 512) {
+    int32_t c[8], r[8];
+    if (base + 512 <= arcs) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + base + k * 64 + lane);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = lab(c[k]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
+    } else {
+      for (int k = 0; k < 8; ++k) {
+        const int64_t i = base + k * 64 + lane;
+        if (i < arcs) al[i] = lab(col[i]);
+      }
+    }
   }
 }
 
