@@ -51,6 +51,67 @@ __global__ void k_vertex_keys(const int32_t* __restrict__ deg, int64_t V, int32_
     keys[v] = ((u64)(u32)(maxdeg - deg[v]) << 32) | (u64)v;
 }
 
+// ---- locality order (g->locality): within each degree bin below the hubs, vertices
+// are ordered by (smallest, second smallest) neighbour degree rank, so the
+// low-degree neighbours a hub row shares with the highest-ranked hubs sit in
+// contiguous slots and its label gathers (al[] rebuild) coalesce.  Hubs keep the
+// (degree desc, id) order; the bins stay contiguous slot ranges.
+__device__ __forceinline__ u32 degree_bin(int32_t d) {
+  if (d > 1024) return 0;
+  if (d == 0) return 12;
+  // d in (2^(j-1), 2^j] -> bin 11 - j for j = 0..10 (1 -> g1 = 11, ..., (512, 1024] -> w16 = 1)
+  const int j = d <= 1 ? 0 : 32 - __clz((u32)(d - 1));
+  return (u32)(11 - j);
+}
+
+__global__ void k_rank_of(const u64* __restrict__ keys, int64_t V, int32_t* __restrict__ rank_of) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < V;
+       k += (int64_t)gridDim.x * blockDim.x)
+    rank_of[(u32)keys[k]] = (int32_t)k;
+}
+
+// pass 0: n1[v] = min neighbour rank; pass 1: n2[v] = min neighbour rank > n1[v]
+// (non-hub vertices only: a hub's row is not reordered)
+__global__ void k_min_nbr(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t m,
+                          const int32_t* __restrict__ deg, const int32_t* __restrict__ rank_of,
+                          int32_t* __restrict__ n1, int32_t* __restrict__ n2, int pass) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t a = src[e], b = dst[e];
+    const int32_t ra = rank_of[a], rb = rank_of[b];
+    if (deg[a] <= 1024) {
+      if (pass == 0) atomicMin(&n1[a], rb);
+      else if (rb > n1[a]) atomicMin(&n2[a], rb);
+    }
+    if (deg[b] <= 1024) {
+      if (pass == 0) atomicMin(&n1[b], ra);
+      else if (ra > n1[b]) atomicMin(&n2[b], ra);
+    }
+  }
+}
+
+// stage 0: (n2 << 32 | v); stage 1 (over the stage-0 order): (bin << 28 | n1) << 32 | v,
+// hubs (maxdeg - deg) in place of n1 and n2 = 0.  Two stable radix sorts give
+// (bin, n1 | degree, n2, id).
+__global__ void k_locality_keys(u64* __restrict__ keys, int64_t V, const int32_t* __restrict__ deg,
+                                const int32_t* __restrict__ n1, const int32_t* __restrict__ n2,
+                                int32_t maxdeg, int stage) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < V;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const u32 v = stage == 0 ? (u32)k : (u32)keys[k];
+    const int32_t d = deg[v];
+    const u32 bin = degree_bin(d);
+    const u32 cap = (1u << 28) - 1u;
+    if (stage == 0) {
+      const u32 b2 = bin == 0 ? 0u : min((u32)n2[v], cap);
+      keys[k] = ((u64)b2 << 32) | v;
+    } else {
+      const u32 a = bin == 0 ? (u32)(maxdeg - d) : min((u32)n1[v], cap);
+      keys[k] = ((u64)((bin << 28) | a) << 32) | v;
+    }
+  }
+}
+
 __global__ void k_vertex_order(const u64* __restrict__ keys, int64_t V, int32_t P, int64_t S,
                                int32_t* __restrict__ new_of, int32_t* __restrict__ old_of) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < V;
@@ -255,6 +316,27 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(vk, vk + V, V, shifts, ns, s));
+    if (g->locality && m > 0 && V < (1 << 28)) {
+      int32_t *rank_of = nullptr, *n1 = nullptr, *n2 = nullptr;
+      LPA_HIP(hipMalloc((void**)&rank_of, sizeof(int32_t) * 3 * (size_t)V));
+      n1 = rank_of + V;
+      n2 = n1 + V;
+      hipLaunchKernelGGL(k_rank_of, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, rank_of);
+      LPA_HIP(hipMemsetAsync(n1, 0x7F, sizeof(int32_t) * 2 * (size_t)V, s));
+      for (int pass = 0; pass < 2; ++pass)
+        hipLaunchKernelGGL(k_min_nbr, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, g->deg,
+                           rank_of, n1, n2, pass);
+      LPA_HIP(hipGetLastError());
+      const int hi[4] = {32, 40, 48, 56};
+      hipLaunchKernelGGL(k_locality_keys, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, g->deg,
+                         n1, n2, g->max_degree, 0);
+      LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
+      hipLaunchKernelGGL(k_locality_keys, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, g->deg,
+                         n1, n2, g->max_degree, 1);
+      LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
+      LPA_HIP(hipGetLastError());
+      LPA_HIP(hipFree(rank_of));
+    }
     hipLaunchKernelGGL(k_vertex_order, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, P, S,
                        g->new_of, g->old_of);
     LPA_HIP(hipGetLastError());

@@ -130,6 +130,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_REBUILD_FRAC")) g->rebuild_frac = atof(f);
   if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
   if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
+  if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   g->rank = rank;
   g->nranks = nranks;
