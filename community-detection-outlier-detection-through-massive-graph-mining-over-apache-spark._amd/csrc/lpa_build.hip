@@ -70,43 +70,37 @@ __global__ void k_rank_of(const u64* __restrict__ keys, int64_t V, int32_t* __re
     rank_of[(u32)keys[k]] = (int32_t)k;
 }
 
-// pass 0: n1[v] = min neighbour rank; pass 1: n2[v] = min neighbour rank > n1[v]
-// (non-hub vertices only: a hub's row is not reordered)
+// key k of a non-hub vertex: its k-th smallest distinct neighbour rank (pass k reads
+// key k-1 and takes the minimum neighbour rank above it); hubs are not reordered
 __global__ void k_min_nbr(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t m,
                           const int32_t* __restrict__ deg, const int32_t* __restrict__ rank_of,
-                          int32_t* __restrict__ n1, int32_t* __restrict__ n2, int pass) {
+                          const int32_t* __restrict__ nprev, int32_t* __restrict__ ncur) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int32_t a = src[e], b = dst[e];
     const int32_t ra = rank_of[a], rb = rank_of[b];
-    if (deg[a] <= 1024) {
-      if (pass == 0) atomicMin(&n1[a], rb);
-      else if (rb > n1[a]) atomicMin(&n2[a], rb);
-    }
-    if (deg[b] <= 1024) {
-      if (pass == 0) atomicMin(&n1[b], ra);
-      else if (ra > n1[b]) atomicMin(&n2[b], ra);
-    }
+    if (deg[a] <= 1024 && (!nprev || rb > nprev[a])) atomicMin(&ncur[a], rb);
+    if (deg[b] <= 1024 && (!nprev || ra > nprev[b])) atomicMin(&ncur[b], ra);
   }
 }
 
-// stage 0: (n2 << 32 | v); stage 1 (over the stage-0 order): (bin << 28 | n1) << 32 | v,
-// hubs (maxdeg - deg) in place of n1 and n2 = 0.  Two stable radix sorts give
-// (bin, n1 | degree, n2, id).
+// one stable radix stage of the locality order per key, last key first: stage keys
+// (n_k << 32 | v) for k = K-1 .. 1, then ((bin << 28 | n_0) << 32 | v), hubs with
+// (maxdeg - deg) in place of n_0 and 0 for the deeper keys.  The K + 1 stable sorts
+// give (bin, n_0 | degree, n_1, ..., id).
 __global__ void k_locality_keys(u64* __restrict__ keys, int64_t V, const int32_t* __restrict__ deg,
-                                const int32_t* __restrict__ n1, const int32_t* __restrict__ n2,
-                                int32_t maxdeg, int stage) {
+                                const int32_t* __restrict__ nk, int32_t maxdeg, int first, int last) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < V;
        k += (int64_t)gridDim.x * blockDim.x) {
-    const u32 v = stage == 0 ? (u32)k : (u32)keys[k];
+    const u32 v = first ? (u32)k : (u32)keys[k];
     const int32_t d = deg[v];
     const u32 bin = degree_bin(d);
     const u32 cap = (1u << 28) - 1u;
-    if (stage == 0) {
-      const u32 b2 = bin == 0 ? 0u : min((u32)n2[v], cap);
+    if (!last) {
+      const u32 b2 = bin == 0 ? 0u : min((u32)nk[v], cap);
       keys[k] = ((u64)b2 << 32) | v;
     } else {
-      const u32 a = bin == 0 ? (u32)(maxdeg - d) : min((u32)n1[v], cap);
+      const u32 a = bin == 0 ? (u32)(maxdeg - d) : min((u32)nk[v], cap);
       keys[k] = ((u64)((bin << 28) | a) << 32) | v;
     }
   }
@@ -327,24 +321,23 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(vk, vk + V, V, shifts, ns, s));
-    if (g->locality && m > 0 && V < (1 << 28)) {
-      int32_t *rank_of = nullptr, *n1 = nullptr, *n2 = nullptr;
-      LPA_HIP(hipMalloc((void**)&rank_of, sizeof(int32_t) * 3 * (size_t)V));
-      n1 = rank_of + V;
-      n2 = n1 + V;
+    if (g->locality > 0 && m > 0 && V < (1 << 28)) {
+      const int K = g->locality < 4 ? g->locality : 4;  // neighbour keys (LPA_LOCALITY)
+      int32_t* rank_of = nullptr;
+      LPA_HIP(hipMalloc((void**)&rank_of, sizeof(int32_t) * (1 + K) * (size_t)V));
+      int32_t* nk[4] = {rank_of + V, rank_of + 2 * V, rank_of + 3 * V, rank_of + 4 * V};
       hipLaunchKernelGGL(k_rank_of, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, rank_of);
-      LPA_HIP(hipMemsetAsync(n1, 0x7F, sizeof(int32_t) * 2 * (size_t)V, s));
-      for (int pass = 0; pass < 2; ++pass)
+      LPA_HIP(hipMemsetAsync(nk[0], 0x7F, sizeof(int32_t) * K * (size_t)V, s));
+      for (int k = 0; k < K; ++k)
         hipLaunchKernelGGL(k_min_nbr, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, g->deg,
-                           rank_of, n1, n2, pass);
+                           rank_of, k ? nk[k - 1] : nullptr, nk[k]);
       LPA_HIP(hipGetLastError());
       const int hi[4] = {32, 40, 48, 56};
-      hipLaunchKernelGGL(k_locality_keys, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, g->deg,
-                         n1, n2, g->max_degree, 0);
-      LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
-      hipLaunchKernelGGL(k_locality_keys, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, g->deg,
-                         n1, n2, g->max_degree, 1);
-      LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
+      for (int k = K - 1; k >= 0; --k) {
+        hipLaunchKernelGGL(k_locality_keys, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, g->deg,
+                           nk[k], g->max_degree, k == K - 1 ? 1 : 0, k == 0 ? 1 : 0);
+        LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
+      }
       LPA_HIP(hipGetLastError());
       LPA_HIP(hipFree(rank_of));
     }

@@ -153,7 +153,7 @@ struct lpa_graph {
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   hipGraphExec_t gexec[4] = {};             // captured converged superstep per (cur, par)
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
-  int locality = 1;                         // LPA_LOCALITY=0: plain (degree desc, id) vertex order
+  int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
