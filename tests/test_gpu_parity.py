@@ -140,6 +140,24 @@ def test_rmat_bit_exact(gfa, oracle, scale):
         assert np.array_equal(got[t], hist[t]), f"R-MAT {scale} superstep {t + 1}"
 
 
+@pytest.mark.parametrize("locality", ["0", "1", "3"])
+def test_vertex_order_invariance(gfa, oracle, monkeypatch, locality):
+    """The slot order inside the degree bins (LPA_LOCALITY: plain degree order, or the
+    locality order by K smallest neighbour ranks) is internal: labels per superstep are
+    bit-exact against the oracle under every order (R-MAT scale 16, hubs and all bins)."""
+    monkeypatch.setenv("LPA_LOCALITY", locality)   # read when the handle is created
+    s, d = gfa.gen_rmat(16, 16, seed=3)
+    V = 1 << 16
+    with gfa.Graph(s, d, V) as g:
+        got = []
+        for _ in range(6):
+            g.step(1)
+            got.append(g.labels())
+    _, hist, _ = oracle.lpa(V, s.cpu().numpy(), d.cpu().numpy(), 6, per_iter=True)
+    for t in range(6):
+        assert np.array_equal(got[t], hist[t]), f"LPA_LOCALITY={locality} superstep {t + 1}"
+
+
 def test_c2_sbm_full_size(gfa, oracle):
     """Config C2: planted partition, 1 M vertices / 20 M edges /
     100 blocks, maxIter 10: bit-exact vs the oracle, and the communities recover the
