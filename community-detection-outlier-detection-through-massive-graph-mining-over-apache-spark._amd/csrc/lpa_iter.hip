@@ -863,7 +863,8 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
 // the rebuild is bound by the L2 request rate of its 4-B random gathers, and every
 // gather served by the block's LDS copy is one L2 request fewer.  One 1024-thread
 // block per CU, 128 KB of LDS.
-constexpr int kHotLabels = 32768;
+constexpr int kHotLabels = 32768;          // rank-strided set (P > 1: power-of-two shares)
+constexpr int kHotLabelsSingle = 40960;    // P = 1: the whole 160 KB of LDS
 // kRanked (P > 1, power-of-two slices and rank count): the hottest vertices of rank
 // r's slice are its first slots (degree rank k lives at slot (k mod P) S + k / P),
 // so the global top kHotLabels are the first H = kHotLabels / P slots of every
@@ -875,7 +876,7 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
                                                          int32_t nhot, int32_t* __restrict__ al,
                                                          int slice_lg, int hot_lg) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
-  __shared__ int32_t hot[kHotLabels];
+  __shared__ int32_t hot[kHotLabelsSingle];
   for (int i = threadIdx.x; i < nhot; i += 1024)
     hot[i] = kRanked ? Ln[((int64_t)(i >> hot_lg) << slice_lg) + (i & ((1 << hot_lg) - 1))] : Ln[i];
   __syncthreads();
@@ -1044,7 +1045,7 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
     int slice_lg = 0, hot_lg = 0;
-    int32_t nhot = (int32_t)(g->vpad < kHotLabels ? g->vpad : kHotLabels);
+    int32_t nhot = (int32_t)(g->vpad < kHotLabelsSingle ? g->vpad : kHotLabelsSingle);
     if (ranked) {
       while ((int64_t(1) << slice_lg) < g->slice) ++slice_lg;
       while ((int64_t(1) << hot_lg) < kHotLabels / g->nranks) ++hot_lg;
