@@ -511,13 +511,14 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
 }
 
 // Same over a compact word run wd[0, n) (a bucket after the scatter).
+// No slot list: the occupied slots are found by a scan of the whole table at the
+// end (a bucket pass loads it to ~1/2, so the scan reads about what a list walk
+// would), which keeps the block's LDS at 64 KB + 32 B: two blocks per CU.
 template <typename Keep>
-__device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64* tab, uint16_t* lst,
-                               int* lcount, u64* redw, int32_t* err) {
+__device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64* tab, u64* redw,
+                               int32_t* err) {
   constexpr int kLg = 13;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (threadIdx.x == 0) *lcount = 0;
-  __syncthreads();
   constexpr int R = kCombDirect / 256;
   for (int b0 = 0; b0 < n; b0 += R * 256) {
     u64 wv[R];
@@ -541,16 +542,16 @@ __device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64
       }
       int sl[8];
       insert_words<8, true>(tab, 32 - kLg, (1u << kLg) - 1u, grp, m, sl, err);
-      list_append_n<8>(lst, lcount, sl, lane);
     }
   }
   __syncthreads();
-  const int cnt = *lcount;
   u64 best = 0ull;
-  for (int i = threadIdx.x; i < cnt; i += 256) {
-    const int sl = lst[i];
-    best = umax64(best, tab[sl]);
-    tab[sl] = 0ull;
+  for (int i = threadIdx.x; i < kCombSlots; i += 256) {
+    const u64 t = tab[i];
+    if (t) {
+      best = umax64(best, t);
+      tab[i] = 0ull;
+    }
   }
   best = wave_max_u64(best);
   if (lane == 0) redw[w] = best;
@@ -573,8 +574,13 @@ __global__ __launch_bounds__(256) void k_hub_mid(const int32_t* __restrict__ lis
                                                  int32_t* __restrict__ wcount,
                                                  int32_t* __restrict__ Ln, int32_t* __restrict__ err) {
   constexpr int kSlots = 1 << kLg;
+  // a row of this tier has at most T words, so at most T distinct labels (tiers:
+  // T <= 1024 / 2048 / kCombDirect, queue_row): the list holds T entries, which
+  // keeps the 8K-slot tier's block at 76 KB (two per CU)
+  constexpr int kList = kLg == 11 ? 1024 : kLg == 12 ? 2048 : kCombDirect;
+  static_assert(kList <= kSlots, "list bounded by the table");
   __shared__ u64 tab[kSlots];
-  __shared__ uint16_t lst[kSlots];
+  __shared__ uint16_t lst[kList];
   __shared__ int lcount;
   __shared__ u64 redw[4];
   const int nB = lcnt[which];
@@ -743,8 +749,6 @@ __global__ __launch_bounds__(256) void k_hub_bucket(const u64* __restrict__ item
                                                     u64* __restrict__ hub_best,
                                                     int32_t* __restrict__ err) {
   __shared__ u64 tab[kCombSlots];
-  __shared__ uint16_t lst[kCombSlots];
-  __shared__ int lcount;
   __shared__ u64 redw[4];
   const int n = lcnt[2];
   if ((int)blockIdx.x >= n) return;
@@ -761,7 +765,7 @@ __global__ __launch_bounds__(256) void k_hub_bucket(const u64* __restrict__ item
     u64 best = 0ull;
     for (u32 j = 0; j < (1u << lgJ); ++j)
       best = umax64(best, block_tally_run(wd, cnt, [=](u32 lab) { return comb_sub(lab, lgJ) == j; },
-                                          tab, lst, &lcount, redw, err));
+                                          tab, redw, err));
     if (threadIdx.x == 0 && best) atomicMax(&hub_best[h], best);
   }
 }
