@@ -131,6 +131,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
   if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
   if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
+  if (const char* f = getenv("LPA_HUB_WAVES")) g->hub_waves = atoi(f) == 4 ? 4 : 8;
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   g->rank = rank;
   g->nranks = nranks;

@@ -271,14 +271,16 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
                                                    u64* __restrict__ itemsCB,
                                                    u64* __restrict__ itemsCC) {
   __shared__ u64 tab_all[4][kSmallSlots];
-  __shared__ int32_t aux_all[4][kSmallWords];  // unit prefixes, then the slot list
+  // unit prefixes (< T <= kSmallWords), then the slot list (< kSmallSlots): both fit
+  // 16 bits, so the block takes 36 KB of LDS and four blocks fit a CU
+  __shared__ uint16_t aux_all[4][kSmallWords];
   __shared__ int lc_all[4];
   constexpr int NC = kSmallWords / 64;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   u64* tab = tab_all[w];
-  int32_t* pre = aux_all[w];
-  uint16_t* lst = reinterpret_cast<uint16_t*>(aux_all[w]);
+  uint16_t* pre = aux_all[w];
+  uint16_t* lst = aux_all[w];
   for (int i = lane; i < kSmallSlots; i += 64) tab[i] = 0ull;
   // rows: [0, nd) directly, then list S (pre-classified by k_hub_classify), then
   // list W (from k_hub_lanes)
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
             const int o = __shfl_up(incl, off, 64);
             if (lane >= off) incl += o;
           }
-          if (c * 64 + lane < nu) pre[c * 64 + lane] = carry + incl - cnt[c];
+          if (c * 64 + lane < nu) pre[c * 64 + lane] = (uint16_t)(carry + incl - cnt[c]);
           carry += __shfl(incl, 63, 64);
         }
       }
@@ -428,8 +430,9 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
 }
 
 // Tally the words of units [j0, j1) of a row whose labels pass `keep` into the
-// block's LDS table (kCombSlots slots).  Returns the block-uniform maximum.
-template <int kLg, typename Keep>
+// block's LDS table (kCombSlots slots) with kW waves.  Returns the block-uniform
+// maximum.
+template <int kLg, int kW, typename Keep>
 __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __restrict__ uc, int j0,
                                  int j1, Keep keep, u64* tab, uint16_t* lst, int* lcount, u64* redw,
                                  int32_t* err) {
@@ -437,11 +440,11 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) *lcount = 0;
   __syncthreads();
-  // wave w takes units j0 + w + 4i, 64 at a time: lane-per-unit for each unit's
+  // wave w takes units j0 + w + kW i, 64 at a time: lane-per-unit for each unit's
   // first kFirst words (converged units hold one), then unit-major for longer units
   constexpr int kFirst = 4;
-  for (int jb = j0 + w; jb < j1; jb += 256) {
-    const int j = jb + 4 * lane;
+  for (int jb = j0 + w; jb < j1; jb += 64 * kW) {
+    const int j = jb + kW * lane;
     const int nj = j < j1 ? uc[j] : 0;
     const u64* src = wd + (int64_t)j * kSegArcs;
     u64 fv[kFirst];
@@ -467,7 +470,7 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
       if (set == 0ull) return;
       const int bl = __ffsll((unsigned long long)set) - 1;
       cnt = __builtin_amdgcn_readlane(nj, bl);
-      const u64* us = wd + (int64_t)(jb + 4 * bl) * kSegArcs;
+      const u64* us = wd + (int64_t)(jb + kW * bl) * kSegArcs;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int i = kFirst + c * 64 + lane;
@@ -497,7 +500,7 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
   __syncthreads();
   const int cnt = *lcount;
   u64 best = 0ull;
-  for (int i = threadIdx.x; i < cnt; i += 256) {
+  for (int i = threadIdx.x; i < cnt; i += 64 * kW) {
     const int sl = lst[i];
     best = umax64(best, tab[sl]);
     tab[sl] = 0ull;
@@ -505,7 +508,9 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
   best = wave_max_u64(best);
   if (lane == 0) redw[w] = best;
   __syncthreads();
-  best = umax64(umax64(redw[0], redw[1]), umax64(redw[2], redw[3]));
+  best = redw[0];
+#pragma unroll
+  for (int i = 1; i < kW; ++i) best = umax64(best, redw[i]);
   __syncthreads();
   return best;
 }
@@ -514,17 +519,20 @@ __device__ u64 block_tally_units(const u64* __restrict__ wd, const int32_t* __re
 // No slot list: the occupied slots are found by a scan of the whole table at the
 // end (a bucket pass loads it to ~1/2, so the scan reads about what a list walk
 // would), which keeps the block's LDS at 64 KB + 32 B: two blocks per CU.
-template <typename Keep>
+template <int kW, typename Keep>
 __device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64* tab, u64* redw,
                                int32_t* err) {
   constexpr int kLg = 13;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  constexpr int R = kCombDirect / 256;
-  for (int b0 = 0; b0 < n; b0 += R * 256) {
+  constexpr int kT = 64 * kW;
+  // words per thread per round: 24 at 4 waves (6144), 8 at 8 waves (4096: a bucket
+  // pass's expected load)
+  constexpr int R = kW == 4 ? kCombDirect / 256 : 8;
+  for (int b0 = 0; b0 < n; b0 += R * kT) {
     u64 wv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int i = b0 + r * 256 + threadIdx.x;
+      const int i = b0 + r * kT + threadIdx.x;
       wv[r] = i < n ? wd[i] : 0ull;
     }
     // batched inserts, 8 words per lane in flight (bounded probing: a bucket's
@@ -532,7 +540,7 @@ __device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64
     static_assert(R % 8 == 0, "insert groups of 8");
 #pragma unroll
     for (int r0 = 0; r0 < R; r0 += 8) {
-      if (b0 + r0 * 256 >= n) break;  // uniform over the block
+      if (b0 + r0 * kT >= n) break;  // uniform over the block
       u64 grp[8];
       u32 m = 0u;
 #pragma unroll
@@ -546,7 +554,7 @@ __device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64
   }
   __syncthreads();
   u64 best = 0ull;
-  for (int i = threadIdx.x; i < kCombSlots; i += 256) {
+  for (int i = threadIdx.x; i < kCombSlots; i += kT) {
     const u64 t = tab[i];
     if (t) {
       best = umax64(best, t);
@@ -556,7 +564,9 @@ __device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64
   best = wave_max_u64(best);
   if (lane == 0) redw[w] = best;
   __syncthreads();
-  best = umax64(umax64(redw[0], redw[1]), umax64(redw[2], redw[3]));
+  best = redw[0];
+#pragma unroll
+  for (int i = 1; i < kW; ++i) best = umax64(best, redw[i]);
   __syncthreads();
   return best;
 }
@@ -564,8 +574,10 @@ __device__ u64 block_tally_run(const u64* __restrict__ wd, int n, Keep keep, u64
 // ---------------------------------------------------------------------------
 // 512 < T <= kCombDirect: one block per queued row (grid-stride over the queue).
 // ---------------------------------------------------------------------------
-template <int kLg>
-__global__ __launch_bounds__(256) void k_hub_mid(const int32_t* __restrict__ list,
+// kW waves per block: the 8K-slot tier runs two 76 KB blocks per CU, so it takes
+// 8 waves each (16 resident waves per CU instead of 8 to cover LDS atomic latency)
+template <int kLg, int kW>
+__global__ __launch_bounds__(64 * kW) void k_hub_mid(const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ lcnt, int which,
                                                  const int64_t* __restrict__ rp,
                                                  const int64_t* __restrict__ uoff,
@@ -582,14 +594,14 @@ __global__ __launch_bounds__(256) void k_hub_mid(const int32_t* __restrict__ lis
   __shared__ u64 tab[kSlots];
   __shared__ uint16_t lst[kList];
   __shared__ int lcount;
-  __shared__ u64 redw[4];
+  __shared__ u64 redw[kW];
   const int nB = lcnt[which];
   if ((int)blockIdx.x >= nB) return;
-  for (int i = threadIdx.x; i < kSlots; i += 256) tab[i] = 0ull;
+  for (int i = threadIdx.x; i < kSlots; i += 64 * kW) tab[i] = 0ull;
   for (int q = blockIdx.x; q < nB; q += gridDim.x) {
     const int64_t h = list[q];
     const RowUnits ru = row_units(rp, uoff, h);
-    const u64 best = block_tally_units<kLg>(stage + ru.sbase, ucnt + ru.u0, 0, ru.nu,
+    const u64 best = block_tally_units<kLg, kW>(stage + ru.sbase, ucnt + ru.u0, 0, ru.nu,
                                             [](u32) { return true; }, tab, lst, &lcount, redw, err);
     if (threadIdx.x == 0) {
       Ln[h] = (int32_t)(~(u32)best);
@@ -739,7 +751,9 @@ __global__ __launch_bounds__(256) void k_hub_scatter(const u64* __restrict__ ite
 
 // one block per (row, bucket): after the scatter, bucket k of row h is
 // scat[rp[h] + gcur[k] - ghist[k], rp[h] + gcur[k])
-__global__ __launch_bounds__(256) void k_hub_bucket(const u64* __restrict__ itemsCB,
+// kW waves per block (64.03 KB blocks: two per CU; kW = 8 gives 16 resident waves)
+template <int kW>
+__global__ __launch_bounds__(64 * kW) void k_hub_bucket(const u64* __restrict__ itemsCB,
                                                     const int32_t* __restrict__ lcnt,
                                                     const int64_t* __restrict__ rp,
                                                     const u64* __restrict__ scat,
@@ -749,10 +763,10 @@ __global__ __launch_bounds__(256) void k_hub_bucket(const u64* __restrict__ item
                                                     u64* __restrict__ hub_best,
                                                     int32_t* __restrict__ err) {
   __shared__ u64 tab[kCombSlots];
-  __shared__ u64 redw[4];
+  __shared__ u64 redw[kW];
   const int n = lcnt[2];
   if ((int)blockIdx.x >= n) return;
-  for (int i = threadIdx.x; i < kCombSlots; i += 256) tab[i] = 0ull;
+  for (int i = threadIdx.x; i < kCombSlots; i += 64 * kW) tab[i] = 0ull;
   for (int it = blockIdx.x; it < n; it += gridDim.x) {
     const u64 item = itemsCB[it];
     const int64_t h = (int64_t)(item >> 32);
@@ -764,7 +778,7 @@ __global__ __launch_bounds__(256) void k_hub_bucket(const u64* __restrict__ item
     const int lgJ = cnt > kCombDirect ? ceil_log2((u32)((cnt + 4095) / 4096)) : 0;
     u64 best = 0ull;
     for (u32 j = 0; j < (1u << lgJ); ++j)
-      best = umax64(best, block_tally_run(wd, cnt, [=](u32 lab) { return comb_sub(lab, lgJ) == j; },
+      best = umax64(best, block_tally_run<kW>(wd, cnt, [=](u32 lab) { return comb_sub(lab, lgJ) == j; },
                                           tab, redw, err));
     if (threadIdx.x == 0 && best) atomicMax(&hub_best[h], best);
   }
@@ -911,9 +925,14 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
     hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
                        g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->gcur, g->scat);
     LPA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_hub_bucket, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, sd,
-                       g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
-                       g->hub_best, g->dev_err);
+    if (g->hub_waves == 4)
+      hipLaunchKernelGGL(k_hub_bucket<4>, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, sd,
+                         g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
+                         g->hub_best, g->dev_err);
+    else
+      hipLaunchKernelGGL(k_hub_bucket<8>, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(512), 0, sd,
+                         g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
+                         g->hub_best, g->dev_err);
     LPA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
                        lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown,
@@ -941,15 +960,20 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
                      g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, lists, lcnt, g->items_cb,
                      g->items_cc);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_mid<13>, dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,
-                     lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
-                     g->dev_err);
+  if (g->hub_waves == 4)
+    hipLaunchKernelGGL((k_hub_mid<13, 4>), dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,
+                       lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
+                       g->dev_err);
+  else
+    hipLaunchKernelGGL((k_hub_mid<13, 8>), dim3(grid_cap(n, 512)), dim3(512), 0, s, lists + 4 * n,
+                       lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
+                       g->dev_err);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_mid<12>, dim3(grid_cap(n, 1024)), dim3(256), 0, s, lists + 3 * n,
+  hipLaunchKernelGGL((k_hub_mid<12, 4>), dim3(grid_cap(n, 1024)), dim3(256), 0, s, lists + 3 * n,
                      lcnt, 5, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
                      g->dev_err);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_hub_mid<11>, dim3(grid_cap(n, 2048)), dim3(256), 0, s, lists, lcnt, 0,
+  hipLaunchKernelGGL((k_hub_mid<11, 4>), dim3(grid_cap(n, 2048)), dim3(256), 0, s, lists, lcnt, 0,
                      g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
   LPA_HIP(hipGetLastError());
   if (!fork) LPA_TRY(bucket_path());

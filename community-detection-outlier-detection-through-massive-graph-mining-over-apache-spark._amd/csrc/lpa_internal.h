@@ -154,6 +154,7 @@ struct lpa_graph {
   hipGraphExec_t gexec[4] = {};             // captured converged superstep per (cur, par)
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
+  int hub_waves = 8;                        // LPA_HUB_WAVES: waves per block of the 8K-slot hub combine (4 or 8)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
