@@ -94,15 +94,31 @@ __device__ __forceinline__ void insert_word(u64 word, bool act, u64* tab, uint16
 // ---------------------------------------------------------------------------
 // rows of <= kLaneUnits units (deg <= 4096): one LANE per row.  A converged
 // row left one word per unit; the lane loads them and takes the mode of <= 8
-// words in registers.  Any other row is handed to k_hub_small (list W).
+// words in registers.  Any other row is classified here by its word count T
+// (<= 8 x 512, never bucketed): T <= kSmallWords -> k_hub_small (list W), else
+// the k_hub_mid tier queue_row would pick, with ONE queue atomic per wave and
+// list: a row-at-a-time queue_row in k_hub_small serialised ~10^5 returning
+// atomics on three counters in the label-dense supersteps (0.5 ms of waiting).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_append(bool p, int32_t* __restrict__ dst, int32_t* ctr,
+                                            int32_t v, int lane) {
+  const u64 m = __ballot(p);
+  if (m == 0ull) return;  // uniform over the wave
+  const int lead = __ffsll((unsigned long long)m) - 1;
+  int base = 0;
+  if (lane == lead) base = atomicAdd(ctr, __popcll(m));
+  base = __builtin_amdgcn_readlane(base, lead);
+  if (p) dst[base + __popcll(m & ((1ull << lane) - 1ull))] = v;
+}
+
 __global__ __launch_bounds__(256) void k_hub_lanes(int64_t h_begin, int64_t h_end,
                                                    const int64_t* __restrict__ rp,
                                                    const int64_t* __restrict__ uoff,
                                                    const int32_t* __restrict__ ucnt,
                                                    const u64* __restrict__ stage,
                                                    int32_t* __restrict__ Ln,
-                                                   int32_t* __restrict__ listW,
+                                                   int32_t* __restrict__ lists, int64_t n_hub,
+                                                   int32_t* __restrict__ wcount,
                                                    int32_t* __restrict__ lcnt) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -110,6 +126,7 @@ __global__ __launch_bounds__(256) void k_hub_lanes(int64_t h_begin, int64_t h_en
     const int64_t h = h0 + threadIdx.x;
     const bool live = h < h_end;
     bool one = false;
+    int T = 0;
     if (live) {
       const int64_t b = rp[h];
       const int nu = (int)((rp[h + 1] - b + kSegArcs - 1) / kSegArcs);
@@ -117,6 +134,8 @@ __global__ __launch_bounds__(256) void k_hub_lanes(int64_t h_begin, int64_t h_en
       int c[kLaneUnits];
 #pragma unroll
       for (int k = 0; k < kLaneUnits; ++k) c[k] = k < nu ? uc[k] : 1;
+#pragma unroll
+      for (int k = 0; k < kLaneUnits; ++k) T += k < nu ? c[k] : 0;
       one = true;
 #pragma unroll
       for (int k = 0; k < kLaneUnits; ++k) one = one && c[k] == 1;
@@ -137,16 +156,16 @@ __global__ __launch_bounds__(256) void k_hub_lanes(int64_t h_begin, int64_t h_en
         Ln[h] = (int32_t)(~(u32)best);
       }
     }
-    const u64 m = __ballot(live && !one);
-    if (m) {
-      const int lead = __ffsll((unsigned long long)m) - 1;
-      int base = 0;
-      if (lane == lead) base = atomicAdd(&lcnt[4], __popcll(m));
-      base = __builtin_amdgcn_readlane(base, lead);
-      if (live && !one) listW[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)h;
-    }
+    const bool q = live && !one;
+    if (q && T > kSmallWords) wcount[h] = T;  // as queue_row
+    // lists: [0] mid T <= 1024, [2n] wave path (list W), [3n] mid <= 2048, [4n] mid <= 6144
+    wave_append(q && T <= kSmallWords, lists + 2 * n_hub, &lcnt[4], (int32_t)h, lane);
+    wave_append(q && T > kSmallWords && T <= 1024, lists, &lcnt[0], (int32_t)h, lane);
+    wave_append(q && T > 1024 && T <= 2048, lists + 3 * n_hub, &lcnt[5], (int32_t)h, lane);
+    wave_append(q && T > 2048, lists + 4 * n_hub, &lcnt[6], (int32_t)h, lane);
   }
 }
+static_assert(kLaneUnits * kSegArcs <= kCombDirect, "lane-path rows are never bucketed");
 
 // queue row h (T staged words) for k_hub_mid (three table sizes) or the bucket
 // path.  lists: [0] mid T <= 1024, [n] bucketed, [2n] wave path, [3n] mid <= 2048,
@@ -909,7 +928,6 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   // queue counters of this superstep's parity (zeroed by the previous k_hub_final)
   int32_t* lcnt = g->hub_lcnt + 8 * g->par;
   const int64_t hl = g->hub_lane_begin;
-  int32_t* listW = g->hub_lists + 2 * n;
   // fork (label-dense supersteps): classify the > 8-unit rows first and start the
   // bucket path on its own stream; the mid tiers follow k_hub_small on the main
   // stream.  Otherwise everything runs in order on the main stream.
@@ -953,7 +971,7 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   }
   if (hl < n) {
     hipLaunchKernelGGL(k_hub_lanes, dim3(grid_cap((n - hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
-                       g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, listW, lcnt);
+                       g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, lists, n, g->hub_wcount, lcnt);
     LPA_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, fork ? (int64_t)0 : hl, n, g->rp,
