@@ -205,9 +205,10 @@ __device__ __forceinline__ void queue_row(int64_t h, int T, int nu, int lane,
 // Label-dense supersteps: classify the rows of > kLaneUnits units right after the
 // unit tallies, so the bucket path (count / scan / scatter / bucket, complete once
 // these rows are queued: rows of <= kLaneUnits units never exceed kCombDirect words)
-// can start on its own stream while k_hub_small works through the rest.  Rows of
-// <= kSmallWords units and words go to list S for k_hub_small; the others are
-// queued with their word count as k_hub_small would.
+// can start on its own stream while k_hub_small works through the rest.  One wave
+// per row sums its word count T into wcount[h] (and emits a bucketed row's work
+// items); k_hub_enqueue then appends the rows to list S (<= kSmallWords units and
+// words, for k_hub_small) or the tier queue_row would pick.
 __global__ __launch_bounds__(256) void k_hub_classify(int64_t h_lane, int64_t n_hub,
                                                       const int64_t* __restrict__ rp,
                                                       const int64_t* __restrict__ uoff,
@@ -227,11 +228,53 @@ __global__ __launch_bounds__(256) void k_hub_classify(int64_t h_lane, int64_t n_
     int T = 0;
     for (int j = lane; j < nu; j += 64) T += uc[j];
     T = (int)wave_sum_u32((u32)T);
-    if (nu <= kSmallWords && T <= kSmallWords) {
-      if (lane == 0) lists[5 * n_hub + atomicAdd(&lcnt[7], 1)] = (int32_t)h;
-    } else {
-      queue_row(h, T, nu, lane, wcount, lists, n_hub, lcnt, itemsCB, itemsCC);
+    if (lane == 0) wcount[h] = T;
+    if (T > kCombDirect) {
+      // bucketed row (few per superstep): its count / bucket work items, as queue_row
+      const int K = 1 << comb_lgK(T);
+      const int nch = (nu + kChunkUnits - 1) / kChunkUnits;
+      int cb = 0, cc = 0;
+      if (lane == 0) {
+        cb = atomicAdd(&lcnt[2], K);
+        cc = atomicAdd(&lcnt[3], nch);
+      }
+      cb = __builtin_amdgcn_readfirstlane(cb);
+      cc = __builtin_amdgcn_readfirstlane(cc);
+      for (int k = lane; k < K; k += 64) itemsCB[cb + k] = ((u64)h << 32) | (u64)k;
+      for (int c = lane; c < nch; c += 64) itemsCC[cc + c] = ((u64)h << 32) | (u64)c;
     }
+  }
+}
+
+// Second half of the classification: one LANE per row of [0, h_lane), its word
+// count from k_hub_classify, every list appended with one atomic per wave (a
+// returning atomic per row on a shared counter serialises: 0.2 ms for ~10^4 rows
+// in the label-dense supersteps).  Bucketed rows (T > kCombDirect, few) got their
+// work items from k_hub_classify.
+__global__ __launch_bounds__(256) void k_hub_enqueue(int64_t h_lane, int64_t n_hub,
+                                                     const int64_t* __restrict__ uoff,
+                                                     int32_t* __restrict__ wcount,
+                                                     int32_t* __restrict__ lists,
+                                                     int32_t* __restrict__ lcnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t h0 = (int64_t)blockIdx.x * blockDim.x; h0 < h_lane; h0 += stride) {
+    const int64_t h = h0 + threadIdx.x;
+    const bool live = h < h_lane;
+    int T = 0, nu = 0;
+    if (live) {
+      T = wcount[h];
+      nu = (int)(uoff[h + 1] - uoff[h]);
+    }
+    const bool sm = live && nu <= kSmallWords && T <= kSmallWords;
+    const bool q = live && !sm;
+    if (sm) wcount[h] = 0;  // only queued rows keep T (queue_row's contract)
+    // lists: [0] mid T <= 1024, [n] bucketed, [3n] mid <= 2048, [4n] mid <= 6144, [5n] S
+    wave_append(sm, lists + 5 * n_hub, &lcnt[7], (int32_t)h, lane);
+    wave_append(q && T <= 1024, lists, &lcnt[0], (int32_t)h, lane);
+    wave_append(q && T > 1024 && T <= 2048, lists + 3 * n_hub, &lcnt[5], (int32_t)h, lane);
+    wave_append(q && T > 2048 && T <= kCombDirect, lists + 4 * n_hub, &lcnt[6], (int32_t)h, lane);
+    wave_append(q && T > kCombDirect, lists + n_hub, &lcnt[1], (int32_t)h, lane);
   }
 }
 
@@ -963,6 +1006,9 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
       hipLaunchKernelGGL(k_hub_classify, dim3(grid_cap((hl + 3) / 4, 2048)), dim3(256), 0, s, hl, n,
                          g->rp, g->hub_uoff, g->ucnt, g->hub_wcount, lists, lcnt, g->items_cb,
                          g->items_cc);
+      LPA_HIP(hipGetLastError());
+      hipLaunchKernelGGL(k_hub_enqueue, dim3(grid_cap((hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
+                         g->hub_uoff, g->hub_wcount, lists, lcnt);
       LPA_HIP(hipGetLastError());
     }
     LPA_HIP(hipEventRecord(g->ev_fork2, s));
