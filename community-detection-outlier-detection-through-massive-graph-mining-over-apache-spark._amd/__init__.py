@@ -7,10 +7,10 @@ compute runs in liblpa_hip.so (hand-written HIP for gfx950, C ABI in
 include/lpa.h); importing this package does not load it -- the first call does,
 and fails loudly if it has not been built.
 """
-from .graph import Graph, comm_unique_id, gen_chunglu, gen_rmat, gen_sbm
+from .graph import Graph, Loopback, comm_unique_id, gen_chunglu, gen_rmat, gen_sbm, run_ranks
 from .graphframe import (GraphFrame, IndexedGraph, OutlierResult, index_graph, label_propagation,
                          outlier_scores)
 from . import ingest
 
-__all__ = ["Graph", "GraphFrame", "IndexedGraph", "OutlierResult", "comm_unique_id", "gen_chunglu", "gen_rmat",
+__all__ = ["Graph", "Loopback", "run_ranks", "GraphFrame", "IndexedGraph", "OutlierResult", "comm_unique_id", "gen_chunglu", "gen_rmat",
            "gen_sbm", "index_graph", "ingest", "label_propagation", "outlier_scores"]

@@ -59,6 +59,7 @@ class LpaGraphInfo(ctypes.Structure):
         ("bin_vertices", ctypes.c_int64 * LPA_NBINS), ("bin_arcs", ctypes.c_int64 * LPA_NBINS),
         ("hub_vertices", ctypes.c_int64), ("segments", ctypes.c_int64),
         ("device_bytes", ctypes.c_int64),
+        ("exchanges_full", ctypes.c_int64), ("exchanges_delta", ctypes.c_int64),
     ]
 
     def to_dict(self):
@@ -98,6 +99,11 @@ SIGNATURES = {
     "lpa_outlier": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                    _i64p, _i64p, _i32p, _u8p, ctypes.POINTER(LpaOutlierSummary)]),
     "lpa_degrees": (ctypes.c_int, [_vp, _i32p]),
+    "lpa_loopback_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_vp)]),
+    "lpa_loopback_abort": (None, [_vp]),
+    "lpa_loopback_destroy": (None, [_vp]),
+    "lpa_graph_create_loopback": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                                 ctypes.c_uint32, ctypes.c_int32, _vp, ctypes.POINTER(_vp)]),
     "lpa_exchange_get": (ctypes.c_int, [_vp, _i32p]),
     "lpa_exchange_put": (ctypes.c_int, [_vp, _i32p]),
     "lpa_exchange_get_delta": (ctypes.c_int, [_vp, _vp, _i64p]),

@@ -251,6 +251,7 @@ int init_labels(lpa_graph* g) {
   hipLaunchKernelGGL(k_init_labels, dim3(grid_for(g->vpad)), dim3(256), 0, g->stream, g->old_of,
                      g->vpad, g->lab[0], g->lab[1]);
   LPA_HIP(hipGetLastError());
+  if (g->dev_err) LPA_HIP(hipMemsetAsync(g->dev_err, 0, sizeof(int32_t), g->stream));
   g->cur = 0;
   g->since_reset = 0;
   g->prev_delta_ok = false;  // the exchange's delta chain restarts from L0

@@ -49,6 +49,7 @@ int gen_chunglu(int32_t V, int64_t m, double gamma, double max_deg, uint64_t see
 
 void destroy(lpa_graph* g) {
   if (g) exchange_free(g);
+  if (g) loopback_detach(g);
   if (g)
     for (auto& ge : g->gexec)
       if (ge) (void)hipGraphExecDestroy(ge);
@@ -108,7 +109,7 @@ static int check_edges(const int32_t* src, const int32_t* dst, int64_t m, int32_
 
 int create_common(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
                   int64_t m, int32_t V, uint32_t flags, int32_t rank, int32_t nranks,
-                  const uint8_t* comm_id, lpa_graph** out) {
+                  const uint8_t* comm_id, Loopback* loop, lpa_graph** out) {
   if (!out) {
     set_error("out must be non-null");
     return LPA_EINVAL;
@@ -159,7 +160,13 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
       return LPA_EHIP;
     }
   }
-  if (nranks > 1 && comm_id) {
+  if (loop) {
+    int rc = loopback_attach(g, loop);
+    if (rc != LPA_OK) {
+      destroy(g);
+      return rc;
+    }
+  } else if (nranks > 1 && comm_id) {
     ncclUniqueId id;
     memcpy(&id, comm_id, sizeof(id));
     ncclResult_t r = ncclCommInitRank(&g->comm, nranks, id, rank);
@@ -182,7 +189,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
 
 int create_local(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
                  int64_t m, int32_t V, uint32_t flags, lpa_graph** out) {
-  return create_common(device, stream, src, dst, m, V, flags, 0, 1, nullptr, out);
+  return create_common(device, stream, src, dst, m, V, flags, 0, 1, nullptr, nullptr, out);
 }
 
 }  // namespace lpa
@@ -195,7 +202,7 @@ const char* lpa_last_error(void) { return g_err; }
 
 int lpa_graph_create(const int32_t* src, const int32_t* dst, int64_t m, int32_t V, int32_t device,
                      uint32_t flags, lpa_graph** out) {
-  return create_common(device, nullptr, src, dst, m, V, flags, 0, 1, nullptr, out);
+  return create_common(device, nullptr, src, dst, m, V, flags, 0, 1, nullptr, nullptr, out);
 }
 
 int lpa_comm_unique_id(uint8_t id_out[128]) {
@@ -217,7 +224,19 @@ int lpa_comm_unique_id(uint8_t id_out[128]) {
 int lpa_graph_create_dist(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
                           int32_t device, uint32_t flags, int32_t rank, int32_t nranks,
                           const uint8_t comm_id[128], lpa_graph** out) {
-  return create_common(device, nullptr, src, dst, m, V, flags, rank, nranks, comm_id, out);
+  return create_common(device, nullptr, src, dst, m, V, flags, rank, nranks, comm_id, nullptr, out);
+}
+
+int lpa_graph_create_loopback(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                              int32_t device, uint32_t flags, int32_t rank, lpa_loopback* group,
+                              lpa_graph** out) {
+  if (!group) {
+    set_error("lpa_graph_create_loopback: null group");
+    return LPA_EINVAL;
+  }
+  Loopback* lb = reinterpret_cast<Loopback*>(group);
+  return create_common(device, nullptr, src, dst, m, V, flags, rank, loopback_ranks(lb), nullptr, lb,
+                       out);
 }
 
 int lpa_exchange_get(lpa_graph* g, int32_t* slice_out) {
@@ -436,6 +455,8 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->hub_vertices = g->n_hub;
   info->segments = g->n_segs;
   info->device_bytes = g->device_bytes;
+  info->exchanges_full = g->n_exch_full;
+  info->exchanges_delta = g->n_exch_delta;
   return LPA_OK;
 }
 

@@ -204,21 +204,17 @@ int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t 
   return LPA_OK;
 }
 
-// In-library RCCL exchange of one superstep (P > 1, comm set): Lown = Ln + own_begin
-// holds the new owned labels; on return Ln holds the full new label vector.
-// *changes_listed: the refresh's position chunks were queued from the delta.
-int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed) {
+// In-library exchange of one superstep (P > 1, RCCL communicator or loopback group):
+// Lown = Ln + own_begin holds the new owned labels; on return Ln holds the full new
+// label vector.  *changes_listed: the refresh's position chunks were queued from the delta.
+int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed) {
   hipStream_t s = g->stream;
   int32_t* Lown = Ln + g->own_begin;
   *changes_listed = false;
   if (!dense) {
     LPA_TRY(exchange_compact(g, Lc, Ln));
     unsigned long long* counts = exchange_recv_counts(g);
-    ncclResult_t r = ncclAllGather(g->dcount, counts, 1, ncclUint64, g->comm, s);
-    if (r != ncclSuccess) {
-      set_error("ncclAllGather (delta counts): %s", ncclGetErrorString(r));
-      return LPA_ERCCL;
-    }
+    LPA_TRY(coll_allgather(g, g->dcount, counts, 1, 8, s));
     LPA_HIP(hipMemcpyAsync(g->h_dcounts, counts, sizeof(unsigned long long) * g->nranks,
                            hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
@@ -226,24 +222,17 @@ int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool
     for (int k = 0; k < g->nranks; ++k)
       if ((int64_t)g->h_dcounts[k] > cap) cap = (int64_t)g->h_dcounts[k];
     if (cap <= g->dcap) {
-      if (cap > 0) {
-        r = ncclAllGather(g->dsend, exchange_recv_buf(g), (size_t)cap, ncclUint64, g->comm, s);
-        if (r != ncclSuccess) {
-          set_error("ncclAllGather (delta): %s", ncclGetErrorString(r));
-          return LPA_ERCCL;
-        }
-      }
+      if (cap > 0) LPA_TRY(coll_allgather(g, g->dsend, exchange_recv_buf(g), (size_t)cap, 8, s));
       g->last_exchange_delta = cap;
+      ++g->n_exch_delta;
       *changes_listed = true;
       return exchange_finish_delta(g, Lc, Ln, cap);
     }
   }
-  ncclResult_t r = ncclAllGather(Lown, Ln, (size_t)g->slice, ncclInt32, g->comm, s);
-  if (r != ncclSuccess) {
-    set_error("ncclAllGather: %s", ncclGetErrorString(r));
-    return LPA_ERCCL;
-  }
+  // full: in-place allgather of the owned slices (rank r's slice at Ln + r * slice)
+  LPA_TRY(coll_allgather(g, Lown, Ln, (size_t)g->slice, 4, s));
   g->last_exchange_delta = -1;
+  ++g->n_exch_full;
   g->prev_delta_ok = false;
   return LPA_OK;
 }

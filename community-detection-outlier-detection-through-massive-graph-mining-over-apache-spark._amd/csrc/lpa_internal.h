@@ -76,6 +76,8 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+struct Loopback;  // in-process collective over P handles on one device (lpa_comm.cpp)
+
 }  // namespace lpa
 
 struct lpa_graph {
@@ -88,7 +90,13 @@ struct lpa_graph {
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   hipEvent_t ev_fork2 = nullptr, ev_join2[2] = {nullptr, nullptr};  // hub combine tail (join2[0] used)
   int32_t rank = 0, nranks = 1;
+  // label-exchange collective backend (P > 1): RCCL communicator (one process per
+  // GPU) or the in-process loopback group (P handles on one device, one host thread
+  // each); neither = the caller-driven exchange (lpa_exchange_get/put)
   ncclComm_t comm = nullptr;
+  lpa::Loopback* loop = nullptr;
+  hipEvent_t loop_ev[2] = {nullptr, nullptr};  // loopback: send-ready / copies-done marks
+  int64_t n_exch_full = 0, n_exch_delta = 0;   // exchanges by mode (lpa_graph_info)
 
   int64_t V = 0, m = 0;
   int64_t slice = 0;      // vertex slots per rank
@@ -206,6 +214,15 @@ int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
 int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st);
 int gather_labels(lpa_graph* g, int32_t* out_dense_dev);
 
+// collective backend (lpa_comm.cpp): allgather of `count` elements of `elem` bytes
+// per rank in rank order (in place when send == recv + rank * count * elem),
+// stream-ordered on s, on the handle's RCCL communicator or loopback group
+inline bool has_collective(const lpa_graph* g) { return g->comm != nullptr || g->loop != nullptr; }
+int coll_allgather(lpa_graph* g, const void* send, void* recv, size_t count, int elem, hipStream_t s);
+int loopback_attach(lpa_graph* g, Loopback* lb);  // registers the handle's rank slot
+int loopback_ranks(const Loopback* lb);
+void loopback_detach(lpa_graph* g);
+
 // label exchange (lpa_exchange.hip)
 int exchange_alloc(lpa_graph* g);
 void exchange_free(lpa_graph* g);
@@ -213,7 +230,7 @@ int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln);
 lpa::u64* exchange_recv_buf(lpa_graph* g);
 unsigned long long* exchange_recv_counts(lpa_graph* g);
 int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap);
-int exchange_rccl(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed);
+int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed);
 int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done);
 
 // outlier (lpa_outlier.hip)

@@ -1163,13 +1163,13 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
     if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
     bool changes_listed = false;
-    if (g->nranks > 1 && g->comm)
-      LPA_TRY(exchange_rccl(g, Lc, Ln, g->since_reset < kDenseSupersteps, &changes_listed));
+    if (g->nranks > 1 && has_collective(g))
+      LPA_TRY(exchange_collective(g, Lc, Ln, g->since_reset < kDenseSupersteps, &changes_listed));
     if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
     // P > 1 without a communicator: the caller completes the superstep with
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
     // (changes + refresh); a refresh here would see a partial vector
-    if (g->nranks == 1 || g->comm) LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed));
+    if (g->nranks == 1 || has_collective(g)) LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed));
     if (tt) {
       LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));
       LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
@@ -1184,6 +1184,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     int32_t err = 0;
     LPA_HIP(hipMemcpy(&err, g->dev_err, sizeof(err), hipMemcpyDeviceToHost));
     if (err) {
+      // reported once per call: a later call on this handle starts clean
+      LPA_HIP(hipMemset(g->dev_err, 0, sizeof(int32_t)));
       set_error("superstep kernel capacity overflow (flags 0x%x): a hub combine bucket exceeded "
                 "its LDS table", err);
       return LPA_EOVERFLOW;

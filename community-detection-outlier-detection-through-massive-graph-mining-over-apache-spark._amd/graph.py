@@ -46,12 +46,15 @@ class Graph:
 
     ``Graph(src, dst, V)`` builds on ``device``; ``Graph(..., rank=r, nranks=P,
     comm_id=id)`` builds rank r's slice for a P-GPU run (one process per GPU,
-    RCCL allgather per superstep); ``comm_id=None`` with ``nranks > 1`` selects the
-    caller-driven exchange (``exchange_get`` / ``exchange_put``).
+    RCCL allgather per superstep); ``Graph(..., rank=r, loopback=group)`` builds
+    rank r of an in-process ``Loopback`` group (P handles on one device, one host
+    thread each, the same exchange code with D2D copies for the allgather);
+    ``comm_id=None`` with ``nranks > 1`` selects the caller-driven exchange
+    (``exchange_get`` / ``exchange_put``).
     """
 
     def __init__(self, src, dst, num_vertices: int, device: int = 0, rank: int = 0,
-                 nranks: int = 1, comm_id: bytes | None = None):
+                 nranks: int = 1, comm_id: bytes | None = None, loopback: "Loopback | None" = None):
         lib = _lib.load()
         self._lib = lib
         self._h = ctypes.c_void_p()
@@ -59,7 +62,11 @@ class Graph:
         V = int(num_vertices)
         if V < 0 or V > np.iinfo(np.int32).max:
             raise ValueError(f"num_vertices out of range: {V}")
-        if nranks == 1:
+        if loopback is not None:
+            nranks = loopback.nranks
+            rc = lib.lpa_graph_create_loopback(sp, dp, m, V, device, flags, rank, loopback._handle(),
+                                               ctypes.byref(self._h))
+        elif nranks == 1:
             rc = lib.lpa_graph_create(sp, dp, m, V, device, flags, ctypes.byref(self._h))
         else:
             cid = None if comm_id is None else bytes(comm_id)
@@ -74,6 +81,7 @@ class Graph:
         self.device = device
         self.rank = rank
         self.nranks = nranks
+        self._loopback = loopback   # the group must outlive the handle
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -191,6 +199,62 @@ class Graph:
             flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(summ)))
         return dict(size=size, incident=inc, sub_labels=sub, flags=flags.astype(bool),
                     summary=summ.to_dict())
+
+
+class Loopback:
+    """In-process collective group of ``nranks`` handles on one device (the
+    multi-GPU exchange rehearsed on one GPU).  Drive each rank's Graph from its own
+    thread; ctypes releases the GIL during the library calls."""
+
+    def __init__(self, nranks: int):
+        self._lib = _lib.load()
+        self._h = ctypes.c_void_p()
+        _lib.check(self._lib.lpa_loopback_create(int(nranks), ctypes.byref(self._h)))
+        self.nranks = int(nranks)
+
+    def _handle(self):
+        if not self._h:
+            raise ValueError("loopback group is closed")
+        return self._h
+
+    def abort(self):
+        """Release every thread blocked in a collective of this group (they fail)."""
+        if self._h:
+            self._lib.lpa_loopback_abort(self._h)
+
+    def close(self):
+        if self._h:
+            self._lib.lpa_loopback_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+
+def run_ranks(graphs, fn):
+    """Call ``fn(rank, graph)`` for every rank of a loopback group on its own thread;
+    returns the results in rank order, re-raising the first failure (after aborting
+    the group so no thread stays blocked in a collective)."""
+    import threading
+
+    res = [None] * len(graphs)
+    err = [None] * len(graphs)
+
+    def work(r):
+        try:
+            res[r] = fn(r, graphs[r])
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            err[r] = e
+            lb = graphs[r]._loopback
+            if lb is not None:
+                lb.abort()
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(len(graphs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in err:
+        if e is not None:
+            raise e
+    return res
 
 
 def comm_unique_id() -> bytes:

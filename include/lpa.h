@@ -70,6 +70,8 @@ typedef struct lpa_graph_info {
   int64_t hub_vertices; /* vertices split over several segments (global merge) */
   int64_t segments;     /* segment count of bin 0                             */
   int64_t device_bytes; /* device memory held by the handle                   */
+  int64_t exchanges_full;  /* P > 1: label exchanges done as a full allgather   */
+  int64_t exchanges_delta; /* P > 1: label exchanges done as changed-label deltas */
 } lpa_graph_info;
 
 /* Outlier summary. */
@@ -108,6 +110,25 @@ int lpa_comm_unique_id(uint8_t id_out[128]);
 int lpa_graph_create_dist(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
                           int32_t device, uint32_t flags, int32_t rank, int32_t nranks,
                           const uint8_t comm_id[128], lpa_graph** out);
+
+/*
+ * In-process loopback collective (SURVEY.md §8(e) "fake backend"): P handles on ONE
+ * device, each created with lpa_graph_create_loopback and driven by its OWN host
+ * thread (lpa_run / lpa_step concurrently, as P processes would).  The library's
+ * exchange runs unchanged -- full/delta switch, host count read, in-place
+ * allgather, delta chain -- with the allgather done as stream-ordered D2D copies
+ * between the handles instead of ncclAllGather.  The group must outlive its
+ * handles.  lpa_loopback_abort releases every thread waiting in a collective
+ * (each then fails with LPA_ERCCL); a rank whose peers never arrive fails the
+ * same way after 300 s.
+ */
+typedef struct lpa_loopback lpa_loopback;
+int lpa_loopback_create(int32_t nranks, lpa_loopback** out);
+void lpa_loopback_abort(lpa_loopback* group);
+void lpa_loopback_destroy(lpa_loopback* group);
+int lpa_graph_create_loopback(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                              int32_t device, uint32_t flags, int32_t rank, lpa_loopback* group,
+                              lpa_graph** out);
 
 /*
  * Caller-driven label exchange (a handle built by lpa_graph_create_dist with

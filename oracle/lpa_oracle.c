@@ -176,12 +176,27 @@ static int build_csr(int32_t V, int64_t m, const int32_t* src, const int32_t* ds
   int32_t* col = (int32_t*)malloc(sizeof(int32_t) * (size_t)(2 * m > 0 ? 2 * m : 1));
   int64_t* cur = (int64_t*)malloc(sizeof(int64_t) * ((size_t)V + 1));
   if (!rp || !col || !cur) { free(rp); free(col); free(cur); return -1; }
-  for (int64_t e = 0; e < m; ++e) { rp[src[e] + 1]++; rp[dst[e] + 1]++; }
+  /* parallel counting + scatter (full-size test configs have up to 2.8 B arcs); the
+   * order of the neighbours inside a row is unspecified -- the mode does not depend
+   * on it (mode_min_tie sorts) */
+#pragma omp parallel for schedule(static)
+  for (int64_t e = 0; e < m; ++e) {
+#pragma omp atomic
+    rp[src[e] + 1]++;
+#pragma omp atomic
+    rp[dst[e] + 1]++;
+  }
   for (int32_t v = 0; v < V; ++v) rp[v + 1] += rp[v];
   memcpy(cur, rp, sizeof(int64_t) * (size_t)V);
+#pragma omp parallel for schedule(static)
   for (int64_t e = 0; e < m; ++e) {
-    col[cur[src[e]]++] = dst[e];
-    col[cur[dst[e]]++] = src[e];
+    int64_t a, b;
+#pragma omp atomic capture
+    a = cur[src[e]]++;
+#pragma omp atomic capture
+    b = cur[dst[e]]++;
+    col[a] = dst[e];
+    col[b] = src[e];
   }
   free(cur);
   *rp_out = rp;

@@ -1,0 +1,115 @@
+"""Multi-rank label exchange executed by the library itself.
+
+P handles of an in-process loopback group share one device; each is driven by its
+own host thread, exactly as P processes drive their ranks under
+torch.distributed.run.  Every superstep goes through the library's own exchange
+(lpa_exchange.hip exchange_collective: full allgather in the label-dense
+supersteps, then the changed-label delta protocol with its host count read, the
+in-place allgather offsets and the previous/next delta chain); only the transport
+differs from RCCL (stream-ordered D2D copies, lpa_comm.cpp).  Bit-exact against
+the oracle per superstep; reference call: Graphframes.py:81.
+"""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from graphs import degree_mix
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gfa():
+    import graphframes_amd
+
+    return graphframes_amd
+
+
+def _group(gfa, s, d, V, P):
+    lb = gfa.Loopback(P)
+    return lb, [gfa.Graph(s, d, V, rank=r, loopback=lb) for r in range(P)]
+
+
+def _close(lb, ranks):
+    for g in ranks:
+        g.close()
+    lb.close()
+
+
+def _per_step_all_ranks(gfa, ranks, n):
+    def work(r, g):
+        out = []
+        for _ in range(n):
+            g.step(1)
+            out.append(g.labels())
+        return out
+
+    return gfa.run_ranks(ranks, work)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_loopback_rmat18_every_superstep(gfa, oracle, P):
+    s, d = gfa.gen_rmat(18, 16, seed=1)
+    V = 1 << 18
+    s, d = s.cpu().numpy(), d.cpu().numpy()
+    _, hist, _ = oracle.lpa(V, s, d, 10, per_iter=True)
+    lb, ranks = _group(gfa, s, d, V, P)
+    try:
+        infos = [g.info() for g in ranks]
+        assert sum(i["arcs"] for i in infos) == 2 * s.size
+        got = _per_step_all_ranks(gfa, ranks, 10)
+        for r in range(P):
+            for t in range(10):
+                bad = int((got[r][t] != hist[t]).sum())
+                assert bad == 0, f"P={P} rank {r} superstep {t + 1}: {bad} labels differ"
+        infos = [g.info() for g in ranks]
+        # the dense supersteps after L0 exchange full slices, the converged ones deltas
+        assert all(i["exchanges_full"] >= 2 and i["exchanges_delta"] >= 2 for i in infos), infos
+        # lpa_run (reset + 10 supersteps) on every rank concurrently: same answer
+        runs = gfa.run_ranks(ranks, lambda r, g: g.run(10))
+        for r in range(P):
+            assert np.array_equal(runs[r], hist[9]), f"P={P} rank {r} lpa_run(10)"
+    finally:
+        _close(lb, ranks)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_loopback_degree_mix_every_superstep(gfa, oracle, P):
+    V, s, d = degree_mix(11)
+    _, hist, _ = oracle.lpa(V, s, d, 10, per_iter=True)
+    lb, ranks = _group(gfa, s, d, V, P)
+    try:
+        got = _per_step_all_ranks(gfa, ranks, 10)
+        for r in range(P):
+            for t in range(10):
+                assert np.array_equal(got[r][t], hist[t]), f"P={P} rank {r} superstep {t + 1}"
+        assert all(g.info()["exchanges_delta"] >= 2 for g in ranks)
+    finally:
+        _close(lb, ranks)
+
+
+def test_loopback_abort_releases_waiting_rank(gfa):
+    """A rank whose peer never arrives is released by lpa_loopback_abort and fails
+    with an error instead of blocking its thread."""
+    V, s, d = degree_mix(2)
+    lb, ranks = _group(gfa, s, d, V, 2)
+    try:
+        err = []
+
+        def lone():
+            try:
+                ranks[0].run(3)
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+
+        th = threading.Thread(target=lone)
+        th.start()
+        time.sleep(1.0)
+        assert th.is_alive()            # blocked in the superstep-1 allgather
+        lb.abort()
+        th.join(timeout=60)
+        assert not th.is_alive() and err and "loopback" in str(err[0])
+    finally:
+        _close(lb, ranks)

@@ -108,3 +108,38 @@ def test_ingest_from_reference_parquet(golden):
     ids, s, d = gfa.ingest.dense_edges(v, e)
     assert np.array_equal(ids, golden["ids"]) and np.array_equal(s, golden["src"])
     assert np.array_equal(d, golden["dst"])
+
+
+def test_loopback_group_host_side():
+    """The loopback group is host state only: it is created and aborted without a GPU,
+    and a handle on it checks the device like any other."""
+    lb = gfa.Loopback(3)
+    assert lb.nranks == 3
+    lib = _lib.load()
+    assert lib.lpa_loopback_create(0, None) == _lib.LPA_EINVAL
+    import torch
+
+    if not torch.cuda.is_available():
+        with pytest.raises(_lib.LpaError, match="device"):
+            gfa.Graph(np.array([0], np.int32), np.array([1], np.int32), 2, rank=1, loopback=lb)
+    lb.abort()
+    lb.close()
+    lb.close()   # idempotent
+
+
+def test_run_ranks_reraises_and_aborts():
+    class _G:
+        def __init__(self, lb):
+            self._loopback = lb
+
+    class _LB:
+        aborted = 0
+
+        def abort(self):
+            _LB.aborted += 1
+
+    lb = _LB()
+    with pytest.raises(RuntimeError, match="rank 1"):
+        gfa.run_ranks([_G(lb), _G(lb)], lambda r, g: (_ for _ in ()).throw(RuntimeError("rank 1")) if r else r)
+    assert _LB.aborted == 1
+    assert gfa.run_ranks([_G(lb), _G(lb)], lambda r, g: r * 10) == [0, 10]
