@@ -1132,15 +1132,17 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     int32_t* Ln = g->lab[g->cur ^ 1];
     int32_t* Lown = Ln + g->own_begin;
     const bool tt = timed && t < nt;
-    hipEvent_t* bev = tt ? &g->bin_ev[t * kBinEvents] : nullptr;
+    // per-kernel events only in the serialized profiling schedule (lpa_set_serial):
+    // there they give standalone kernel times; the concurrent schedule is timed per
+    // superstep only, so a timed converged superstep still replays its graph
+    hipEvent_t* bev = (tt && g->serial) ? &g->bin_ev[t * kBinEvents] : nullptr;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
     const bool diff_in_tally = g->nranks == 1 && !g->serial;
     // converged supersteps on one GPU replay a captured HIP graph of the whole
     // superstep (tally on four streams + diff + refresh; ~25 kernels and the
     // fork/join events): one launch instead of ~40 queue operations.  The graph bakes
     // the label / counter buffers, so there is one per (cur, par) state.
-    if (g->use_graphs && g->nranks == 1 && !tt && !g->serial &&
-        g->since_reset >= kDenseSupersteps) {
+    if (g->use_graphs && g->nranks == 1 && !g->serial && g->since_reset >= kDenseSupersteps) {
       const int key = g->cur * 2 + g->par;
       if (!g->gexec[key]) {
         hipGraph_t graph = nullptr;
@@ -1155,25 +1157,24 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
         LPA_HIP(ec);
       }
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
+      if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
       g->cur ^= 1;
       g->par ^= 1;
       ++g->since_reset;
       continue;
     }
     LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
-    if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
+    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
     bool changes_listed = false;
     if (g->nranks > 1 && has_collective(g))
       LPA_TRY(exchange_collective(g, Lc, Ln, g->since_reset < kDenseSupersteps, &changes_listed));
-    if (tt) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
+    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
     // P > 1 without a communicator: the caller completes the superstep with
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
     // (changes + refresh); a refresh here would see a partial vector
     if (g->nranks == 1 || has_collective(g)) LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed));
-    if (tt) {
-      LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));
-      LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
-    }
+    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));
+    if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     g->cur ^= 1;
     g->par ^= 1;
     ++g->since_reset;
@@ -1196,6 +1197,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     st->n_iter_ms = nt;
     for (int t = 0; t < nt; ++t) {
       LPA_HIP(hipEventElapsedTime(&st->iter_ms[t], g->ev[2 * t], g->ev[2 * t + 1]));
+      if (!g->serial) continue;  // per-kernel times: serialized schedule only
       hipEvent_t* bev = &g->bin_ev[t * kBinEvents];
       float ms;
       for (int k = 0; k < LPA_NKERNELS - 1; ++k) {

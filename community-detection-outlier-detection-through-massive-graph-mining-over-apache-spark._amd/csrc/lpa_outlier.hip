@@ -35,39 +35,85 @@ inline unsigned grid_for(int64_t n) {
 
 #define GRID_STRIDE(i, n) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+// uniform variant: every lane of a wave runs every trip (wave-level ballots inside);
+// `act` says whether this lane holds an element
+#define GRID_STRIDE_UNIFORM_BEGIN(i, act, n)                                         \
+  for (int64_t i##_b = (int64_t)blockIdx.x * blockDim.x; i##_b < (n);                \
+       i##_b += (int64_t)gridDim.x * blockDim.x) {                                   \
+    const int64_t i = i##_b + threadIdx.x;                                           \
+    const bool act = i < (n);
+
+// Wave-aggregated histogram increment (all 64 lanes call it; lanes with act add 1
+// to hist[key]).  Communities are heavily skewed -- a converged R-MAT labelling
+// puts most vertices in one community -- so a plain atomicAdd per element
+// serialises on a few addresses; here each round the first pending lane's key is
+// counted for the whole wave with one ballot and added by one atomic, and only
+// the lanes still pending after kAggRounds rounds add individually.
+constexpr int kAggRounds = 4;
+__device__ __forceinline__ void hist_inc(int32_t* __restrict__ hist, bool act, u32 key, int lane) {
+  bool mine = act;
+#pragma unroll
+  for (int r = 0; r < kAggRounds; ++r) {
+    const u64 pend = __ballot(mine);
+    if (pend == 0ull) return;  // uniform
+    const int lead = __ffsll((unsigned long long)pend) - 1;
+    const u32 k = (u32)__builtin_amdgcn_readlane((int)key, lead);
+    const bool eq = mine && key == k;
+    const u64 em = __ballot(eq);
+    if (lane == lead) atomicAdd(&hist[k], (int32_t)__popcll(em));
+    if (eq) mine = false;
+  }
+  if (mine) atomicAdd(&hist[key], 1);
+}
 
 __global__ void k_edge_keys(const int32_t* __restrict__ s, const int32_t* __restrict__ d, int64_t m,
                             u64* __restrict__ k) {
   GRID_STRIDE(e, m) k[e] = ((u64)(u32)s[e] << 32) | (u32)d[e];
 }
 
-// compact the distinct keys of a sorted array (first occurrence kept)
+// first occurrence of each key of a sorted array (the distinct directed edges)
 __global__ void k_mark_first(const u64* __restrict__ k, int64_t n, int32_t* __restrict__ mark) {
   GRID_STRIDE(i, n) mark[i] = (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
 }
 
-__global__ void k_scatter_marked(const u64* __restrict__ k, const int32_t* __restrict__ mark,
-                                 const int64_t* __restrict__ pos, int64_t n, u64* __restrict__ out) {
-  GRID_STRIDE(i, n) if (mark[i]) out[pos[i]] = k[i];
+// size[l] = members of community l; labels outside [0, V) are counted in *bad and
+// skipped (reported after the final sync instead of a host round trip up front)
+__global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ lab, int64_t V,
+                                                   int32_t* __restrict__ hist,
+                                                   unsigned long long* __restrict__ bad) {
+  const int lane = threadIdx.x & 63;
+  GRID_STRIDE_UNIFORM_BEGIN(v, act, V)
+    u32 l = act ? (u32)lab[v] : 0u;
+    const bool oob = act && l >= (u32)V;
+    if (oob) atomicAdd(bad, 1ull);
+    hist_inc(hist, act && !oob, l, lane);
+  }
 }
 
-__global__ void k_histogram(const int32_t* __restrict__ lab, int64_t V, int32_t* __restrict__ hist) {
-  GRID_STRIDE(v, V) atomicAdd(&hist[lab[v]], 1);
-}
-
-__global__ void k_incident(const u64* __restrict__ ek, int64_t n, const int32_t* __restrict__ L,
-                           int32_t* __restrict__ inc) {
-  GRID_STRIDE(i, n) {
-    const int32_t ls = L[(int32_t)(ek[i] >> 32)], ld = L[(int32_t)(u32)ek[i]];
-    atomicAdd(&inc[ls], 1);
-    if (ld != ls) atomicAdd(&inc[ld], 1);
+// incident distinct edges per community, over the sorted edge keys (distinct =
+// first occurrences): +1 for L[s], +1 for L[d] when it differs
+__global__ __launch_bounds__(256) void k_incident(const u64* __restrict__ ek, const int32_t* __restrict__ first,
+                                                  int64_t n, const int32_t* __restrict__ L, int64_t nv,
+                                                  int32_t* __restrict__ inc) {
+  const int lane = threadIdx.x & 63;
+  GRID_STRIDE_UNIFORM_BEGIN(i, act, n)
+    bool a = act && first[i];
+    u32 ls = 0u, ld = 0u;
+    if (a) {
+      const u64 k = ek[i];
+      ls = (u32)L[(int32_t)(k >> 32)];
+      ld = (u32)L[(int32_t)(u32)k];
+    }
+    const u32 V = (u32)nv;   // out-of-range labels (reported by k_histogram) are skipped
+    hist_inc(inc, a && ls < V, ls, lane);
+    hist_inc(inc, a && ld != ls && ld < V, ld, lane);
   }
 }
 
 // E' edges: distinct keys whose endpoints share a label
-__global__ void k_mark_intra(const u64* __restrict__ ek, int64_t n, const int32_t* __restrict__ L,
-                             int32_t* __restrict__ mark) {
-  GRID_STRIDE(i, n) mark[i] = L[(int32_t)(ek[i] >> 32)] == L[(int32_t)(u32)ek[i]] ? 1 : 0;
+__global__ void k_mark_intra(const u64* __restrict__ ek, const int32_t* __restrict__ first, int64_t n,
+                             const int32_t* __restrict__ L, int32_t* __restrict__ mark) {
+  GRID_STRIDE(i, n) mark[i] = (first[i] && L[(int32_t)(ek[i] >> 32)] == L[(int32_t)(u32)ek[i]]) ? 1 : 0;
 }
 
 __global__ void k_split_marked(const u64* __restrict__ ek, const int32_t* __restrict__ mark,
@@ -79,59 +125,68 @@ __global__ void k_split_marked(const u64* __restrict__ ek, const int32_t* __rest
   }
 }
 
-// group keys (segment << 32 | size) for every label l with size[l] > 0
-__global__ void k_group_flags(const int32_t* __restrict__ size, int64_t V, int32_t* __restrict__ mark) {
-  GRID_STRIDE(l, V) mark[l] = size[l] > 0 ? 1 : 0;
-}
-
+// group keys (segment << 32 | size) for every label l: size[l] > 0 -> a group of
+// segment seg_of[l] (nullptr: one segment); size 0 -> the sentinel segment nseg,
+// which the sort moves behind every group (no compaction, no host count)
 __global__ void k_group_keys(const int32_t* __restrict__ size, const int32_t* __restrict__ seg_of,
-                             const int32_t* __restrict__ mark, const int64_t* __restrict__ pos,
-                             int64_t V, u64* __restrict__ keys) {
-  GRID_STRIDE(l, V) if (mark[l]) {
-    const u32 sg = seg_of ? (u32)seg_of[l] : 0u;
-    keys[pos[l]] = ((u64)sg << 32) | (u32)size[l];
+                             int64_t V, u32 nseg, u64* __restrict__ keys) {
+  GRID_STRIDE(l, V) {
+    u32 sg = size[l] > 0 ? (seg_of ? (u32)seg_of[l] : 0u) : nseg;
+    if (sg > nseg) sg = nseg;   // out-of-range community label (reported separately)
+    keys[l] = ((u64)sg << 32) | (u32)size[l];
   }
 }
 
 // per segment: first / last index in the sorted group keys
-__global__ void k_seg_bounds(const u64* __restrict__ keys, int64_t n, int32_t* __restrict__ first,
-                             int32_t* __restrict__ last) {
+__global__ void k_seg_bounds(const u64* __restrict__ keys, int64_t n, u32 nseg, int32_t* __restrict__ first,
+                             int32_t* __restrict__ last, unsigned long long* __restrict__ ngroups) {
   GRID_STRIDE(i, n) {
     const u32 sg = (u32)(keys[i] >> 32);
+    if (sg == nseg) continue;
     if (i == 0 || (u32)(keys[i - 1] >> 32) != sg) first[sg] = (int32_t)i;
-    if (i == n - 1 || (u32)(keys[i + 1] >> 32) != sg) last[sg] = (int32_t)i;
+    if (i == n - 1 || (u32)(keys[i + 1] >> 32) != sg) {
+      last[sg] = (int32_t)i;
+      if (i == n - 1 || (u32)(keys[i + 1] >> 32) == nseg) *ngroups = (unsigned long long)(i + 1);
+    }
   }
 }
 
-// threshold per segment present in the keys
-__global__ void k_seg_threshold(const u64* __restrict__ keys, int64_t n, const int32_t* __restrict__ first,
-                                const int32_t* __restrict__ last, int32_t* __restrict__ thr,
-                                int32_t* __restrict__ ngroups) {
+// threshold per segment present in the keys (App. B a13: the k-th smallest size,
+// k = groups / 10, or the largest when k == 0)
+__global__ void k_seg_threshold(const u64* __restrict__ keys, int64_t n, u32 nseg,
+                                const int32_t* __restrict__ first, const int32_t* __restrict__ last,
+                                int32_t* __restrict__ thr) {
   GRID_STRIDE(i, n) {
     const u32 sg = (u32)(keys[i] >> 32);
-    if (first[sg] != (int32_t)i) continue;
+    if (sg == nseg || first[sg] != (int32_t)i) continue;
     const int64_t cnt = (int64_t)last[sg] - first[sg] + 1;
     const int64_t k = cnt / 10;
     const int64_t at = k > 0 ? first[sg] + k - 1 : last[sg];
     thr[sg] = (int32_t)(u32)keys[at];
-    ngroups[sg] = (int32_t)cnt;
   }
 }
 
-// flags[v] = size(group of v) < thr(segment of v); counts
-__global__ void k_flag(const int32_t* __restrict__ group_of, const int32_t* __restrict__ size,
-                       const int32_t* __restrict__ seg_of_v, const int32_t* __restrict__ thr,
-                       int64_t V, uint8_t* __restrict__ flags, int32_t* __restrict__ seg_flagged,
-                       unsigned long long* __restrict__ nflag) {
-  GRID_STRIDE(v, V) {
-    const int32_t gph = group_of[v];
-    const u32 sg = seg_of_v ? (u32)seg_of_v[v] : 0u;
-    const uint8_t f = size[gph] < thr[sg] ? 1 : 0;
-    flags[v] = f;
-    if (f) {
-      atomicAdd(nflag, 1ull);
-      seg_flagged[sg] = 1;
+// flags[v] = size(group of v) < thr(segment of v); flagged count (one atomic per wave)
+__global__ __launch_bounds__(256) void k_flag(const int32_t* __restrict__ group_of,
+                                              const int32_t* __restrict__ size,
+                                              const int32_t* __restrict__ seg_of_v,
+                                              const int32_t* __restrict__ thr, int64_t V,
+                                              uint8_t* __restrict__ flags, int32_t* __restrict__ seg_flagged,
+                                              unsigned long long* __restrict__ nflag) {
+  const int lane = threadIdx.x & 63;
+  GRID_STRIDE_UNIFORM_BEGIN(v, act, V)
+    uint8_t f = 0;
+    if (act) {
+      const u32 gph = (u32)group_of[v];
+      const u32 sg = seg_of_v ? (u32)seg_of_v[v] : 0u;
+      if (gph < (u32)V && sg < (u32)V) {   // else: a bad label, reported by k_histogram
+        f = size[gph] < thr[sg] ? 1 : 0;
+        if (f) seg_flagged[sg] = 1;
+      }
+      flags[v] = f;
     }
+    const u64 fm = __ballot(f != 0);
+    if (lane == 0 && fm) atomicAdd(nflag, (unsigned long long)__popcll(fm));
   }
 }
 
@@ -140,10 +195,6 @@ __global__ void k_count_nonzero(const int32_t* __restrict__ a, int64_t n, unsign
   GRID_STRIDE(i, n) c += a[i] != 0;
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
-}
-
-__global__ void k_check_range(const int32_t* __restrict__ a, int64_t n, unsigned long long* bad) {
-  GRID_STRIDE(i, n) if ((u32)a[i] >= (u32)n) atomicAdd(bad, 1ull);
 }
 
 __global__ void k_widen(const int32_t* __restrict__ a, int64_t n, int64_t* __restrict__ out) {
@@ -170,14 +221,6 @@ struct Scratch {
   }
 };
 
-// stable compaction helper: mark -> positions (exclusive scan) -> count
-int compact_positions(const int32_t* mark, int64_t n, int64_t* pos, int64_t* total, hipStream_t s) {
-  LPA_TRY(exclusive_scan_i32_i64(mark, pos, n, s));
-  LPA_HIP(hipMemcpyAsync(total, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  LPA_HIP(hipStreamSynchronize(s));
-  return LPA_OK;
-}
-
 int sort_keys(u64* keys, u64* tmp, int64_t n, int bits_lo, int bits_hi, hipStream_t s) {
   int shifts[16], ns = 0;
   for (int b = 0; b < bits_lo; b += 8) shifts[ns++] = b;
@@ -185,70 +228,55 @@ int sort_keys(u64* keys, u64* tmp, int64_t n, int bits_lo, int bits_hi, hipStrea
   return radix_sort_u64(keys, tmp, n, shifts, ns, s);
 }
 
-// distinct directed edges of the handle as sorted (s << 32 | d) keys
-int distinct_edges(lpa_graph* g, Scratch& sc, u64** out, int64_t* nd) {
+// the handle's edges as sorted (s << 32 | d) keys plus first-occurrence marks
+// (distinct directed edges = the marked keys; their count = sum of the marks)
+int sorted_edges(lpa_graph* g, Scratch& sc, u64** keys, int32_t** first) {
   hipStream_t s = g->stream;
   const int64_t m = g->m;
-  u64* k = nullptr;
-  int32_t* mark = nullptr;
-  int64_t* pos = nullptr;
-  u64* dk = nullptr;
-  LPA_TRY(sc.get(&k, 2 * m));
-  LPA_TRY(sc.get(&mark, m));
-  LPA_TRY(sc.get(&pos, m + 1));
+  LPA_TRY(sc.get(keys, 2 * m));
+  LPA_TRY(sc.get(first, m));
   if (m > 0) {
-    hipLaunchKernelGGL(k_edge_keys, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, k);
+    hipLaunchKernelGGL(k_edge_keys, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, *keys);
     LPA_HIP(hipGetLastError());
     const int b = bits_for((uint64_t)(g->V > 0 ? g->V - 1 : 0));
-    LPA_TRY(sort_keys(k, k + m, m, b, b, s));
-    hipLaunchKernelGGL(k_mark_first, dim3(grid_for(m)), dim3(256), 0, s, k, m, mark);
+    LPA_TRY(sort_keys(*keys, *keys + m, m, b, b, s));
+    hipLaunchKernelGGL(k_mark_first, dim3(grid_for(m)), dim3(256), 0, s, *keys, m, *first);
     LPA_HIP(hipGetLastError());
   }
-  LPA_TRY(compact_positions(mark, m, pos, nd, s));
-  LPA_TRY(sc.get(&dk, *nd));
-  if (m > 0) {
-    hipLaunchKernelGGL(k_scatter_marked, dim3(grid_for(m)), dim3(256), 0, s, k, mark, pos, m, dk);
-    LPA_HIP(hipGetLastError());
-  }
-  *out = dk;
   return LPA_OK;
 }
 
 // groups = labels l with size[l] > 0, segment seg_of[l] (nullptr: one segment).
-// Returns per-segment thresholds (thr[V]) and group counts (ngroups[V]).
+// Per-segment thresholds into thr[]; the group count lands in *ngroups (device).
+// No host round trip: empty labels sort behind the groups as a sentinel segment.
 int segmented_threshold(lpa_graph* g, Scratch& sc, const int32_t* size, const int32_t* seg_of,
-                        int64_t V, int32_t* thr, int32_t* ngroups, int64_t* n_groups_total) {
+                        int64_t V, int32_t* thr, unsigned long long* ngroups) {
   hipStream_t s = g->stream;
-  int32_t* mark = nullptr;
-  int64_t* pos = nullptr;
-  LPA_TRY(sc.get(&mark, V));
-  LPA_TRY(sc.get(&pos, V + 1));
-  hipLaunchKernelGGL(k_group_flags, dim3(grid_for(V)), dim3(256), 0, s, size, V, mark);
-  LPA_HIP(hipGetLastError());
-  int64_t ng = 0;
-  LPA_TRY(compact_positions(mark, V, pos, &ng, s));
-  *n_groups_total = ng;
-  if (ng == 0) return LPA_OK;
   u64* keys = nullptr;
   int32_t *first = nullptr, *last = nullptr;
-  LPA_TRY(sc.get(&keys, 2 * ng));
-  LPA_TRY(sc.get(&first, V));
-  LPA_TRY(sc.get(&last, V));
-  hipLaunchKernelGGL(k_group_keys, dim3(grid_for(V)), dim3(256), 0, s, size, seg_of, mark, pos, V,
-                     keys);
+  LPA_TRY(sc.get(&keys, 2 * V));
+  LPA_TRY(sc.get(&first, V + 1));
+  LPA_TRY(sc.get(&last, V + 1));
+  const u32 nseg = seg_of ? (u32)V : 1u;
+  hipLaunchKernelGGL(k_group_keys, dim3(grid_for(V)), dim3(256), 0, s, size, seg_of, V, nseg, keys);
   LPA_HIP(hipGetLastError());
-  const int b = bits_for((uint64_t)(V > 0 ? V : 0));
-  LPA_TRY(sort_keys(keys, keys + ng, ng, b, seg_of ? b : 0, s));
-  hipLaunchKernelGGL(k_seg_bounds, dim3(grid_for(ng)), dim3(256), 0, s, keys, ng, first, last);
+  LPA_TRY(sort_keys(keys, keys + V, V, bits_for((uint64_t)V), bits_for((uint64_t)nseg), s));
+  hipLaunchKernelGGL(k_seg_bounds, dim3(grid_for(V)), dim3(256), 0, s, keys, V, nseg, first, last, ngroups);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_seg_threshold, dim3(grid_for(ng)), dim3(256), 0, s, keys, ng, first, last,
-                     thr, ngroups);
+  hipLaunchKernelGGL(k_seg_threshold, dim3(grid_for(V)), dim3(256), 0, s, keys, V, nseg, first, last, thr);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
 
+int bad_labels(unsigned long long n, int64_t V) {
+  set_error("outlier: %llu labels outside [0, V=%lld)", n, (long long)V);
+  return LPA_EINVAL;
+}
+
 }  // namespace
 
+// Host round trips: none in L1 before the results are copied out; one in L2 (the
+// size of E', which the second LPA's graph build needs).
 int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
             int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
             uint8_t* flags, lpa_outlier_summary* summary) {
@@ -261,23 +289,23 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     return LPA_EINVAL;
   }
   hipStream_t s = g->stream;
-  const int64_t V = g->V;
+  const int64_t V = g->V, m = g->m;
   Scratch sc(s);
   lpa_outlier_summary sum = {};
-  int32_t *L = nullptr, *size = nullptr, *inc = nullptr, *thr = nullptr, *ngr = nullptr,
-          *segflag = nullptr;
+  int32_t *L = nullptr, *size = nullptr, *inc = nullptr, *thr = nullptr, *segflag = nullptr;
   uint8_t* fl = nullptr;
   int64_t* wide = nullptr;
+  // cnt: 0 communities, 1 flagged, 2 communities flagged, 3 bad labels, 4 groups,
+  //      5 distinct edges
   unsigned long long* cnt = nullptr;
   LPA_TRY(sc.get(&L, V));
   LPA_TRY(sc.get(&size, V));
   LPA_TRY(sc.get(&inc, V));
-  LPA_TRY(sc.get(&thr, V));
-  LPA_TRY(sc.get(&ngr, V));
+  LPA_TRY(sc.get(&thr, V + 1));
   LPA_TRY(sc.get(&segflag, V));
   LPA_TRY(sc.get(&fl, V));
   LPA_TRY(sc.get(&wide, V));
-  LPA_TRY(sc.get(&cnt, 4));
+  LPA_TRY(sc.get(&cnt, 8));
   if (V == 0) {
     if (summary) *summary = sum;
     return LPA_OK;
@@ -287,73 +315,70 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
   LPA_HIP(hipMemsetAsync(size, 0, sizeof(int32_t) * V, s));
   LPA_HIP(hipMemsetAsync(inc, 0, sizeof(int32_t) * V, s));
   LPA_HIP(hipMemsetAsync(segflag, 0, sizeof(int32_t) * V, s));
-  LPA_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 4, s));
+  LPA_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 8, s));
 
-  // labels must be dense ids: a label outside [0, V) would index out of bounds
-  hipLaunchKernelGGL(k_check_range, dim3(grid_for(V)), dim3(256), 0, s, L, V, cnt + 3);
-  LPA_HIP(hipGetLastError());
-  {
-    unsigned long long bad = 0;
-    LPA_HIP(hipMemcpyAsync(&bad, cnt + 3, sizeof(bad), hipMemcpyDeviceToHost, s));
-    LPA_HIP(hipStreamSynchronize(s));
-    if (bad) {
-      set_error("outlier: %llu labels outside [0, V=%lld)", bad, (long long)V);
-      return LPA_EINVAL;
-    }
-  }
-  hipLaunchKernelGGL(k_histogram, dim3(grid_for(V)), dim3(256), 0, s, L, V, size);
+  hipLaunchKernelGGL(k_histogram, dim3(grid_for(V)), dim3(256), 0, s, L, V, size, cnt + 3);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(V)), dim3(256), 0, s, size, V, cnt);
   LPA_HIP(hipGetLastError());
 
   u64* ek = nullptr;
-  int64_t nd = 0;
-  LPA_TRY(distinct_edges(g, sc, &ek, &nd));
-  sum.distinct_edges = nd;
-  if (nd > 0) {
-    hipLaunchKernelGGL(k_incident, dim3(grid_for(nd)), dim3(256), 0, s, ek, nd, L, inc);
+  int32_t* first = nullptr;
+  LPA_TRY(sorted_edges(g, sc, &ek, &first));
+  if (m > 0) {
+    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(m)), dim3(256), 0, s, first, m, cnt + 5);
+    LPA_HIP(hipGetLastError());
+  }
+
+  if (m > 0) {
+    hipLaunchKernelGGL(k_incident, dim3(grid_for(m)), dim3(256), 0, s, ek, first, m, L, V, inc);
     LPA_HIP(hipGetLastError());
   }
 
   if (mode == 1) {
-    int64_t ng = 0;
-    LPA_TRY(segmented_threshold(g, sc, size, nullptr, V, thr, ngr, &ng));
+    LPA_TRY(segmented_threshold(g, sc, size, nullptr, V, thr, cnt + 4));
     hipLaunchKernelGGL(k_flag, dim3(grid_for(V)), dim3(256), 0, s, L, size, (const int32_t*)nullptr,
                        thr, V, fl, segflag, cnt + 1);
     LPA_HIP(hipGetLastError());
     int32_t h_thr = 0;
     LPA_HIP(hipMemcpyAsync(&h_thr, thr, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    unsigned long long h_cnt[4];
+    unsigned long long h_cnt[8];
     LPA_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
-    sum.n_groups = ng;
-    sum.k = ng / 10;
+    if (h_cnt[3]) return bad_labels(h_cnt[3], V);
+    sum.n_groups = (int64_t)h_cnt[4];
+    sum.k = sum.n_groups / 10;
     sum.threshold = h_thr;
     sum.n_flagged = (int64_t)h_cnt[1];
     sum.n_communities = (int64_t)h_cnt[0];
     sum.n_communities_flagged = sum.n_flagged > 0 ? 1 : 0;
+    sum.distinct_edges = (int64_t)h_cnt[5];
   } else {
-    // E' = distinct intra-community edges
+    // E' = distinct intra-community edges (compacted: the second LPA builds on it)
     int32_t* mark = nullptr;
     int64_t* pos = nullptr;
     int32_t *s2 = nullptr, *d2 = nullptr, *sub = nullptr, *subsize = nullptr;
-    LPA_TRY(sc.get(&mark, nd));
-    LPA_TRY(sc.get(&pos, nd + 1));
-    if (nd > 0) {
-      hipLaunchKernelGGL(k_mark_intra, dim3(grid_for(nd)), dim3(256), 0, s, ek, nd, L, mark);
+    LPA_TRY(sc.get(&mark, m));
+    LPA_TRY(sc.get(&pos, m + 1));
+    if (m > 0) {
+      hipLaunchKernelGGL(k_mark_intra, dim3(grid_for(m)), dim3(256), 0, s, ek, first, m, L, mark);
       LPA_HIP(hipGetLastError());
     }
+    LPA_TRY(exclusive_scan_i32_i64(mark, pos, m, s));
     int64_t m2 = 0;
-    LPA_TRY(compact_positions(mark, nd, pos, &m2, s));
+    unsigned long long nbad = 0;
+    LPA_HIP(hipMemcpyAsync(&m2, pos + m, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipMemcpyAsync(&nbad, cnt + 3, sizeof(nbad), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));   // the one round trip: E' size for the build
+    if (nbad) return bad_labels(nbad, V);
     LPA_TRY(sc.get(&s2, m2));
     LPA_TRY(sc.get(&d2, m2));
     LPA_TRY(sc.get(&sub, V));
     LPA_TRY(sc.get(&subsize, V));
-    if (nd > 0) {
-      hipLaunchKernelGGL(k_split_marked, dim3(grid_for(nd)), dim3(256), 0, s, ek, mark, pos, nd, s2, d2);
+    if (m > 0) {
+      hipLaunchKernelGGL(k_split_marked, dim3(grid_for(m)), dim3(256), 0, s, ek, mark, pos, m, s2, d2);
       LPA_HIP(hipGetLastError());
     }
-    LPA_HIP(hipStreamSynchronize(s));
     // second LPA on the induced simple subgraph (same device, same stream)
     lpa_graph* h = nullptr;
     LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE, &h));
@@ -363,26 +388,26 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     destroy(h);
     if (rc != LPA_OK) return rc;
     LPA_HIP(hipMemsetAsync(subsize, 0, sizeof(int32_t) * V, s));
-    hipLaunchKernelGGL(k_histogram, dim3(grid_for(V)), dim3(256), 0, s, sub, V, subsize);
+    hipLaunchKernelGGL(k_histogram, dim3(grid_for(V)), dim3(256), 0, s, sub, V, subsize, cnt + 3);
     LPA_HIP(hipGetLastError());
     // segment of a sub-label group = the community of the sub-label vertex: L itself
-    int64_t ng = 0;
-    LPA_TRY(segmented_threshold(g, sc, subsize, L, V, thr, ngr, &ng));
+    LPA_TRY(segmented_threshold(g, sc, subsize, L, V, thr, cnt + 4));
     hipLaunchKernelGGL(k_flag, dim3(grid_for(V)), dim3(256), 0, s, sub, subsize, L, thr, V, fl,
                        segflag, cnt + 1);
     LPA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(V)), dim3(256), 0, s, segflag, V, cnt + 2);
     LPA_HIP(hipGetLastError());
-    unsigned long long h_cnt[4];
+    unsigned long long h_cnt[8];
     LPA_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
     if (sub_labels) LPA_HIP(hipMemcpyAsync(sub_labels, sub, sizeof(int32_t) * V, hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
-    sum.n_groups = ng;
+    sum.n_groups = (int64_t)h_cnt[4];
     sum.k = -1;
     sum.threshold = -1;
     sum.n_flagged = (int64_t)h_cnt[1];
     sum.n_communities = (int64_t)h_cnt[0];
     sum.n_communities_flagged = (int64_t)h_cnt[2];
+    sum.distinct_edges = (int64_t)h_cnt[5];
   }
 
   if (size_hist) {

@@ -129,11 +129,18 @@ class Graph:
         _lib.check(self._lib.lpa_get_labels(self._handle(), lab.ctypes.data, 0))
         return lab
 
-    def run(self, max_iter: int, stats: bool = False):
-        """labelPropagation(maxIter): reset, exactly max_iter supersteps, labels."""
-        lab = np.empty(self.num_vertices, dtype=np.int32)
+    def run(self, max_iter: int, stats: bool = False, out=None):
+        """labelPropagation(maxIter): reset, exactly max_iter supersteps, labels
+        (host int32 array, or written into the device tensor ``out``)."""
         st = _lib.LpaStats() if stats else None
-        _lib.check(self._lib.lpa_run(self._handle(), int(max_iter), lab.ctypes.data, 0,
+        if out is not None and _is_device_tensor(out):
+            if out.numel() != self.num_vertices:
+                raise ValueError(f"out must hold {self.num_vertices} labels")
+            lab, ptr, on_dev = out, out.data_ptr(), 1
+        else:
+            lab = np.empty(self.num_vertices, dtype=np.int32)
+            ptr, on_dev = lab.ctypes.data, 0
+        _lib.check(self._lib.lpa_run(self._handle(), int(max_iter), ptr, on_dev,
                                      ctypes.byref(st) if stats else None))
         return (lab, st.to_dict()) if stats else lab
 

@@ -46,13 +46,17 @@ extern "C" {
 
 typedef struct lpa_graph lpa_graph;
 
-/* Per-call timing, filled by lpa_step / lpa_run (HIP events on the handle's stream). */
+/* Per-call timing, filled by lpa_step / lpa_run (HIP events on the handle's stream).
+ * iter_ms: always (events around each superstep; converged single-GPU supersteps
+ * still replay their captured graph).  kernel_ms / exchange_ms: only on a handle in
+ * the serialized profiling schedule (lpa_set_serial(g, 1)), where events bracket
+ * every tally kernel so each time is that kernel's standalone duration. */
 typedef struct lpa_stats {
   int32_t iters;                           /* supersteps executed by this call          */
   int32_t n_iter_ms;                       /* entries filled in iter_ms                 */
   float iter_ms[LPA_STATS_MAX_ITERS];      /* device time per superstep (incl. exchange) */
-  float kernel_ms[LPA_NKERNELS];           /* summed device time per kernel (first 64)  */
-  float exchange_ms;                       /* summed RCCL allgather time                */
+  float kernel_ms[LPA_NKERNELS];           /* summed device time per kernel (serial)    */
+  float exchange_ms;                       /* summed label-exchange time (serial)       */
   double total_ms;                         /* device time of all supersteps of the call */
 } lpa_stats;
 

@@ -95,3 +95,25 @@ def test_c5_chunglu_full_maxiter10(gfa, oracle):
     del sn, dn
     bad = int((lab != ref).sum())
     assert bad == 0, f"C5 maxIter=10: {bad} labels differ"
+
+
+def test_c2_outlier_l1_l2_vs_oracle(gfa, oracle):
+    """Outlier stage (Graphframes.py:92-137) at config C2 size (SBM
+    1 M V / 20 M E, labels after maxIter=10): size / incident histograms, thresholds,
+    L2 sub-labels and flags identical to the oracle."""
+    V, B, m = 1_000_000, 100, 20_000_000
+    s, d = gfa.gen_sbm(V, B, m)
+    sn, dn = _host(s), _host(d)
+    with gfa.Graph(s, d, V) as g:
+        lab = g.run(10)
+        o1 = g.outlier(lab, "L1")
+        o2 = g.outlier(lab, "L2", sub_iter=5)
+    size, inc, flags, summ = oracle.outlier_l1(V, sn, dn, lab)
+    assert np.array_equal(o1["size"], size) and np.array_equal(o1["incident"], inc)
+    assert np.array_equal(o1["flags"], flags) and o1["summary"]["threshold"] == summ["thr"]
+    assert o1["summary"]["n_groups"] == summ["n_groups"] and o1["summary"]["n_flagged"] == summ["n_flagged"]
+    sub, flags2, summ2 = oracle.outlier_l2(V, sn, dn, lab, 5)
+    assert np.array_equal(o2["sub_labels"], sub) and np.array_equal(o2["flags"], flags2)
+    assert o2["summary"]["n_flagged"] == summ2["n_flagged"]
+    assert o2["summary"]["n_groups"] == summ2["n_subgroups"]
+    assert o2["summary"]["n_communities_flagged"] == summ2["n_communities_flagged"]

@@ -353,3 +353,47 @@ def test_dropin_integral_ids_and_dangling(gfa, oracle):
     res = gfa.outlier_scores(v, e, labels=out, mode="L1")
     assert res.communities["size"].tolist() == [5, 6]
     assert res.summary["threshold"] == 6 and res.flagged_ids.tolist() == ids[:5].tolist()
+
+
+def test_c1_end_to_end_from_parquet(gfa, golden, tmp_path):
+    """Config C1 through the reference's own pipeline shape (Graphframes.py:16-85 and
+    the intended :121-137): outlinks parquet (4 nullable string columns, one all-null
+    row) -> null filter -> SHA-1[:8] ids -> GraphFrame -> labelPropagation(maxIter=5)
+    -> distinct-label count -> outlier L1 / L2.  The parquet is rebuilt from the
+    committed R9 fixture (the reference data itself is not on the GPU box)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    names = golden["names"].astype(str)
+    pdom, cdom = names[golden["src"]].tolist(), names[golden["dst"]].tolist()
+    tbl = pa.table({"_c0": [f"http://{x}/" for x in pdom] + ['"'], "_c1": pdom + [None],
+                    "_c2": cdom + [None], "_c3": [f"http://{x}/" for x in cdom] + [None]})
+    pq.write_table(tbl, str(tmp_path / "part-00000-c000.snappy.parquet"), compression="snappy")
+    v, e = gfa.ingest.load_outlinks_graph(str(tmp_path))
+    assert len(e) == 18398 and len(v) == 4613                     # :18, :30 filter, :53
+    assert v["id"].tolist() == golden["ids"].tolist()             # NodeHash ids (:57-58)
+    gf = gfa.GraphFrame(v, e)                                     # :78
+    try:
+        out = gf.labelPropagation(maxIter=5)                      # :81
+        assert out["label"].nunique() == 619                      # :85
+        assert np.array_equal(out["label"].to_numpy(), golden["labels_iter"][4].astype(np.int64))
+        r1 = gf.outlierScores(labels=out, mode="L1")
+        assert r1.summary["n_flagged"] == 0 and r1.flagged_ids.size == 0
+        assert r1.communities["size"].sum() == 4613 and len(r1.communities) == 619   # :100-120
+        r2 = gf.outlierScores(labels=out, mode="L2", subIter=5)   # :121-137
+        assert r2.summary["n_flagged"] == 40
+        assert r2.flagged_ids.tolist() == golden["ids"][golden["l2_flags"].astype(bool)].tolist()
+    finally:
+        gf.close()
+
+
+def test_outlier_rejects_out_of_range_labels(gfa):
+    V, s, d = two_cliques()
+    with gfa.Graph(s, d, V) as g:
+        bad = np.zeros(V, np.int32)
+        bad[3] = V + 5
+        for mode in ("L1", "L2"):
+            with pytest.raises(ValueError, match="outside"):
+                g.outlier(bad, mode)
+        # the handle is still usable afterwards
+        assert g.outlier(g.run(20), "L1")["summary"]["n_communities"] == 2
