@@ -267,11 +267,15 @@ def main():
     # ---- breakdown: supersteps 2..10 again with the tally kernels serialized on one
     # stream and HIP events around every kernel (standalone durations: the roofline
     # of that kernel, not of its co-runners; not used for `value`) ----
+    # frontier off here: every row is tallied, so each kernel's time covers the
+    # bytes `kernel_bytes` counts (the frontier skips most rows once labels settle)
+    g.set_frontier(False)
     g.reset()
     g.step(1)
     g.set_serial(True)
     st = g.step(MAX_ITER - 1, stats=True)
     g.set_serial(False)
+    g.set_frontier(True)
     kms = st["kernel_ms"]
     dom = max((k for k in kms if kernel_bytes(info, k) is not None), key=lambda k: kms[k])
     dom_ms = kms[dom] / (MAX_ITER - 1)

@@ -92,6 +92,7 @@ SIGNATURES = {
                                              ctypes.c_int32, ctypes.c_char_p, ctypes.POINTER(_vp)]),
     "lpa_set_stream": (ctypes.c_int, [_vp, _vp]),
     "lpa_set_serial": (ctypes.c_int, [_vp, ctypes.c_int32]),
+    "lpa_set_frontier": (ctypes.c_int, [_vp, ctypes.c_int32]),
     "lpa_reset": (ctypes.c_int, [_vp]),
     "lpa_step": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(LpaStats)]),
     "lpa_get_labels": (ctypes.c_int, [_vp, _vp, ctypes.c_int32]),

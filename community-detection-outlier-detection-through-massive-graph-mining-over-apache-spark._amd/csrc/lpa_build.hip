@@ -163,10 +163,16 @@ __global__ void k_emit_arcs_owned(const int32_t* __restrict__ src, const int32_t
   }
 }
 
-__global__ void k_keys_to_col(const u64* __restrict__ keys, int64_t n, int32_t* __restrict__ col) {
+// sorted (row << 32 | col) keys -> col[] and the row of every arc position (crow[],
+// read by the al[] scatter to mark the rows its writes make dirty)
+__global__ void k_keys_to_col(const u64* __restrict__ keys, int64_t n, int32_t* __restrict__ col,
+                              int32_t* __restrict__ crow) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += (int64_t)gridDim.x * blockDim.x)
-    col[j] = (int32_t)(u32)keys[j];
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const u64 k = keys[j];
+    col[j] = (int32_t)(u32)k;
+    crow[j] = (int32_t)(k >> 32);
+  }
 }
 
 // CSC keys: (column << 32 | position), generated in position order so a stable
@@ -252,6 +258,13 @@ int init_labels(lpa_graph* g) {
                      g->vpad, g->lab[0], g->lab[1]);
   LPA_HIP(hipGetLastError());
   if (g->dev_err) LPA_HIP(hipMemsetAsync(g->dev_err, 0, sizeof(int32_t), g->stream));
+  // L0: every row is tallied in superstep 1; no stale dirty flags
+  for (int p = 0; p < 2; ++p) {
+    LPA_HIP(hipMemsetAsync(g->rdirty[p], 0, g->slice, g->stream));
+    LPA_HIP(hipMemsetAsync(g->udirty[p], 0, (g->n_segs + 16) / 16 * 16, g->stream));
+  }
+  LPA_HIP(hipMemsetD32Async((hipDeviceptr_t)g->fr_all, 1, 2, g->stream));
+  LPA_HIP(hipMemsetAsync(g->fcnt, 0, sizeof(int32_t) * 32, g->stream));
   g->cur = 0;
   g->since_reset = 0;
   g->prev_delta_ok = false;  // the exchange's delta chain restarts from L0
@@ -386,7 +399,8 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
-    hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col);
+    LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t) * arcs));
+    hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col, g->crow);
     LPA_HIP(hipGetLastError());
     // CSC position index over this rank's arcs (for the replicated-label refresh)
     if (arcs >= (int64_t)UINT32_MAX) {
@@ -476,6 +490,16 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
 
   LPA_TRY(dev_alloc(g, (void**)&g->dev_err, sizeof(int32_t)));
   LPA_HIP(hipMemsetAsync(g->dev_err, 0, sizeof(int32_t), s));
+  // frontier flags (cleared / set to "all rows" by init_labels)
+  for (int p = 0; p < 2; ++p) {
+    LPA_TRY(dev_alloc(g, (void**)&g->rdirty[p], S));   // S: a multiple of 64
+    LPA_TRY(dev_alloc(g, (void**)&g->udirty[p], (g->n_segs + 16) / 16 * 16));
+  }
+  LPA_TRY(dev_alloc(g, (void**)&g->fr_all, 2 * sizeof(int32_t)));
+  LPA_TRY(dev_alloc(g, (void**)&g->flist, sizeof(int32_t) * S));
+  LPA_TRY(dev_alloc(g, (void**)&g->ulist, sizeof(int32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->fcnt, sizeof(int32_t) * 32));
+  if (g->crow == nullptr) LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t)));
 
   // ---- labels (replicated, ping-pong) ----
   LPA_TRY(dev_alloc(g, (void**)&g->lab[0], sizeof(int32_t) * g->vpad));

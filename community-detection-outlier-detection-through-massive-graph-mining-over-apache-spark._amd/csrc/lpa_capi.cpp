@@ -60,7 +60,8 @@ void destroy(lpa_graph* g) {
                   g->segs, g->e_src,  g->e_dst, g->al,   g->cptr,  g->cpos,   g->chunks,
                   g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->items_cb,
-                  g->items_cc, g->hub_uoff, g->ucnt};
+                  g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
+                  g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
@@ -134,6 +135,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
   if (const char* f = getenv("LPA_HUB_WAVES")) g->hub_waves = atoi(f) == 4 ? 4 : 8;
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
+  if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {
@@ -261,6 +263,7 @@ int lpa_exchange_put(lpa_graph* g, const int32_t* full_in) {
                          g->stream));
   g->prev_delta_ok = false;
   LPA_TRY(rebuild_arc_labels(g));
+  LPA_TRY(frontier_all(g, g->par));
   LPA_HIP(hipStreamSynchronize(g->stream));
   return LPA_OK;
 }
@@ -315,6 +318,9 @@ int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t*
   int32_t* Ln = g->lab[g->cur];
   LPA_TRY(exchange_finish_delta(g, Lc, Ln, cap));
   LPA_TRY(launch_refresh_ext(g, Lc, Ln, true));
+  // this refresh runs outside the superstep's parity bookkeeping: the next superstep
+  // tallies every row instead of reading its flags
+  LPA_TRY(frontier_all(g, g->par));
   LPA_HIP(hipStreamSynchronize(s));
   return LPA_OK;
 }
@@ -325,6 +331,29 @@ int lpa_set_serial(lpa_graph* g, int32_t serial) {
     return LPA_EINVAL;
   }
   g->serial = serial ? 1 : 0;
+  return LPA_OK;
+}
+
+int lpa_set_frontier(lpa_graph* g, int32_t on) {
+  if (!g) {
+    set_error("null handle");
+    return LPA_EINVAL;
+  }
+  on = on ? 1 : 0;
+  if (on != g->frontier) {
+    LPA_HIP(hipSetDevice(g->device));
+    LPA_HIP(hipStreamSynchronize(g->stream));
+    // the flag is baked into the captured superstep graphs
+    for (auto& ge : g->gexec)
+      if (ge) {
+        (void)hipGraphExecDestroy(ge);
+        ge = nullptr;
+      }
+    g->frontier = on;
+    // the next superstep tallies every row either way (flags may be stale)
+    LPA_TRY(frontier_all(g, g->par));
+    LPA_HIP(hipStreamSynchronize(g->stream));
+  }
   return LPA_OK;
 }
 

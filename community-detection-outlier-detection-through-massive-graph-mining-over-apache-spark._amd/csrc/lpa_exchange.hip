@@ -88,13 +88,17 @@ __global__ void k_delta_apply(const u64* __restrict__ drecv, const unsigned long
 }
 
 // the gathered changes as al[] position chunks (u << 32 | k) + the dirty-arc count:
-// k_diff's output, from the change list instead of a scan of the whole vector
+// k_diff's output, from the change list instead of a scan of the whole vector.
+// Frontier (as k_diff): this rank's own changed labels are also copied into Lsync
+// (the current vector Lc, the next superstep's output), so an owned row the next
+// superstep skips already holds its label there.
 __global__ __launch_bounds__(256) void k_delta_chunks(const u64* __restrict__ drecv,
                                                       const unsigned long long* __restrict__ counts,
                                                       int64_t cap, int32_t P, int64_t slice,
                                                       const int64_t* __restrict__ cptr,
                                                       u64* __restrict__ chunks,
-                                                      unsigned long long* __restrict__ counters) {
+                                                      unsigned long long* __restrict__ counters,
+                                                      int32_t own, int32_t* __restrict__ Lsync) {
   const int lane = threadIdx.x & 63;
   const int64_t tot = cap * P;
   for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (int64_t)gridDim.x * blockDim.x) {
@@ -104,7 +108,9 @@ __global__ __launch_bounds__(256) void k_delta_chunks(const u64* __restrict__ dr
     if (k < tot) {
       const int64_t r = k / cap, j = k - r * cap;
       if (j < (int64_t)counts[r]) {
-        u = r * slice + (int64_t)(drecv[k] >> 32);
+        const u64 e = drecv[k];
+        u = r * slice + (int64_t)(e >> 32);
+        if (r == own) Lsync[u] = (int32_t)(uint32_t)e;
         cnt = cptr[u + 1] - cptr[u];
         nch = (int)((cnt + kChunkPos - 1) / kChunkPos);
       }
@@ -195,7 +201,7 @@ int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t 
     LPA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_delta_chunks, dim3(grid_of(cap * P, 4096)), dim3(256), 0, s,
                        exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->slice, g->cptr,
-                       g->chunks, g->counters + 4 * g->par);
+                       g->chunks, g->counters + 4 * g->par, g->rank, const_cast<int32_t*>(Lc));
     LPA_HIP(hipGetLastError());
   }
   g->prev_cap = cap;

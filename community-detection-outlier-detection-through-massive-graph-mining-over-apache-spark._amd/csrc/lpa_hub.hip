@@ -68,29 +68,6 @@ __device__ __forceinline__ RowUnits row_units(const int64_t* __restrict__ rp,
   return r;
 }
 
-// Per-lane insert of one word with a wave pre-combine: the first active label of
-// the wave's 64 words is summed in registers and inserted once.
-__device__ __forceinline__ void insert_word(u64 word, bool act, u64* tab, uint16_t* lst, int* lcount,
-                                            int lg, int lane, int32_t* err) {
-  const u64 am = __ballot(act);
-  if (am == 0ull) return;  // uniform over the wave
-  const u32 lab = ~(u32)word;
-  const int f = __ffsll((unsigned long long)am) - 1;
-  const u32 x = (u32)__builtin_amdgcn_readlane((int)lab, f);
-  const bool mt = act && lab == x;
-  const u32 c = wave_sum_u32(mt ? (u32)(word >> 32) : 0u);
-  u32 ilab = lab, icnt = (u32)(word >> 32);
-  bool ins = act && !mt;
-  if (lane == f) {
-    ins = true;
-    ilab = x;
-    icnt = c;
-  }
-  int slot = -1;
-  if (ins) slot = lds_insert_bounded(tab, 32 - lg, (1u << lg) - 1u, ilab, icnt, err);
-  list_append(lst, lcount, slot, lane);
-}
-
 // ---------------------------------------------------------------------------
 // rows of <= kLaneUnits units (deg <= 4096): one LANE per row.  A converged
 // row left one word per unit; the lane loads them and takes the mode of <= 8
@@ -119,12 +96,24 @@ __global__ __launch_bounds__(256) void k_hub_lanes(int64_t h_begin, int64_t h_en
                                                    int32_t* __restrict__ Ln,
                                                    int32_t* __restrict__ lists, int64_t n_hub,
                                                    int32_t* __restrict__ wcount,
-                                                   int32_t* __restrict__ lcnt) {
+                                                   int32_t* __restrict__ lcnt,
+                                                   const int32_t* __restrict__ flist,
+                                                   const int32_t* __restrict__ fcnt0,
+                                                   const int32_t* __restrict__ fr_all) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t h0 = h_begin + (int64_t)blockIdx.x * blockDim.x; h0 < h_end; h0 += stride) {
-    const int64_t h = h0 + threadIdx.x;
-    const bool live = h < h_end;
+  // frontier: only the listed dirty hub rows (bin 0 of k_frontier_lists; rows below
+  // h_begin are k_hub_small's), else every row of [h_begin, h_end)
+  const int all = *fr_all;
+  const int64_t n_items = all ? h_end - h_begin : (int64_t)*fcnt0;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n_items; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
+    int64_t h = 0;
+    bool live = false;
+    if (i < n_items) {
+      h = all ? h_begin + i : (int64_t)flist[i];
+      live = h >= h_begin;
+    }
     bool one = false;
     int T = 0;
     if (live) {
@@ -331,7 +320,10 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
                                                    int32_t* __restrict__ lists,
                                                    int32_t* __restrict__ lcnt,
                                                    u64* __restrict__ itemsCB,
-                                                   u64* __restrict__ itemsCC) {
+                                                   u64* __restrict__ itemsCC,
+                                                   const int32_t* __restrict__ flist,
+                                                   const int32_t* __restrict__ fcnt0,
+                                                   const int32_t* __restrict__ fr_all) {
   __shared__ u64 tab_all[4][kSmallSlots];
   // unit prefixes (< T <= kSmallWords), then the slot list (< kSmallSlots): both fit
   // 16 bits, so the block takes 36 KB of LDS and four blocks fit a CU
@@ -346,13 +338,17 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
   for (int i = lane; i < kSmallSlots; i += 64) tab[i] = 0ull;
   // rows: [0, nd) directly, then list S (pre-classified by k_hub_classify), then
   // list W (from k_hub_lanes)
+  // direct rows [0, nd): with the frontier, the listed dirty hub rows below nd
+  const int all = *fr_all;
+  const int64_t nd_items = (all || nd == 0) ? nd : (int64_t)*fcnt0;
   const int64_t nS = lcnt[7];
-  const int64_t nq = nd + nS + lcnt[4];
+  const int64_t nq = nd_items + nS + lcnt[4];
   const int64_t stride = (int64_t)gridDim.x * 4;
   for (int64_t q = (int64_t)blockIdx.x * 4 + w; q < nq; q += stride) {
-    const int64_t h = q < nd ? q
-                             : (q < nd + nS ? (int64_t)lists[5 * n_hub + (q - nd)]
-                                            : (int64_t)lists[2 * n_hub + (q - nd - nS)]);
+    const int64_t h = q < nd_items ? (all ? q : (int64_t)flist[q])
+                                   : (q < nd_items + nS ? (int64_t)lists[5 * n_hub + (q - nd_items)]
+                                                        : (int64_t)lists[2 * n_hub + (q - nd_items - nS)]);
+    if (h >= nd && q < nd_items) continue;  // a lane-path row (k_hub_lanes); uniform
     const RowUnits ru = row_units(rp, uoff, h);
     const int nu = ru.nu;
     const int32_t* uc = ucnt + ru.u0;
@@ -826,9 +822,12 @@ __global__ __launch_bounds__(64 * kW) void k_hub_bucket(const u64* __restrict__ 
                                                     int32_t* __restrict__ err) {
   __shared__ u64 tab[kCombSlots];
   __shared__ u64 redw[kW];
+  __shared__ int32_t ovf;  // a pass whose distinct labels overflowed the table
   const int n = lcnt[2];
   if ((int)blockIdx.x >= n) return;
   for (int i = threadIdx.x; i < kCombSlots; i += 64 * kW) tab[i] = 0ull;
+  if (threadIdx.x == 0) ovf = 0;
+  __syncthreads();
   for (int it = blockIdx.x; it < n; it += gridDim.x) {
     const u64 item = itemsCB[it];
     const int64_t h = (int64_t)(item >> 32);
@@ -839,9 +838,32 @@ __global__ __launch_bounds__(64 * kW) void k_hub_bucket(const u64* __restrict__ 
     // a bucket far above its expected load is tallied in sub-bucket passes
     const int lgJ = cnt > kCombDirect ? ceil_log2((u32)((cnt + 4095) / 4096)) : 0;
     u64 best = 0ull;
-    for (u32 j = 0; j < (1u << lgJ); ++j)
-      best = umax64(best, block_tally_run<kW>(wd, cnt, [=](u32 lab) { return comb_sub(lab, lgJ) == j; },
-                                          tab, redw, err));
+    for (u32 j = 0; j < (1u << lgJ); ++j) {
+      // Spill guard (the hub spill path must not lose counts): the
+      // hashes spread an ordinary bucket's labels well below the table size, but a
+      // pass can still meet more distinct labels than the table holds (adversarial
+      // or unlucky label sets).  Such a pass is dropped and redone on half its
+      // label-value range, and the range grows back after a pass fits; every label's
+      // votes always fall in exactly one pass, so each count stays whole.  Ranges of
+      // <= kCombSlots / 2 label values always fit, so the sweep terminates.
+      u64 lo = 0, width = 1ull << 32;
+      while (lo < (1ull << 32)) {
+        const u64 hi = lo + width < (1ull << 32) ? lo + width : (1ull << 32);
+        const u64 pass = block_tally_run<kW>(
+            wd, cnt, [=](u32 lab) { return comb_sub(lab, lgJ) == j && lab >= lo && lab < hi; }, tab, redw,
+            &ovf);
+        if (ovf) {  // block-uniform (read after block_tally_run's closing barrier)
+          __syncthreads();
+          if (threadIdx.x == 0) ovf = 0;
+          __syncthreads();
+          width >>= 1;
+          continue;
+        }
+        best = umax64(best, pass);
+        lo = hi;
+        if (width < (1ull << 32)) width <<= 1;
+      }
+    }
     if (threadIdx.x == 0 && best) atomicMax(&hub_best[h], best);
   }
 }
@@ -1017,12 +1039,13 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   }
   if (hl < n) {
     hipLaunchKernelGGL(k_hub_lanes, dim3(grid_cap((n - hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
-                       g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, lists, n, g->hub_wcount, lcnt);
+                       g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, lists, n, g->hub_wcount, lcnt,
+                       g->flist, g->fcnt + 16 * g->par, g->fr_all + g->par);
     LPA_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, fork ? (int64_t)0 : hl, n, g->rp,
                      g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, lists, lcnt, g->items_cb,
-                     g->items_cc);
+                     g->items_cc, g->flist, g->fcnt + 16 * g->par, g->fr_all + g->par);
   LPA_HIP(hipGetLastError());
   if (g->hub_waves == 4)
     hipLaunchKernelGGL((k_hub_mid<13, 4>), dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,

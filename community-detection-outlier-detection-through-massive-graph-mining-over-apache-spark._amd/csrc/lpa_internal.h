@@ -148,6 +148,24 @@ struct lpa_graph {
   int64_t n_hub_buckets = 0, n_hub_chunks = 0;
   int32_t* dev_err = nullptr;     // [1] kernel-side error flags (checked after a call)
 
+  // frontier (exact active set): a row whose neighbours all kept their label keeps
+  // its own, L_{t+1}[v] = mode(L_t[N(v)]) = mode(L_{t-1}[N(v)]) = L_t[v], so only rows
+  // with a changed neighbour are re-tallied.  The al[] scatter of superstep t marks
+  // the rows (and hub units) whose al entries it rewrote in rdirty/udirty[par ^ 1];
+  // k_frontier_lists turns them into per-bin row lists and a unit list at the start
+  // of superstep t + 1 (clearing the flags), and the bin kernels walk only those.  fr_all[par] = 1:
+  // every row is tallied (after L0, after an al[] rebuild, frontier off).  Skipped rows
+  // need no write: the diff copies every changed label into the other label vector,
+  // which is the next superstep's output (k_diff / k_delta_compact).
+  int32_t* crow = nullptr;        // [arcs] row (local slot) of each arc position
+  uint8_t* rdirty[2] = {nullptr, nullptr};  // [slice] per parity
+  uint8_t* udirty[2] = {nullptr, nullptr};  // [n_segs] per parity (hub units)
+  int32_t* fr_all = nullptr;      // [2] per parity: 1 = tally every row
+  int32_t* flist = nullptr;       // [slice] dirty rows of this superstep, bin b at bin_begin[b]
+  int32_t* ulist = nullptr;       // [n_segs] dirty hub units of this superstep
+  int32_t* fcnt = nullptr;        // [2][16] per parity: list lengths (bins 0..12, units at 13)
+  int frontier = 1;               // LPA_FRONTIER / lpa_set_frontier
+
   // replicated neighbour labels (GraphX ReplicatedVertexView analogue):
   // al[i] = L_cur[col[i]]; kept current by scatter (few changes) or rebuild
   int32_t* al = nullptr;        // [arcs]
@@ -209,6 +227,7 @@ int init_labels(lpa_graph* g);
 int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
 int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork);  // lpa_hub.hip
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
+int frontier_all(lpa_graph* g, int par);  // next tally of parity `par` takes every row
 
 // iteration (lpa_iter.hip)
 int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st);

@@ -72,6 +72,10 @@ namespace {
 // launch_hub_combine)
 constexpr int kDenseSupersteps = 2;
 
+// frontier: mark the rows the al[] scatter makes dirty while <= this fraction of the
+// arcs changed; above it the next superstep tallies every row
+constexpr double kFrontierFrac = 0.005;
+
 constexpr int kChunks = 8;    // 64-arc chunks per wave: a wave-bin row / a quarter segment
 constexpr u32 kNone = 0xFFFFFFFFu;  // empty lane
 static_assert(kSegArcs == 64 * kChunks, "a unit is one batch of chunks");
@@ -307,15 +311,34 @@ __device__ __forceinline__ void load_labels(u32 (&lab)[NC], const int32_t* __res
 // ---------------------------------------------------------------------------
 // bins g1 / g2 / g4 / g8 / g16
 // ---------------------------------------------------------------------------
+// Frontier row lists (k_frontier_lists): with *fr_all == 0 a bin kernel tallies only
+// the dirty rows of its bin, listed at flist[vbeg, vbeg + *fcnt); otherwise its whole
+// slot range [vbeg, vend).  Index i of the bin's work -> row.
+struct BinRows {
+  int64_t vbeg, n;
+  const int32_t* list;  // nullptr: range mode
+  __device__ __forceinline__ int64_t row(int64_t i) const { return list ? (int64_t)list[vbeg + i] : vbeg + i; }
+};
+__device__ __forceinline__ BinRows bin_rows(int64_t vbeg, int64_t vend, const int32_t* __restrict__ flist,
+                                            const int32_t* __restrict__ fcnt_b,
+                                            const int32_t* __restrict__ fr_all) {
+  BinRows br;
+  br.vbeg = vbeg;
+  if (*fr_all) {
+    br.n = vend - vbeg;
+    br.list = nullptr;
+  } else {
+    br.n = *fcnt_b;
+    br.list = flist;
+  }
+  return br;
+}
+
+// G lanes per row (G <= 64, all 64 lanes of the wave call it: ballot peel)
 template <int G>
-__global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ rp,
-                                                   const int32_t* __restrict__ al,
-                                                   int32_t* __restrict__ Ln, int64_t vbeg,
-                                                   int64_t vend) {
-  const int lane = threadIdx.x & 63;
-  const int64_t v = vbeg + ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
-  const int j = threadIdx.x & (G - 1);
-  const bool live = v < vend;
+__device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
+                                          int32_t* __restrict__ Ln, int64_t v, bool live, int lane) {
+  const int j = lane & (G - 1);
   int64_t b = 0;
   int d = 0;
   if (live) {
@@ -346,6 +369,20 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
   }
 }
 
+template <int G>
+__global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ rp,
+                                                   const int32_t* __restrict__ al,
+                                                   int32_t* __restrict__ Ln, int64_t vbeg,
+                                                   int64_t vend, const int32_t* __restrict__ flist,
+                                                   const int32_t* __restrict__ fcnt_b,
+                                                   const int32_t* __restrict__ fr_all) {
+  const int lane = threadIdx.x & 63;
+  const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const bool live = i < br.n;
+  group_row<G>(rp, al, Ln, live ? br.row(i) : 0, live, lane);
+}
+
 // ---------------------------------------------------------------------------
 // bins w2 / w4 / w8: 64 < deg <= 64 * NC, one wave per vertex, grid-stride,
 // software-pipelined: the next vertex's labels stream in while the current one is
@@ -355,22 +392,31 @@ struct RowSpan {
   int64_t b, e;
 };
 
-__device__ __forceinline__ RowSpan row_span(const int64_t* __restrict__ rp, int64_t v, int64_t vend) {
+// bounds of work item i of the bin (row br.row(i)); past the end: an empty span
+__device__ __forceinline__ RowSpan row_span(const int64_t* __restrict__ rp, const BinRows& br, int64_t i) {
   RowSpan r;
   r.b = 0;
   r.e = 0;
-  if (v < vend) {
+  if (i < br.n) {
+    const int64_t v = br.row(i);
     r.b = rp[v];
     r.e = rp[v + 1];
   }
   return r;
 }
 
+__device__ __forceinline__ int span_len(const RowSpan& r) { return (int)(r.e - r.b); }
+
 // unconditional loads of a row's labels (address clamped into the row)
 template <int NC>
 __device__ __forceinline__ void row_load(u32 (&raw)[NC], const int32_t* __restrict__ al,
                                          const RowSpan& r, int lane) {
-  const int d = (int)(r.e - r.b);
+  const int d = span_len(r);
+  if (__builtin_amdgcn_readfirstlane(d) == 0) {  // frontier-clean row: no loads
+#pragma unroll
+    for (int c = 0; c < NC; ++c) raw[c] = kNone;
+    return;
+  }
   const int last = d > 0 ? d - 1 : 0;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -383,7 +429,7 @@ template <int NC>
 __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r, int64_t v,
                                           int32_t* __restrict__ Ln, u64* tab, uint16_t* lst, int lane,
                                           u64 lt) {
-  const int d = (int)(r.e - r.b);
+  const int d = span_len(r);
   if (d == 0) return;
   u32 lab[NC];
 #pragma unroll
@@ -417,7 +463,9 @@ template <int NC>
 __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp,
                                                   const int32_t* __restrict__ al,
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
-                                                  int64_t vend) {
+                                                  int64_t vend, const int32_t* __restrict__ flist,
+                                                  const int32_t* __restrict__ fcnt_b,
+                                                  const int32_t* __restrict__ fr_all) {
   constexpr int kCap = 2 * 64 * NC;
   __shared__ u64 tab_all[4][kCap];
   __shared__ uint16_t lst_all[4][64 * NC];
@@ -428,29 +476,29 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   for (int i = lane; i < kCap; i += 64) tab[i] = 0ull;
   const u64 lt = (1ull << lane) - 1ull;
   const int64_t stride = (int64_t)gridDim.x * 4;
-  int64_t v = vbeg + (int64_t)blockIdx.x * 4 + w;
-  if (v >= vend) return;  // no block-level barriers in this kernel
-  RowSpan s0 = row_span(rp, v, vend), s1 = row_span(rp, v + stride, vend),
-          s2 = row_span(rp, v + 2 * stride, vend);
+  const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
+  int64_t i = (int64_t)blockIdx.x * 4 + w;   // work item: row br.row(i)
+  if (i >= br.n) return;  // no block-level barriers in this kernel
+  RowSpan s0 = row_span(rp, br, i), s1 = row_span(rp, br, i + stride), s2 = row_span(rp, br, i + 2 * stride);
   u32 ra[NC], rb[NC], rc[NC];
   row_load<NC>(ra, al, s0, lane);
   row_load<NC>(rb, al, s1, lane);
   while (true) {
     row_load<NC>(rc, al, s2, lane);
-    RowSpan s3 = row_span(rp, v + 3 * stride, vend);
-    row_tally<NC>(ra, s0, v, Ln, tab, lst, lane, lt);
-    v += stride;
-    if (v >= vend) break;
+    RowSpan s3 = row_span(rp, br, i + 3 * stride);
+    row_tally<NC>(ra, s0, br.row(i), Ln, tab, lst, lane, lt);
+    i += stride;
+    if (i >= br.n) break;
     row_load<NC>(ra, al, s3, lane);
-    RowSpan s4 = row_span(rp, v + 3 * stride, vend);
-    row_tally<NC>(rb, s1, v, Ln, tab, lst, lane, lt);
-    v += stride;
-    if (v >= vend) break;
+    RowSpan s4 = row_span(rp, br, i + 3 * stride);
+    row_tally<NC>(rb, s1, br.row(i), Ln, tab, lst, lane, lt);
+    i += stride;
+    if (i >= br.n) break;
     row_load<NC>(rb, al, s4, lane);
-    RowSpan s5 = row_span(rp, v + 3 * stride, vend);
-    row_tally<NC>(rc, s2, v, Ln, tab, lst, lane, lt);
-    v += stride;
-    if (v >= vend) break;
+    RowSpan s5 = row_span(rp, br, i + 3 * stride);
+    row_tally<NC>(rc, s2, br.row(i), Ln, tab, lst, lane, lt);
+    i += stride;
+    if (i >= br.n) break;
     s0 = s3;
     s1 = s4;
     s2 = s5;
@@ -518,11 +566,25 @@ template <int G>
 __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp,
                                                   const int32_t* __restrict__ al,
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
-                                                  int64_t vend) {
+                                                  int64_t vend, const int32_t* __restrict__ flist,
+                                                  const int32_t* __restrict__ fcnt_b,
+                                                  const int32_t* __restrict__ fr_all) {
   static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "lane width");
   constexpr int RB = 512 / G;  // rows per batch
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (!*fr_all) {
+    // frontier: the listed dirty rows, G lanes each (rows are not consecutive, so
+    // no batched offsets); every lane of a wave runs every trip (ballot peel)
+    const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
+    const int64_t per = 64 / G, nw = (int64_t)gridDim.x * 4;
+    for (int64_t i0 = ((int64_t)blockIdx.x * 4 + w) * per; i0 < br.n; i0 += nw * per) {
+      const int64_t i = i0 + lane / G;
+      const bool live = i < br.n;
+      group_row<G>(rp, al, Ln, live ? br.row(i) : 0, live, lane);
+    }
+    return;
+  }
   const int64_t nb = (vend - vbeg + RB - 1) / RB;
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t bi = (int64_t)blockIdx.x * 4 + w;
@@ -584,12 +646,21 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
 // combine (lpa_hub.hip) merges a row's units.  Unit: begin arc, row,
 // len | (unit index within the row << 10).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ Segment load_unit(const Segment* __restrict__ units, int64_t u, int64_t n) {
+// work item i of the units kernel -> unit id (frontier: the listed dirty units; a
+// unit not listed keeps the words it staged when last tallied -- its al[] entries
+// are unchanged since, so they are still exact)
+struct UnitIds {
+  int64_t n;
+  const int32_t* list;  // nullptr: every unit
+  __device__ __forceinline__ int64_t id(int64_t i) const { return list ? (int64_t)list[i] : i; }
+};
+
+__device__ __forceinline__ Segment load_unit(const Segment* __restrict__ units, const UnitIds& ui, int64_t i) {
   Segment d;
   d.begin = 0;
   d.len = 0;
   d.v = 0;
-  if (u < n) d = units[u];
+  if (i < ui.n) d = units[ui.id(i)];
   return d;
 }
 
@@ -598,6 +669,11 @@ __device__ __forceinline__ Segment load_unit(const Segment* __restrict__ units, 
 __device__ __forceinline__ void unit_load(u32 (&raw)[kChunks], const int32_t* __restrict__ al,
                                           const Segment& d, int lane) {
   const int len = d.len & 1023;
+  if (__builtin_amdgcn_readfirstlane(len) == 0) {  // frontier-clean unit: no loads
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) raw[c] = kNone;
+    return;
+  }
   const int last = len > 0 ? len - 1 : 0;
 #pragma unroll
   for (int c = 0; c < kChunks; ++c) {
@@ -641,7 +717,10 @@ __device__ __forceinline__ void unit_tally(const u32 (&raw)[kChunks], const Segm
 __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ al,
                                                    const Segment* __restrict__ units, int64_t nunits,
                                                    u64* __restrict__ stage,
-                                                   int32_t* __restrict__ ucnt) {
+                                                   int32_t* __restrict__ ucnt,
+                                                   const int32_t* __restrict__ ulist,
+                                                   const int32_t* __restrict__ fcnt_u,
+                                                   const int32_t* __restrict__ fr_all) {
   constexpr int kCap = 2 * 64 * kChunks;
   __shared__ u64 tab_all[4][kCap];
   __shared__ uint16_t lst_all[4][64 * kChunks];
@@ -656,28 +735,32 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
   if (u >= nunits) return;  // no block-level barriers in this kernel
   // three register sets in a ring, unrolled so no set is ever copied (a copy of a
   // register with a load in flight would wait for it): labels two units ahead
-  Segment d0 = load_unit(units, u, nunits);
-  Segment d1 = load_unit(units, u + stride, nunits);
-  Segment d2 = load_unit(units, u + 2 * stride, nunits);
+  UnitIds ui;
+  ui.n = *fr_all ? nunits : (int64_t)*fcnt_u;
+  ui.list = *fr_all ? nullptr : ulist;
+  if (u >= ui.n) return;
+  Segment d0 = load_unit(units, ui, u);
+  Segment d1 = load_unit(units, ui, u + stride);
+  Segment d2 = load_unit(units, ui, u + 2 * stride);
   u32 ra[kChunks], rb[kChunks], rc[kChunks];
   unit_load(ra, al, d0, lane);
   unit_load(rb, al, d1, lane);
   while (true) {
     unit_load(rc, al, d2, lane);
-    Segment d3 = load_unit(units, u + 3 * stride, nunits);
-    unit_tally(ra, d0, u, stage, ucnt, tab, lst, lane, lt);
+    Segment d3 = load_unit(units, ui, u + 3 * stride);
+    unit_tally(ra, d0, ui.id(u), stage, ucnt, tab, lst, lane, lt);
     u += stride;
-    if (u >= nunits) break;
+    if (u >= ui.n) break;
     unit_load(ra, al, d3, lane);
-    Segment d4 = load_unit(units, u + 3 * stride, nunits);
-    unit_tally(rb, d1, u, stage, ucnt, tab, lst, lane, lt);
+    Segment d4 = load_unit(units, ui, u + 3 * stride);
+    unit_tally(rb, d1, ui.id(u), stage, ucnt, tab, lst, lane, lt);
     u += stride;
-    if (u >= nunits) break;
+    if (u >= ui.n) break;
     unit_load(rb, al, d4, lane);
-    Segment d5 = load_unit(units, u + 3 * stride, nunits);
-    unit_tally(rc, d2, u, stage, ucnt, tab, lst, lane, lt);
+    Segment d5 = load_unit(units, ui, u + 3 * stride);
+    unit_tally(rc, d2, ui.id(u), stage, ucnt, tab, lst, lane, lt);
     u += stride;
-    if (u >= nunits) break;
+    if (u >= ui.n) break;
     d0 = d3;
     d1 = d4;
     d2 = d5;
@@ -692,8 +775,11 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
 // multiple of 64), queues its changed slots in LDS, then reserves its chunk slots
 // with ONE global atomic (a global counter hit by every wave serialises).
 constexpr int kDiffQuads = 2048;  // quads (8192 slots) per block
+// Frontier: every changed label is also copied into Lc (the next superstep's output
+// vector), so a row the next superstep skips already holds its label there.
 __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
-                                              const int4* __restrict__ Ln4, int64_t s0, int64_t s1,
+                                              const int4* __restrict__ Ln4, int32_t* __restrict__ Lsync,
+                                              int64_t s0, int64_t s1,
                                               const int64_t* __restrict__ cptr,
                                               u64* __restrict__ chunks,
                                               unsigned long long* __restrict__ counters) {
@@ -719,10 +805,12 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
         if (q * 4 + k < s0 || q * 4 + k >= s1) chg &= ~(1 << k);
     }
     if (chg) {
+      const int32_t nb[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if ((chg >> k) & 1) {
           const int64_t u = q * 4 + k;
+          Lsync[u] = nb[k];
           const int64_t cnt = cptr[u + 1] - cptr[u];
           const int i = atomicAdd(&qn, 1);
           q_slot[i] = (int32_t)(u - q0 * 4);
@@ -765,6 +853,75 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
   }
 }
 
+// Frontier lists: consume the dirty flags the previous superstep's al[] scatter left
+// (rdirty / udirty of this parity) into per-bin row lists -- bin b's dirty rows at
+// flist[bin_begin[b], + fcnt[b]) -- and a unit list (ulist, fcnt[kFcntUnits]); clears
+// the consumed flags and zeroes the other parity's counts.  When every row is
+// tallied (*fr_all) the bin kernels take their ranges and the flags are left alone
+// (a stale flag only costs one redundant tally later).
+struct BinBounds {
+  int64_t b[LPA_NBINS + 1];
+};
+constexpr int kFcntUnits = LPA_NBINS;  // fcnt[] slot of the unit count
+constexpr int kListTile = 4096;        // flags per block (256 threads x 16)
+__global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rdirty, int64_t S,
+                                                        uint8_t* __restrict__ udirty, int64_t nunits,
+                                                        BinBounds bb, const int32_t* __restrict__ fr_all,
+                                                        int32_t* __restrict__ flist,
+                                                        int32_t* __restrict__ ulist,
+                                                        int32_t* __restrict__ fcnt,
+                                                        int32_t* __restrict__ fcnt_next,
+                                                        int64_t nblk_rows) {
+  __shared__ int32_t lcnt[LPA_NBINS + 1];
+  __shared__ int32_t gbase[LPA_NBINS + 1];
+  if (blockIdx.x == 0 && threadIdx.x < LPA_NBINS + 1) fcnt_next[threadIdx.x] = 0;
+  if (*fr_all) return;  // uniform
+  const bool units = (int64_t)blockIdx.x >= nblk_rows;
+  const int64_t n = units ? nunits : S;
+  uint8_t* flags = units ? udirty : rdirty;
+  const int64_t i0 = ((units ? (int64_t)blockIdx.x - nblk_rows : (int64_t)blockIdx.x) * kListTile) +
+                     (int64_t)threadIdx.x * 16;
+  if (threadIdx.x < LPA_NBINS + 1) lcnt[threadIdx.x] = 0;
+  __syncthreads();
+  // 16 flags per thread (both flag arrays are padded to a multiple of 16 bytes)
+  uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+  if (i0 < n) raw = *reinterpret_cast<const uint4*>(flags + i0);
+  const u32 wv[4] = {raw.x, raw.y, raw.z, raw.w};
+  int16_t rank[16];
+  uint8_t bin[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    rank[k] = -1;
+    bin[k] = 0;
+    const int64_t i = i0 + k;
+    if (((wv[k >> 2] >> (8 * (k & 3))) & 0xFFu) && i < n) {
+      int b = kFcntUnits;
+      if (!units) {
+        b = 0;
+        while (b + 1 < LPA_NBINS && i >= bb.b[b + 1]) ++b;
+      }
+      bin[k] = (uint8_t)b;
+      rank[k] = (int16_t)atomicAdd(&lcnt[b], 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < LPA_NBINS + 1) {
+    const int c = lcnt[threadIdx.x];
+    gbase[threadIdx.x] = c ? atomicAdd(&fcnt[threadIdx.x], c) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (rank[k] >= 0) {
+      const int b = bin[k];
+      const int32_t pos = gbase[b] + rank[k];
+      if (units) ulist[pos] = (int32_t)(i0 + k);
+      else flist[bb.b[b] + pos] = (int32_t)(i0 + k);
+    }
+  }
+  if ((raw.x | raw.y | raw.z | raw.w) && i0 < n) *reinterpret_cast<uint4*>(flags + i0) = make_uint4(0u, 0u, 0u, 0u);
+}
+
 // rebuild al[] when the changed vertices touch more than `thr` arcs (host-set)
 __device__ __forceinline__ bool rebuild_wanted(const unsigned long long* counters, int64_t thr) {
   return (int64_t)counters[1] > thr;
@@ -775,16 +932,42 @@ __device__ __forceinline__ bool rebuild_wanted(const unsigned long long* counter
 // chunks, one per lane (independent loads of cptr and the label): chunks of <= 16
 // positions are written by their own lane (4 stores in flight per step), longer
 // ones by the whole wave (coalesced cpos).
+// Frontier marks for the next superstep: the row holding arc position p (and, for a
+// hub row, the 512-arc unit holding it) must be re-tallied.
+struct FrontierMarks {
+  const int32_t* crow;       // [arcs] row of each position
+  const int64_t* rp;         // row offsets
+  const int64_t* uoff;       // hub rows: first unit
+  int64_t n_hub;
+  uint8_t* rdirty;           // next parity
+  uint8_t* udirty;           // next parity
+  __device__ __forceinline__ void mark(int64_t p) const {
+    const int32_t r = crow[p];
+    rdirty[r] = 1;
+    if (r < n_hub) udirty[uoff[r] + ((p - rp[r]) >> 9)] = 1;
+  }
+};
+static_assert(kSegArcs == 512, "unit of a position: (p - rp[row]) >> 9");
+
 __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chunks,
                                                     const unsigned long long* __restrict__ counters,
                                                     unsigned long long* __restrict__ counters_next,
                                                     const int64_t* __restrict__ cptr,
                                                     const uint32_t* __restrict__ cpos,
                                                     const int32_t* __restrict__ Ln,
-                                                    int32_t* __restrict__ al, int64_t thr) {
+                                                    int32_t* __restrict__ al, int64_t thr,
+                                                    FrontierMarks fm, int32_t* __restrict__ fr_all_next,
+                                                    int frontier, int64_t fr_thr) {
   // the next superstep's counters (the other parity; no memset launch)
   if (blockIdx.x == 0 && threadIdx.x < 2) counters_next[threadIdx.x] = 0ull;
-  if (rebuild_wanted(counters, thr)) return;
+  const bool rebuild = rebuild_wanted(counters, thr);
+  // The next superstep tallies every row after a rebuild, with the frontier off, or
+  // when more than fr_thr arcs changed: then nearly every row has a changed neighbour
+  // anyway (R-MAT superstep 3 -> 4: 1.5 % of arcs dirty, 88 % of the arcs in dirty
+  // rows) and the per-position marks would cost more than they save.
+  const bool all = rebuild || !frontier || (int64_t)counters[1] > fr_thr;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *fr_all_next = all ? 1 : 0;
+  if (rebuild) return;
   const int64_t nchunks = (int64_t)counters[0];
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -809,7 +992,10 @@ __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chun
       for (int t = 0; t < 4; ++t) p[t] = k + t < ns ? cpos[b + k + t] : 0u;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        if (k + t < ns) al[p[t]] = lab;
+        if (k + t < ns) {
+          al[p[t]] = lab;
+          if (!all) fm.mark(p[t]);
+        }
     }
     u64 big = __ballot(n > 16);
     while (big) {
@@ -818,7 +1004,11 @@ __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chun
       const int64_t bb = __shfl(b, bl, 64);
       const int bn = __shfl(n, bl, 64);
       const int32_t bv = __shfl(lab, bl, 64);
-      for (int i = lane; i < bn; i += 64) al[cpos[bb + i]] = bv;
+      for (int i = lane; i < bn; i += 64) {
+        const uint32_t pp = cpos[bb + i];
+        al[pp] = bv;
+        if (!all) fm.mark(pp);
+      }
     }
   }
 }
@@ -946,11 +1136,25 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // kernel trace shows each kernel's standalone duration
   hipStream_t sb = g->serial ? s : g->aux_stream[0], sc = g->serial ? s : g->aux_stream[1];
   const int64_t* bb = g->bin_begin;
+  const int32_t* fr_all = g->fr_all + g->par;
+  int32_t* fcnt = g->fcnt + 16 * g->par;
+  // frontier lists of this superstep (no-op when every row is tallied)
+  {
+    BinBounds bnd;
+    for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = bb[b];
+    const int64_t nbr = (g->slice + kListTile - 1) / kListTile;
+    const int64_t nbu = (g->n_segs + kListTile - 1) / kListTile;
+    hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, s, g->rdirty[g->par],
+                       g->slice, g->udirty[g->par], g->n_segs, bnd, fr_all, g->flist, g->ulist, fcnt,
+                       g->fcnt + 16 * (g->par ^ 1), nbr);
+    LPA_HIP(hipGetLastError());
+  }
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
     LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
     LPA_HIP(hipStreamWaitEvent(sc, g->ev_fork, 0));
   }
+
   auto mark = [&](int i, hipStream_t st) -> int {
     if (bev) LPA_HIP(hipEventRecord(bev[i], st));
     return LPA_OK;
@@ -958,7 +1162,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_TRY(mark(0, s));
   if (g->n_segs > 0) {
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
-                       g->al, g->segs, g->n_segs, g->stage, g->ucnt);
+                       g->al, g->segs, g->n_segs, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all);
     LPA_HIP(hipGetLastError());
     LPA_TRACE_POINT("seg");
   }
@@ -969,7 +1173,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(mark(2 * (BIN + 1), ST));                                                         \
     if (n > 0) {                                                                              \
       hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, ST,  \
-                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                          \
+                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all); \
       LPA_HIP(hipGetLastError());                                                             \
     }                                                                                         \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                     \
@@ -980,7 +1184,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(mark(2 * (BIN + 1), sc));                                                        \
     if (n > 0) {                                                                             \
       hipLaunchKernelGGL(k_lpa_group<G>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
-                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                     \
+                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all); \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
@@ -992,7 +1196,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     if (n > 0) {                                                                             \
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
       hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
-                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1]);                     \
+                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all); \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
@@ -1080,8 +1284,8 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
   if (s1 <= s0) return LPA_OK;
   const int64_t nq = (s1 + 3) / 4 - s0 / 4;
   hipLaunchKernelGGL(k_diff, dim3((unsigned)((nq + kDiffQuads - 1) / kDiffQuads)), dim3(256), 0, st,
-                     (const int4*)Lc, (const int4*)Ln, s0, s1, g->cptr, g->chunks,
-                     g->counters + 4 * g->par);
+                     (const int4*)Lc, (const int4*)Ln, const_cast<int32_t*>(Lc), s0, s1, g->cptr,
+                     g->chunks, g->counters + 4 * g->par);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -1096,9 +1300,17 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, g->vpad));
   LPA_TRACE_POINT("diff");
   const int64_t thr = (int64_t)(g->rebuild_frac * (double)g->arcs);
+  FrontierMarks fm;
+  fm.crow = g->crow;
+  fm.rp = g->rp;
+  fm.uoff = g->hub_uoff;
+  fm.n_hub = g->n_hub;
+  fm.rdirty = g->rdirty[g->par ^ 1];
+  fm.udirty = g->udirty[g->par ^ 1];
   hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, ctr,
                      g->counters + 4 * (g->par ^ 1), g->cptr,
-                     g->cpos, Ln, g->al, thr);
+                     g->cpos, Ln, g->al, thr, fm, g->fr_all + (g->par ^ 1), g->frontier,
+                     (int64_t)(kFrontierFrac * (double)g->arcs));
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
@@ -1213,6 +1425,11 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     LPA_HIP(hipEventElapsedTime(&tot, g->ev[2 * LPA_STATS_MAX_ITERS], g->ev[2 * LPA_STATS_MAX_ITERS + 1]));
     st->total_ms = tot;
   }
+  return LPA_OK;
+}
+
+int frontier_all(lpa_graph* g, int par) {
+  LPA_HIP(hipMemsetD32Async((hipDeviceptr_t)(g->fr_all + par), 1, 1, g->stream));
   return LPA_OK;
 }
 

@@ -149,6 +149,10 @@ class Graph:
         _lib.check(self._lib.lpa_degrees(self._handle(), deg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return deg
 
+    def set_frontier(self, on: bool = True):
+        """Re-tally only rows with a changed neighbour (exact; default on) or every row."""
+        _lib.check(self._lib.lpa_set_frontier(self._handle(), int(bool(on))))
+
     def set_serial(self, serial: bool = True):
         """Profiling: queue every tally kernel on one stream (standalone kernel times)."""
         _lib.check(self._lib.lpa_set_serial(self._handle(), int(bool(serial))))

@@ -162,6 +162,12 @@ int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t*
  * stream (no concurrent bins), so per-kernel times in lpa_stats are standalone
  * durations.  Labels are identical either way. */
 int lpa_set_serial(lpa_graph* g, int32_t serial);
+/* Frontier (default on; LPA_FRONTIER=0 at create time turns it off): a superstep
+ * re-tallies only the rows with a neighbour whose label changed in the previous
+ * superstep -- exact, since a row whose neighbourhood labels are unchanged has the
+ * same mode (GraphX Pregel's active-set idea applied to LPA).  Off: every row is
+ * tallied every superstep.  Labels are identical either way. */
+int lpa_set_frontier(lpa_graph* g, int32_t on);
 /* Run on a caller-provided hipStream_t (NULL = the handle's own stream). */
 int lpa_set_stream(lpa_graph* g, void* hip_stream);
 

@@ -77,3 +77,28 @@ def giant_hub(seed=0, n_plain=200000, n_skew=20000, lg=7):
     bs = rng.integers(1, V, size=V // 2)
     bd = rng.integers(1, V, size=V // 2)
     return V, np.concatenate([s, bs]).astype(np.int32), np.concatenate([nb, bd]).astype(np.int32)
+
+
+def comb_sub(labels, lg):
+    """k_hub_bucket's sub-bucket hash (lpa_hub.hip comb_sub)."""
+    x = (labels.astype(np.uint64) * np.uint64(0xC2B2AE3D)) & np.uint64(0xFFFFFFFF)
+    return (x >> np.uint64(32 - lg)).astype(np.int64) if lg else np.zeros(labels.shape, np.int64)
+
+
+def adversarial_hub(n_nb=20000, seed=0):
+    """Hub 0 whose n_nb distinct neighbours ALL share one combine bucket (4 hash bits)
+    and one sub-bucket (3 bits): in superstep 1 (labels = ids) its bucket pass meets
+    n_nb > 8192 distinct labels, more than the LDS table holds (the case the spill
+    guard must handle without dropping votes).  One neighbour carries a triple edge,
+    so the hub's mode is decided inside that pass; a sparse background among the
+    neighbours keeps later supersteps non-trivial."""
+    rng = np.random.default_rng(seed)
+    ids = np.arange(1, 200 * n_nb, dtype=np.int64)
+    sel = ids[(comb_bucket(ids, 4) == 5) & (comb_sub(ids, 3) == 2)][:n_nb]
+    assert sel.size == n_nb
+    V = int(sel.max()) + 1
+    nb = np.concatenate([rng.permutation(sel), [sel[17]] * 2])
+    s = np.zeros(nb.size, np.int64)
+    bs = rng.choice(sel, size=n_nb)
+    bd = rng.choice(sel, size=n_nb)
+    return V, np.concatenate([s, bs]).astype(np.int32), np.concatenate([nb, bd]).astype(np.int32)
