@@ -265,6 +265,7 @@ int init_labels(lpa_graph* g) {
   }
   LPA_HIP(hipMemsetD32Async((hipDeviceptr_t)g->fr_all, 1, 2, g->stream));
   LPA_HIP(hipMemsetAsync(g->fcnt, 0, sizeof(int32_t) * 32, g->stream));
+  LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 8, g->stream));
   g->cur = 0;
   g->since_reset = 0;
   g->prev_delta_ok = false;  // the exchange's delta chain restarts from L0

@@ -311,16 +311,15 @@ int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t*
                            hipMemcpyHostToDevice, s));
   LPA_HIP(hipMemcpyAsync(exchange_recv_counts(g), counts, sizeof(int64_t) * g->nranks,
                          hipMemcpyHostToDevice, s));
-  // the refresh's counters of this parity (a full put between two deltas runs no
-  // scatter, which would otherwise have zeroed them)
-  LPA_HIP(hipMemsetAsync(g->counters + 4 * g->par, 0, sizeof(unsigned long long) * 2, s));
+  // this refresh completes the superstep that just ran (lpa_step already flipped the
+  // parity): its counters (zeroed here -- the caller-driven path runs no scatter of
+  // its own), its arc mode, and the next superstep's flags / mode
+  const int pp = g->par ^ 1;
+  LPA_HIP(hipMemsetAsync(g->counters + 4 * pp, 0, sizeof(unsigned long long) * 2, s));
   const int32_t* Lc = g->lab[g->cur ^ 1];
   int32_t* Ln = g->lab[g->cur];
-  LPA_TRY(exchange_finish_delta(g, Lc, Ln, cap));
-  LPA_TRY(launch_refresh_ext(g, Lc, Ln, true));
-  // this refresh runs outside the superstep's parity bookkeeping: the next superstep
-  // tallies every row instead of reading its flags
-  LPA_TRY(frontier_all(g, g->par));
+  LPA_TRY(exchange_finish_delta(g, Lc, Ln, cap, pp));
+  LPA_TRY(launch_refresh_ext(g, Lc, Ln, true, pp));
   LPA_HIP(hipStreamSynchronize(s));
   return LPA_OK;
 }

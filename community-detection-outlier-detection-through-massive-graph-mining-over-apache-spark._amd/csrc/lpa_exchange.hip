@@ -177,8 +177,8 @@ int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
 
 // Ln := L_{t+1} from the gathered changes in the current receive buffer (cap entries
 // per rank) -- see the header; also queues the al[] position chunks of the changes
-// (counters of this superstep's parity).  Flips the receive buffer.
-int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap) {
+// (counters of parity `par`, the superstep's).  Flips the receive buffer.
+int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par) {
   hipStream_t s = g->stream;
   const int P = g->nranks;
   const int64_t n4 = g->vpad / 4;
@@ -201,7 +201,7 @@ int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t 
     LPA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_delta_chunks, dim3(grid_of(cap * P, 4096)), dim3(256), 0, s,
                        exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->slice, g->cptr,
-                       g->chunks, g->counters + 4 * g->par, g->rank, const_cast<int32_t*>(Lc));
+                       g->chunks, g->counters + 4 * par, g->rank, const_cast<int32_t*>(Lc));
     LPA_HIP(hipGetLastError());
   }
   g->prev_cap = cap;
@@ -232,7 +232,7 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense
       g->last_exchange_delta = cap;
       ++g->n_exch_delta;
       *changes_listed = true;
-      return exchange_finish_delta(g, Lc, Ln, cap);
+      return exchange_finish_delta(g, Lc, Ln, cap, g->par);
     }
   }
   // full: in-place allgather of the owned slices (rank r's slice at Ln + r * slice)

@@ -175,10 +175,10 @@ struct lpa_graph {
   int64_t n_chunk_cap = 0;
   lpa::u64* chunks = nullptr;   // changed-vertex position chunks: (u << 32 | chunk index)
   double rebuild_frac = lpa::kRebuildFrac;  // LPA_REBUILD_FRAC overrides (tuning experiments)
+  int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   hipGraphExec_t gexec[4] = {};             // captured converged superstep per (cur, par)
-  int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
   int hub_waves = 8;                        // LPA_HUB_WAVES: waves per block of the 8K-slot hub combine (4 or 8)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
@@ -248,9 +248,9 @@ void exchange_free(lpa_graph* g);
 int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln);
 lpa::u64* exchange_recv_buf(lpa_graph* g);
 unsigned long long* exchange_recv_counts(lpa_graph* g);
-int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap);
+int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par);
 int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed);
-int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done);
+int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par);
 
 // outlier (lpa_outlier.hip)
 int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,

@@ -775,8 +775,9 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
 // multiple of 64), queues its changed slots in LDS, then reserves its chunk slots
 // with ONE global atomic (a global counter hit by every wave serialises).
 constexpr int kDiffQuads = 2048;  // quads (8192 slots) per block
-// Frontier: every changed label is also copied into Lc (the next superstep's output
-// vector), so a row the next superstep skips already holds its label there.
+// Frontier: with Lsync != nullptr every changed label is also copied into Lc (the next
+// superstep's output vector), so a row the next superstep skips already holds its
+// label there (inside the concurrent tally the scatter refresh does it instead).
 __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
                                               const int4* __restrict__ Ln4, int32_t* __restrict__ Lsync,
                                               int64_t s0, int64_t s1,
@@ -810,7 +811,7 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
       for (int k = 0; k < 4; ++k) {
         if ((chg >> k) & 1) {
           const int64_t u = q * 4 + k;
-          Lsync[u] = nb[k];
+          if (Lsync) Lsync[u] = nb[k];
           const int64_t cnt = cptr[u + 1] - cptr[u];
           const int i = atomicAdd(&qn, 1);
           q_slot[i] = (int32_t)(u - q0 * 4);
@@ -845,11 +846,26 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
   }
   if (threadIdx.x == 0) base_s = atomicAdd(&counters[0], (unsigned long long)tot);
   if (lane == 0 && dirty) atomicAdd(&counters[1], dirty);
-  __syncthreads();
-  u64 pos = base_s + (u64)(before + incl - loc);
+  // q_nch -> inclusive prefix over the queue (block-relative)
+  int run = before + incl - loc;
   for (int i = i0; i < i1; ++i) {
-    const u64 u = (u64)(q0 * 4 + q_slot[i]);
-    for (int c = 0; c < q_nch[i]; ++c) chunks[pos++] = (u << 32) | (u64)c;
+    run += q_nch[i];
+    q_nch[i] = run;
+  }
+  __syncthreads();
+  // chunk k of the block belongs to the first queued vertex whose prefix exceeds k:
+  // every thread writes a strided share, so a hub column with thousands of chunks
+  // (C5: ~5K per million-arc column) is not written by one thread
+  const u64 base = base_s;
+  for (int k = threadIdx.x; k < tot; k += 256) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (q_nch[mid] > k) hi = mid; else lo = mid + 1;
+    }
+    const int first = lo ? q_nch[lo - 1] : 0;
+    const u64 u = (u64)(q0 * 4 + q_slot[lo]);
+    chunks[base + k] = (u << 32) | (u64)(k - first);
   }
 }
 
@@ -957,7 +973,8 @@ __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chun
                                                     const int32_t* __restrict__ Ln,
                                                     int32_t* __restrict__ al, int64_t thr,
                                                     FrontierMarks fm, int32_t* __restrict__ fr_all_next,
-                                                    int frontier, int64_t fr_thr) {
+                                                    int frontier, int64_t fr_thr,
+                                                    int32_t* __restrict__ Lold) {
   // the next superstep's counters (the other parity; no memset launch)
   if (blockIdx.x == 0 && threadIdx.x < 2) counters_next[threadIdx.x] = 0ull;
   const bool rebuild = rebuild_wanted(counters, thr);
@@ -984,6 +1001,9 @@ __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chun
       b = rb + (int64_t)(u32)ch * kChunkPos;
       n = (int)min((int64_t)kChunkPos, re - b);
       lab = Ln[u];
+      // frontier sync of a changed label into the next superstep's output vector
+      // (after the join; every changed vertex with local arcs has a chunk 0)
+      if ((u32)ch == 0u) Lold[u] = lab;
     }
     const int ns = n <= 16 ? n : 0;
     for (int k = 0; k < ns; k += 4) {
@@ -1124,7 +1144,7 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
 // tails of the small bins.  bev (nullable): events 2k / 2k+1 bracket tally kernel
 // k on its own stream (0 units, 1 hub combine, 2..11 bins w8 .. g1).
 int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* Ln, int64_t s0,
-                int64_t s1);
+                int64_t s1, bool sync, int par);
 
 // diff (P = 1, concurrent schedule): each stream diffs the slots its own bins
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
@@ -1224,9 +1244,10 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_TRACE_POINT("hub_combine");
   LPA_TRY(mark(3, s));
   if (diff) {
-    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2]));
-    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], g->vpad));
-    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16]));
+    // inside the concurrent tally: no Lc sync here, the scatter refresh does it
+    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2], false, g->par));
+    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], g->vpad, false, g->par));
+    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par));
   }
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_join[0], sb));
@@ -1280,24 +1301,25 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
 // changed slots in [s0, s1) -> position chunks + dirty-arc count (counters of this
 // superstep's parity)
 int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* Ln, int64_t s0,
-                int64_t s1) {
+                int64_t s1, bool sync, int par) {
   if (s1 <= s0) return LPA_OK;
   const int64_t nq = (s1 + 3) / 4 - s0 / 4;
   hipLaunchKernelGGL(k_diff, dim3((unsigned)((nq + kDiffQuads - 1) / kDiffQuads)), dim3(256), 0, st,
-                     (const int4*)Lc, (const int4*)Ln, const_cast<int32_t*>(Lc), s0, s1, g->cptr,
-                     g->chunks, g->counters + 4 * g->par);
+                     (const int4*)Lc, (const int4*)Ln, sync ? const_cast<int32_t*>(Lc) : nullptr, s0, s1,
+                     g->cptr, g->chunks, g->counters + 4 * par);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
 
-// refresh al[] for L_next (after the exchange, so every rank sees all changes);
-// diff_done: the tally schedule already ran the diff per stream (launch_tally)
-int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done) {
+// refresh al[] for L_next (after the exchange, so every rank sees all changes) of the
+// superstep of parity `par`; diff_done: the tally schedule already ran the diff per
+// stream (launch_tally) or the exchange listed the changes
+int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par) {
   if (g->arcs == 0) return LPA_OK;
   hipStream_t s = g->stream;
   // this superstep's counters (zeroed by the previous k_al_scatter or at build)
-  unsigned long long* ctr = g->counters + 4 * g->par;
-  if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, g->vpad));
+  unsigned long long* ctr = g->counters + 4 * par;
+  if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, g->vpad, true, par));
   LPA_TRACE_POINT("diff");
   const int64_t thr = (int64_t)(g->rebuild_frac * (double)g->arcs);
   FrontierMarks fm;
@@ -1305,12 +1327,12 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   fm.rp = g->rp;
   fm.uoff = g->hub_uoff;
   fm.n_hub = g->n_hub;
-  fm.rdirty = g->rdirty[g->par ^ 1];
-  fm.udirty = g->udirty[g->par ^ 1];
+  fm.rdirty = g->rdirty[par ^ 1];
+  fm.udirty = g->udirty[par ^ 1];
   hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, ctr,
-                     g->counters + 4 * (g->par ^ 1), g->cptr,
-                     g->cpos, Ln, g->al, thr, fm, g->fr_all + (g->par ^ 1), g->frontier,
-                     (int64_t)(kFrontierFrac * (double)g->arcs));
+                     g->counters + 4 * (par ^ 1), g->cptr,
+                     g->cpos, Ln, g->al, thr, fm, g->fr_all + (par ^ 1), g->frontier,
+                     (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc));
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
@@ -1320,8 +1342,8 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
 
 }  // namespace
 
-int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done) {
-  return launch_refresh(g, Lc, Ln, diff_done);
+int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par) {
+  return launch_refresh(g, Lc, Ln, diff_done, par);
 }
 
 int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
@@ -1360,7 +1382,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
         hipGraph_t graph = nullptr;
         LPA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
         int rc = launch_tally(g, Lown, nullptr, Lc, Ln, true);
-        if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true);
+        if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true, g->par);
         hipError_t ec = hipStreamEndCapture(s, &graph);
         if (rc != LPA_OK) return rc;
         LPA_HIP(ec);
@@ -1384,7 +1406,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // P > 1 without a communicator: the caller completes the superstep with
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
     // (changes + refresh); a refresh here would see a partial vector
-    if (g->nranks == 1 || has_collective(g)) LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed));
+    if (g->nranks == 1 || has_collective(g))
+      LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     g->cur ^= 1;
