@@ -186,6 +186,21 @@ __global__ void k_csc_keys(const int32_t* __restrict__ col, int64_t n, u64* __re
   }
 }
 
+// scatter chunks of every column: count, then owner of each chunk
+__global__ void k_col_chunks(const int32_t* __restrict__ colcnt, int64_t n, int32_t* __restrict__ nch) {
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n;
+       u += (int64_t)gridDim.x * blockDim.x)
+    nch[u] = (colcnt[u] + kChunkPos - 1) / kChunkPos;
+}
+__global__ void k_chunk_owner(const int64_t* __restrict__ cch, int64_t n, int32_t* __restrict__ cowner,
+                              unsigned long long* __restrict__ scan_end) {
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t c = cch[u]; c < cch[u + 1]; ++c) cowner[c] = (int32_t)u;
+    if (cch[u + 1] - cch[u] > 1) atomicMax(scan_end, (unsigned long long)cch[u + 1]);
+  }
+}
+
 __global__ void k_keys_to_pos(const u64* __restrict__ keys, int64_t n, uint32_t* __restrict__ pos) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += (int64_t)gridDim.x * blockDim.x)
@@ -421,16 +436,47 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t) * arcs));
     hipLaunchKernelGGL(k_keys_to_pos, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->cpos);
     LPA_HIP(hipGetLastError());
+    // static scatter chunks (colcnt is reused for the per-column chunk counts)
+    hipLaunchKernelGGL(k_col_chunks, dim3(grid_for(g->vpad)), dim3(256), 0, s, colcnt, g->vpad, colcnt);
+    LPA_HIP(hipGetLastError());
+    LPA_TRY(dev_alloc(g, (void**)&g->cch, sizeof(int64_t) * (g->vpad + 1)));
+    LPA_TRY(exclusive_scan_i32_i64(colcnt, g->cch, g->vpad, s));
+    LPA_HIP(hipMemcpyAsync(&g->n_chunks, g->cch + g->vpad, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t) * (g->n_chunks > 0 ? g->n_chunks : 1)));
+    {
+      // multi-chunk columns are the high-degree ones, i.e. the first slots at P = 1:
+      // the scatter scans the chunk flags only up to the last such column's chunks
+      unsigned long long* d_end = nullptr;
+      LPA_HIP(hipMalloc((void**)&d_end, sizeof(unsigned long long)));
+      LPA_HIP(hipMemsetAsync(d_end, 0, sizeof(unsigned long long), s));
+      hipLaunchKernelGGL(k_chunk_owner, dim3(grid_for(g->vpad)), dim3(256), 0, s, g->cch, g->vpad,
+                         g->cowner, d_end);
+      LPA_HIP(hipGetLastError());
+      unsigned long long h_end = 0;
+      LPA_HIP(hipMemcpyAsync(&h_end, d_end, sizeof(h_end), hipMemcpyDeviceToHost, s));
+      LPA_HIP(hipStreamSynchronize(s));
+      LPA_HIP(hipFree(d_end));
+      g->n_chunk_scan = (int64_t)h_end;
+    }
     LPA_HIP(hipFree(colcnt));
     LPA_HIP(hipFree(keys));
   } else {
     LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
     LPA_HIP(hipMemsetAsync(g->cptr, 0, sizeof(int64_t) * (g->vpad + 1), s));
     LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t)));
+    LPA_TRY(dev_alloc(g, (void**)&g->cch, sizeof(int64_t) * (g->vpad + 1)));
+    LPA_HIP(hipMemsetAsync(g->cch, 0, sizeof(int64_t) * (g->vpad + 1), s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t)));
+    g->n_chunks = 0;
   }
   LPA_TRY(dev_alloc(g, (void**)&g->al, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
-  g->n_chunk_cap = arcs / kChunkPos + g->vpad + 1;
-  LPA_TRY(dev_alloc(g, (void**)&g->chunks, sizeof(u64) * g->n_chunk_cap));
+  {
+    const int64_t nfl = (g->n_chunks + 16) / 16 * 16;
+    LPA_TRY(dev_alloc(g, (void**)&g->chflag, nfl));
+    LPA_HIP(hipMemsetAsync(g->chflag, 0, nfl, s));
+    LPA_TRY(dev_alloc(g, (void**)&g->chlist, sizeof(int32_t) * g->vpad));
+  }
   LPA_TRY(dev_alloc(g, (void**)&g->counters, sizeof(unsigned long long) * 8));  // 2 parities
   LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 8, s));
 

@@ -87,52 +87,48 @@ __global__ void k_delta_apply(const u64* __restrict__ drecv, const unsigned long
   }
 }
 
-// the gathered changes as al[] position chunks (u << 32 | k) + the dirty-arc count:
-// k_diff's output, from the change list instead of a scan of the whole vector.
-// Frontier (as k_diff): this rank's own changed labels are also copied into Lsync
-// (the current vector Lc, the next superstep's output), so an owned row the next
-// superstep skips already holds its label there.
+// the gathered changes as flagged al[] scatter chunks + the dirty-arc count: k_diff's
+// output, from the change list instead of a scan of the whole vector.  Frontier (as
+// k_diff): this rank's own changed labels are also copied into Lsync (the current
+// vector Lc, the next superstep's output), so an owned row the next superstep skips
+// already holds its label there.
 __global__ __launch_bounds__(256) void k_delta_chunks(const u64* __restrict__ drecv,
                                                       const unsigned long long* __restrict__ counts,
                                                       int64_t cap, int32_t P, int64_t slice,
                                                       const int64_t* __restrict__ cptr,
-                                                      u64* __restrict__ chunks,
+                                                      const int64_t* __restrict__ cch,
+                                                      uint8_t* __restrict__ chflag,
+                                                      int32_t* __restrict__ chlist,
                                                       unsigned long long* __restrict__ counters,
                                                       int32_t own, int32_t* __restrict__ Lsync) {
   const int lane = threadIdx.x & 63;
   const int64_t tot = cap * P;
+  unsigned long long dirty = 0;
   for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = k0 + threadIdx.x;
-    int nch = 0;
-    int64_t u = 0, cnt = 0;
+    bool one = false;
+    int64_t u = 0;
     if (k < tot) {
       const int64_t r = k / cap, j = k - r * cap;
       if (j < (int64_t)counts[r]) {
         const u64 e = drecv[k];
         u = r * slice + (int64_t)(e >> 32);
         if (r == own) Lsync[u] = (int32_t)(uint32_t)e;
-        cnt = cptr[u + 1] - cptr[u];
-        nch = (int)((cnt + kChunkPos - 1) / kChunkPos);
+        dirty += (unsigned long long)(cptr[u + 1] - cptr[u]);
+        const int64_t nch = cch[u + 1] - cch[u];
+        one = nch == 1;
+        for (int64_t c = cch[u]; nch > 1 && c < cch[u + 1]; ++c) chflag[c] = 1;
       }
     }
-    // wave-aggregated reservation of chunk slots and dirty-arc count
-    int incl = nch;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += o;
-    }
-    const int wtot = __shfl(incl, 63, 64);
-    unsigned long long dirty = (unsigned long long)cnt;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) dirty += __shfl_xor(dirty, off, 64);
+    // one-chunk columns -> the scatter's list (one atomic per wave)
+    const u64 om = __ballot(one);
     unsigned long long base = 0;
-    if (lane == 0 && wtot) base = atomicAdd(&counters[0], (unsigned long long)wtot);
-    if (lane == 0 && dirty) atomicAdd(&counters[1], dirty);
+    if (lane == 0 && om) base = atomicAdd(&counters[0], (unsigned long long)__popcll(om));
     base = __shfl(base, 0, 64);
-    u64 pos = base + (u64)(incl - nch);
-    for (int c = 0; c < nch; ++c) chunks[pos++] = ((u64)u << 32) | (u64)c;
+    if (one) chlist[base + __popcll(om & ((1ull << lane) - 1ull))] = (int32_t)u;
   }
+  for (int off = 32; off > 0; off >>= 1) dirty += __shfl_xor(dirty, off, 64);
+  if (lane == 0 && dirty) atomicAdd(&counters[1], dirty);
 }
 
 inline unsigned grid_of(int64_t n, int64_t cap) {
@@ -200,8 +196,8 @@ int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t 
                        exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->rank, g->slice, Ln);
     LPA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_delta_chunks, dim3(grid_of(cap * P, 4096)), dim3(256), 0, s,
-                       exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->slice, g->cptr,
-                       g->chunks, g->counters + 4 * par, g->rank, const_cast<int32_t*>(Lc));
+                       exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->slice, g->cptr, g->cch,
+                       g->chflag, g->chlist, g->counters + 4 * par, g->rank, const_cast<int32_t*>(Lc));
     LPA_HIP(hipGetLastError());
   }
   g->prev_cap = cap;

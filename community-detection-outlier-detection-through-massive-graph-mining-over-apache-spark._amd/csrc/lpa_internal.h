@@ -172,8 +172,14 @@ struct lpa_graph {
   int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
   uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])
   // per-superstep change bookkeeping (device)
-  int64_t n_chunk_cap = 0;
-  lpa::u64* chunks = nullptr;   // changed-vertex position chunks: (u << 32 | chunk index)
+  // scatter chunks: column u's positions cpos[cptr[u] ..) in pieces of kChunkPos,
+  // numbered statically: chunks cch[u] .. cch[u+1] - 1 belong to u (cowner[])
+  int64_t n_chunks = 0;
+  int64_t* cch = nullptr;       // [vpad + 1]
+  int32_t* cowner = nullptr;    // [n_chunks]
+  uint8_t* chflag = nullptr;    // [n_chunks, padded to 16] changed multi-chunk columns' flags
+  int64_t n_chunk_scan = 0;     // chunks below this belong to every multi-chunk column
+  int32_t* chlist = nullptr;    // [vpad] changed one-chunk columns (count: counters[par][0])
   double rebuild_frac = lpa::kRebuildFrac;  // LPA_REBUILD_FRAC overrides (tuning experiments)
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)

@@ -770,30 +770,43 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
 // ---------------------------------------------------------------------------
 // refresh of the replicated neighbour labels al[]
 // ---------------------------------------------------------------------------
-// changed vertices -> position chunks (u << 32 | k) and the dirty-arc count.
-// Each block scans one contiguous range of 4-slot quads (int4 loads; vpad is a
-// multiple of 64), queues its changed slots in LDS, then reserves its chunk slots
-// with ONE global atomic (a global counter hit by every wave serialises).
-constexpr int kDiffQuads = 2048;  // quads (8192 slots) per block
-// Frontier: with Lsync != nullptr every changed label is also copied into Lc (the next
-// superstep's output vector), so a row the next superstep skips already holds its
-// label there (inside the concurrent tally the scatter refresh does it instead).
+// Scatter chunks: column u's al[] positions cpos[cptr[u] ..) are cut into chunks of
+// kChunkPos, numbered statically at build time (chunks cch[u] .. cch[u+1] - 1,
+// cowner[chunk] = u).  A changed column flags its chunks in the bytemap chflag[]
+// (plain byte stores, no list to build); the scatter walks the bytemap.
+__device__ __forceinline__ void flag_chunks(uint8_t* __restrict__ chflag, const int64_t* __restrict__ cch,
+                                            int64_t u) {
+  int64_t c = cch[u];
+  const int64_t e = cch[u + 1];
+  for (; c < e && (c & 15); ++c) chflag[c] = 1;  // hub columns: thousands of chunks,
+  for (; c + 16 <= e; c += 16)                    // 16 flags per store
+    *reinterpret_cast<uint4*>(chflag + c) = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+  for (; c < e; ++c) chflag[c] = 1;
+}
+
+// changed vertices of the slot range [s0, s1): a column with one scatter chunk (the
+// vast majority) is appended to chlist[] (LDS queue, one atomic per block), a longer
+// one flags its chunks in chflag[]; the dirty arcs are counted (one atomic per wave);
+// with Lsync != nullptr the new label is also copied into Lc (the next superstep's
+// output vector: frontier, a row the next superstep skips already holds its label
+// there; inside the concurrent tally the scatter does it).  int4 quads (vpad is a
+// multiple of 64), kDiffQuads per block; lanes outside the range masked (the
+// neighbouring slots may belong to a bin another stream is still computing).
+constexpr int kDiffQuads = 2048;
 __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
                                               const int4* __restrict__ Ln4, int32_t* __restrict__ Lsync,
                                               int64_t s0, int64_t s1,
                                               const int64_t* __restrict__ cptr,
-                                              u64* __restrict__ chunks,
+                                              const int64_t* __restrict__ cch,
+                                              uint8_t* __restrict__ chflag,
+                                              int32_t* __restrict__ chlist,
                                               unsigned long long* __restrict__ counters) {
-  __shared__ int32_t q_slot[kDiffQuads * 4];
-  __shared__ int32_t q_nch[kDiffQuads * 4];
+  __shared__ int32_t q_col[kDiffQuads * 4];
   __shared__ int qn;
-  __shared__ int wsum[4];
   __shared__ unsigned long long base_s;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   if (threadIdx.x == 0) qn = 0;
   __syncthreads();
-  // slot range [s0, s1): quads [s0 / 4, ceil(s1 / 4)), lanes outside the range masked
-  // (the neighbouring slots may belong to a bin another stream is still computing)
   const int64_t q0 = s0 / 4 + (int64_t)blockIdx.x * kDiffQuads;
   const int64_t q1 = min((s1 + 3) / 4, q0 + kDiffQuads);
   unsigned long long dirty = 0;
@@ -812,61 +825,22 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
         if ((chg >> k) & 1) {
           const int64_t u = q * 4 + k;
           if (Lsync) Lsync[u] = nb[k];
-          const int64_t cnt = cptr[u + 1] - cptr[u];
-          const int i = atomicAdd(&qn, 1);
-          q_slot[i] = (int32_t)(u - q0 * 4);
-          q_nch[i] = (int)((cnt + kChunkPos - 1) / kChunkPos);
-          dirty += (unsigned long long)cnt;
+          dirty += (unsigned long long)(cptr[u + 1] - cptr[u]);
+          const int64_t nch = cch[u + 1] - cch[u];
+          if (nch == 1) q_col[atomicAdd(&qn, 1)] = (int32_t)u;
+          else if (nch > 1) flag_chunks(chflag, cch, u);
         }
       }
     }
   }
+  for (int off = 32; off > 0; off >>= 1) dirty += __shfl_xor(dirty, off, 64);
+  if (lane == 0 && dirty) atomicAdd(&counters[1], dirty);
   __syncthreads();
   const int n = qn;
   if (n == 0) return;  // uniform
-  // exclusive scan of q_nch over the queue (serial per thread over its stripe)
-  const int per = (n + 255) / 256;
-  const int i0 = min(n, (int)threadIdx.x * per), i1 = min(n, i0 + per);
-  int loc = 0;
-  for (int i = i0; i < i1; ++i) loc += q_nch[i];
-  int incl = loc;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += o;
-  }
-  if (lane == 63) wsum[w] = incl;
-  for (int off = 32; off > 0; off >>= 1) dirty += __shfl_xor(dirty, off, 64);
+  if (threadIdx.x == 0) base_s = atomicAdd(&counters[0], (unsigned long long)n);
   __syncthreads();
-  int before = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i < w) before += wsum[i];
-    tot += wsum[i];
-  }
-  if (threadIdx.x == 0) base_s = atomicAdd(&counters[0], (unsigned long long)tot);
-  if (lane == 0 && dirty) atomicAdd(&counters[1], dirty);
-  // q_nch -> inclusive prefix over the queue (block-relative)
-  int run = before + incl - loc;
-  for (int i = i0; i < i1; ++i) {
-    run += q_nch[i];
-    q_nch[i] = run;
-  }
-  __syncthreads();
-  // chunk k of the block belongs to the first queued vertex whose prefix exceeds k:
-  // every thread writes a strided share, so a hub column with thousands of chunks
-  // (C5: ~5K per million-arc column) is not written by one thread
-  const u64 base = base_s;
-  for (int k = threadIdx.x; k < tot; k += 256) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (q_nch[mid] > k) hi = mid; else lo = mid + 1;
-    }
-    const int first = lo ? q_nch[lo - 1] : 0;
-    const u64 u = (u64)(q0 * 4 + q_slot[lo]);
-    chunks[base + k] = (u << 32) | (u64)(k - first);
-  }
+  for (int i = threadIdx.x; i < n; i += 256) chlist[base_s + i] = q_col[i];
 }
 
 // Frontier lists: consume the dirty flags the previous superstep's al[] scatter left
@@ -965,7 +939,10 @@ struct FrontierMarks {
 };
 static_assert(kSegArcs == 512, "unit of a position: (p - rp[row]) >> 9");
 
-__global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chunks,
+__global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ chlist,
+                                                    const uint4* __restrict__ chflag16, int64_t ngroups,
+                                                    const int32_t* __restrict__ cowner,
+                                                    const int64_t* __restrict__ cch,
                                                     const unsigned long long* __restrict__ counters,
                                                     unsigned long long* __restrict__ counters_next,
                                                     const int64_t* __restrict__ cptr,
@@ -984,50 +961,109 @@ __global__ __launch_bounds__(256) void k_al_scatter(const u64* __restrict__ chun
   // rows) and the per-position marks would cost more than they save.
   const bool all = rebuild || !frontier || (int64_t)counters[1] > fr_thr;
   if (blockIdx.x == 0 && threadIdx.x == 0) *fr_all_next = all ? 1 : 0;
-  if (rebuild) return;
-  const int64_t nchunks = (int64_t)counters[0];
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t c0 = wid * 64; c0 < nchunks; c0 += nw * 64) {
-    const int64_t c = c0 + lane;
-    int64_t b = 0;
-    int n = 0;
-    int32_t lab = 0;
-    if (c < nchunks) {
-      const u64 ch = chunks[c];
-      const int64_t u = (int64_t)(ch >> 32);
-      const int64_t rb = cptr[u], re = cptr[u + 1];
-      b = rb + (int64_t)(u32)ch * kChunkPos;
-      n = (int)min((int64_t)kChunkPos, re - b);
-      lab = Ln[u];
-      // frontier sync of a changed label into the next superstep's output vector
-      // (after the join; every changed vertex with local arcs has a chunk 0)
-      if ((u32)ch == 0u) Lold[u] = lab;
-    }
-    const int ns = n <= 16 ? n : 0;
-    for (int k = 0; k < ns; k += 4) {
-      uint32_t p[4];
+  // one-chunk columns from the list: a lane each, longer rows of positions by the wave
+  if (!rebuild) {
+    const int64_t nl = (int64_t)counters[0];
+    for (int64_t c0 = wid * 64; c0 < nl; c0 += nw * 64) {
+      const int64_t c = c0 + lane;
+      int64_t b = 0;
+      int n = 0;
+      int32_t lab = 0;
+      if (c < nl) {
+        const int64_t u = chlist[c];
+        b = cptr[u];
+        n = (int)(cptr[u + 1] - b);  // <= kChunkPos
+        lab = Ln[u];
+        Lold[u] = lab;  // frontier sync (after the join)
+      }
+      const int ns = n <= 16 ? n : 0;
+      for (int k = 0; k < ns; k += 4) {
+        uint32_t p[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) p[t] = k + t < ns ? cpos[b + k + t] : 0u;
+        for (int t = 0; t < 4; ++t) p[t] = k + t < ns ? cpos[b + k + t] : 0u;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        if (k + t < ns) {
-          al[p[t]] = lab;
-          if (!all) fm.mark(p[t]);
+        for (int t = 0; t < 4; ++t)
+          if (k + t < ns) {
+            al[p[t]] = lab;
+            if (!all) fm.mark(p[t]);
+          }
+      }
+      u64 big = __ballot(n > 16);
+      while (big) {
+        const int bl = __ffsll((unsigned long long)big) - 1;
+        big &= big - 1ull;
+        const int64_t bb = __shfl(b, bl, 64);
+        const int bn = __shfl(n, bl, 64);
+        const int32_t bv = __shfl(lab, bl, 64);
+        for (int i = lane; i < bn; i += 64) {
+          const uint32_t pp = cpos[bb + i];
+          al[pp] = bv;
+          if (!all) fm.mark(pp);
         }
+      }
     }
-    u64 big = __ballot(n > 16);
-    while (big) {
-      const int bl = __ffsll((unsigned long long)big) - 1;
-      big &= big - 1ull;
-      const int64_t bb = __shfl(b, bl, 64);
-      const int bn = __shfl(n, bl, 64);
-      const int32_t bv = __shfl(lab, bl, 64);
-      for (int i = lane; i < bn; i += 64) {
-        const uint32_t pp = cpos[bb + i];
-        al[pp] = bv;
-        if (!all) fm.mark(pp);
+  }
+  uint4* __restrict__ flw = const_cast<uint4*>(chflag16);
+  // multi-chunk columns: a wave takes 64 groups of 16 chunk flags, one group per lane,
+  // and clears them
+  for (int64_t g0 = wid * 64; g0 < ngroups; g0 += nw * 64) {
+    const int64_t gi = g0 + lane;
+    uint4 f = make_uint4(0u, 0u, 0u, 0u);
+    if (gi < ngroups) f = chflag16[gi];
+    const bool any = (f.x | f.y | f.z | f.w) != 0u;
+    if (any) flw[gi] = make_uint4(0u, 0u, 0u, 0u);
+    if (rebuild || __ballot(any) == 0ull) continue;  // the rebuild re-gathers every arc
+    u32 bits = 0u;
+    const u32 fw[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if ((fw[k >> 2] >> (8 * (k & 3))) & 0xFFu) bits |= 1u << k;
+    // every lane pops its next flagged chunk per round: chunks of <= 16 positions are
+    // written by their own lane, longer ones by the whole wave (coalesced cpos)
+    while (__ballot(bits != 0u)) {
+      int64_t b = 0;
+      int n = 0;
+      int32_t lab = 0;
+      if (bits) {
+        const int t = __ffs(bits) - 1;
+        bits &= bits - 1u;
+        const int64_t cid = gi * 16 + t;
+        const int64_t u = cowner[cid];
+        const int64_t kk = cid - cch[u];
+        b = cptr[u] + kk * kChunkPos;
+        n = (int)min((int64_t)kChunkPos, cptr[u + 1] - b);
+        lab = Ln[u];
+        // frontier sync of a changed label into the next superstep's output vector
+        // (after the join; every changed vertex with local arcs has a chunk 0)
+        if (kk == 0) Lold[u] = lab;
+      }
+      const int ns = n <= 16 ? n : 0;
+      for (int k = 0; k < ns; k += 4) {
+        uint32_t p[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) p[t] = k + t < ns ? cpos[b + k + t] : 0u;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (k + t < ns) {
+            al[p[t]] = lab;
+            if (!all) fm.mark(p[t]);
+          }
+      }
+      u64 big = __ballot(n > 16);
+      while (big) {
+        const int bl = __ffsll((unsigned long long)big) - 1;
+        big &= big - 1ull;
+        const int64_t bb = __shfl(b, bl, 64);
+        const int bn = __shfl(n, bl, 64);
+        const int32_t bv = __shfl(lab, bl, 64);
+        for (int i = lane; i < bn; i += 64) {
+          const uint32_t pp = cpos[bb + i];
+          al[pp] = bv;
+          if (!all) fm.mark(pp);
+        }
       }
     }
   }
@@ -1306,7 +1342,7 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
   const int64_t nq = (s1 + 3) / 4 - s0 / 4;
   hipLaunchKernelGGL(k_diff, dim3((unsigned)((nq + kDiffQuads - 1) / kDiffQuads)), dim3(256), 0, st,
                      (const int4*)Lc, (const int4*)Ln, sync ? const_cast<int32_t*>(Lc) : nullptr, s0, s1,
-                     g->cptr, g->chunks, g->counters + 4 * par);
+                     g->cptr, g->cch, g->chflag, g->chlist, g->counters + 4 * par);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -1329,7 +1365,8 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   fm.n_hub = g->n_hub;
   fm.rdirty = g->rdirty[par ^ 1];
   fm.udirty = g->udirty[par ^ 1];
-  hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chunks, ctr,
+  hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chlist, (const uint4*)g->chflag,
+                     (g->n_chunk_scan + 15) / 16, g->cowner, g->cch, ctr,
                      g->counters + 4 * (par ^ 1), g->cptr,
                      g->cpos, Ln, g->al, thr, fm, g->fr_all + (par ^ 1), g->frontier,
                      (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc));
