@@ -792,6 +792,14 @@ __device__ __forceinline__ void flag_chunks(uint8_t* __restrict__ chflag, const 
 // there; inside the concurrent tally the scatter does it).  int4 quads (vpad is a
 // multiple of 64), kDiffQuads per block; lanes outside the range masked (the
 // neighbouring slots may belong to a bin another stream is still computing).
+//
+// Frontier superstep (lists != nullptr and *fr_all == 0): only the rows listed for
+// bins [b0, b1) were re-tallied (every other row provably kept its label, and its
+// output slot already holds it), so the diff walks those lists -- grid-stride over
+// their concatenation -- instead of the slot range.
+struct BinBounds {
+  int64_t b[LPA_NBINS + 1];
+};
 constexpr int kDiffQuads = 2048;
 __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
                                               const int4* __restrict__ Ln4, int32_t* __restrict__ Lsync,
@@ -800,36 +808,56 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
                                               const int64_t* __restrict__ cch,
                                               uint8_t* __restrict__ chflag,
                                               int32_t* __restrict__ chlist,
-                                              unsigned long long* __restrict__ counters) {
+                                              unsigned long long* __restrict__ counters,
+                                              BinBounds bb, int b0, int b1,
+                                              const int32_t* __restrict__ flist,
+                                              const int32_t* __restrict__ fcnt,
+                                              const int32_t* __restrict__ fr_all) {
   __shared__ int32_t q_col[kDiffQuads * 4];
   __shared__ int qn;
   __shared__ unsigned long long base_s;
   const int lane = threadIdx.x & 63;
   if (threadIdx.x == 0) qn = 0;
   __syncthreads();
-  const int64_t q0 = s0 / 4 + (int64_t)blockIdx.x * kDiffQuads;
-  const int64_t q1 = min((s1 + 3) / 4, q0 + kDiffQuads);
   unsigned long long dirty = 0;
-  for (int64_t q = q0 + threadIdx.x; q < q1; q += 256) {
-    const int4 a = Lc4[q], b = Ln4[q];
-    int chg = (a.x != b.x) | ((a.y != b.y) << 1) | ((a.z != b.z) << 2) | ((a.w != b.w) << 3);
-    if (q * 4 < s0 || q * 4 + 4 > s1) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (q * 4 + k < s0 || q * 4 + k >= s1) chg &= ~(1 << k);
+  auto emit = [&](int64_t u, int32_t nb) {
+    if (Lsync) Lsync[u] = nb;
+    dirty += (unsigned long long)(cptr[u + 1] - cptr[u]);
+    const int64_t nch = cch[u + 1] - cch[u];
+    if (nch == 1) q_col[atomicAdd(&qn, 1)] = (int32_t)u;
+    else if (nch > 1) flag_chunks(chflag, cch, u);
+  };
+  if (flist != nullptr && *fr_all == 0) {
+    // a list holds at most its bin's rows, so the grid (sized for the slot range)
+    // gives each thread <= 32 entries, inside the block's queue
+    int64_t total = 0;
+    for (int b = b0; b < b1; ++b) total += fcnt[b];
+    const int32_t* Lc = reinterpret_cast<const int32_t*>(Lc4);
+    const int32_t* Ln = reinterpret_cast<const int32_t*>(Ln4);
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+      int64_t acc = 0;
+      int b = b0;
+      while (v >= acc + fcnt[b]) acc += fcnt[b++];
+      const int64_t u = flist[bb.b[b] + (v - acc)];
+      const int32_t nb = Ln[u];
+      if (Lc[u] != nb) emit(u, nb);
     }
-    if (chg) {
-      const int32_t nb[4] = {b.x, b.y, b.z, b.w};
+  } else {
+    const int64_t q0 = s0 / 4 + (int64_t)blockIdx.x * kDiffQuads;
+    const int64_t q1 = min((s1 + 3) / 4, q0 + kDiffQuads);
+    for (int64_t q = q0 + threadIdx.x; q < q1; q += 256) {
+      const int4 a = Lc4[q], b = Ln4[q];
+      int chg = (a.x != b.x) | ((a.y != b.y) << 1) | ((a.z != b.z) << 2) | ((a.w != b.w) << 3);
+      if (q * 4 < s0 || q * 4 + 4 > s1) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if ((chg >> k) & 1) {
-          const int64_t u = q * 4 + k;
-          if (Lsync) Lsync[u] = nb[k];
-          dirty += (unsigned long long)(cptr[u + 1] - cptr[u]);
-          const int64_t nch = cch[u + 1] - cch[u];
-          if (nch == 1) q_col[atomicAdd(&qn, 1)] = (int32_t)u;
-          else if (nch > 1) flag_chunks(chflag, cch, u);
-        }
+        for (int k = 0; k < 4; ++k)
+          if (q * 4 + k < s0 || q * 4 + k >= s1) chg &= ~(1 << k);
+      }
+      if (chg) {
+        const int32_t nb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((chg >> k) & 1) emit(q * 4 + k, nb[k]);
       }
     }
   }
@@ -849,11 +877,41 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
 // the consumed flags and zeroes the other parity's counts.  When every row is
 // tallied (*fr_all) the bin kernels take their ranges and the flags are left alone
 // (a stale flag only costs one redundant tally later).
-struct BinBounds {
-  int64_t b[LPA_NBINS + 1];
-};
 constexpr int kFcntUnits = LPA_NBINS;  // fcnt[] slot of the unit count
-constexpr int kListTile = 4096;        // flags per block (256 threads x 16)
+constexpr int kListSub = 8;            // 16-byte flag groups per thread, all loaded up front
+constexpr int kListTile = 256 * 16 * kListSub;  // flags per block (32 K: few global atomics per count)
+// bin of slot i from the block's bin bounds in LDS (binary search, 4 reads)
+__device__ __forceinline__ int flag_bin(const int64_t* sbb, int64_t i) {
+  int b = 0;
+#pragma unroll
+  for (int step = 8; step; step >>= 1)
+    if (b + step < LPA_NBINS && sbb[b + step] <= i) b += step;
+  return b;
+}
+// bit k set <=> byte k of the 16-byte group is non-zero
+__device__ __forceinline__ u32 nz_mask16(uint4 r) {
+  const u32 w[4] = {r.x, r.y, r.z, r.w};
+  u32 m = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    u32 t = w[q] | (w[q] >> 4);
+    t |= t >> 2;
+    t |= t >> 1;  // bit 8c set <=> byte c non-zero
+    m |= ((t & 1u) | ((t >> 7) & 2u) | ((t >> 14) & 4u) | ((t >> 21) & 8u)) << (4 * q);
+  }
+  return m;
+}
+// bits of the 16-flag group at i0 whose slots lie in [lo, hi)
+__device__ __forceinline__ u32 bin_bits(u32 m, int64_t i0, int64_t lo, int64_t hi) {
+  const int64_t a = lo - i0, c = hi - i0;
+  const u32 top = c >= 16 ? 0xFFFFu : (c <= 0 ? 0u : ((1u << c) - 1u));
+  const u32 bot = a <= 0 ? 0u : (a >= 16 ? 0xFFFFu : ((1u << a) - 1u));
+  return m & top & ~bot;
+}
+// The flags are sparse once the frontier is on (<= 0.5 % of the arcs dirty, in
+// practice ~0.2 % of the rows) and the kernel is latency-bound: 32 K flags per
+// block (few global atomics on the counter line), all loads in flight at once, and
+// for a tile inside one bin a block scan instead of per-flag LDS atomics.
 __global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rdirty, int64_t S,
                                                         uint8_t* __restrict__ udirty, int64_t nunits,
                                                         BinBounds bb, const int32_t* __restrict__ fr_all,
@@ -863,35 +921,99 @@ __global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rd
                                                         int32_t* __restrict__ fcnt_next,
                                                         int64_t nblk_rows) {
   __shared__ int32_t lcnt[LPA_NBINS + 1];
+  __shared__ int32_t lpos[LPA_NBINS + 1];
   __shared__ int32_t gbase[LPA_NBINS + 1];
+  __shared__ int64_t sbb[LPA_NBINS + 1];
   if (blockIdx.x == 0 && threadIdx.x < LPA_NBINS + 1) fcnt_next[threadIdx.x] = 0;
   if (*fr_all) return;  // uniform
   const bool units = (int64_t)blockIdx.x >= nblk_rows;
-  const int64_t n = units ? nunits : S;
+  const int64_t n = units ? nunits : S;   // flag arrays are padded to 16 bytes
   uint8_t* flags = units ? udirty : rdirty;
-  const int64_t i0 = ((units ? (int64_t)blockIdx.x - nblk_rows : (int64_t)blockIdx.x) * kListTile) +
-                     (int64_t)threadIdx.x * 16;
-  if (threadIdx.x < LPA_NBINS + 1) lcnt[threadIdx.x] = 0;
-  __syncthreads();
-  // 16 flags per thread (both flag arrays are padded to a multiple of 16 bytes)
-  uint4 raw = make_uint4(0u, 0u, 0u, 0u);
-  if (i0 < n) raw = *reinterpret_cast<const uint4*>(flags + i0);
-  const u32 wv[4] = {raw.x, raw.y, raw.z, raw.w};
-  int16_t rank[16];
-  uint8_t bin[16];
+  const int64_t t0 = (units ? (int64_t)blockIdx.x - nblk_rows : (int64_t)blockIdx.x) * kListTile;
+  if (threadIdx.x < LPA_NBINS + 1) {
+    lcnt[threadIdx.x] = 0;
+    lpos[threadIdx.x] = 0;
+    sbb[threadIdx.x] = bb.b[threadIdx.x];
+  }
+  // every group load in flight at once (coalesced 16-byte loads); set-flag masks kept
+  uint4 raw[kListSub];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    rank[k] = -1;
-    bin[k] = 0;
-    const int64_t i = i0 + k;
-    if (((wv[k >> 2] >> (8 * (k & 3))) & 0xFFu) && i < n) {
-      int b = kFcntUnits;
-      if (!units) {
-        b = 0;
-        while (b + 1 < LPA_NBINS && i >= bb.b[b + 1]) ++b;
+  for (int j = 0; j < kListSub; ++j) {
+    const int64_t i0 = t0 + (int64_t)j * 4096 + (int64_t)threadIdx.x * 16;
+    raw[j] = i0 < n ? *reinterpret_cast<const uint4*>(flags + i0) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  u32 msk[kListSub];
+  u32 anyw = 0;
+#pragma unroll
+  for (int j = 0; j < kListSub; ++j) {
+    const int64_t i0 = t0 + (int64_t)j * 4096 + (int64_t)threadIdx.x * 16;
+    u32 m = nz_mask16(raw[j]);
+    if (i0 + 16 > n) m = bin_bits(m, i0, 0, n);
+    msk[j] = m;
+    anyw |= m;
+  }
+  if (!__syncthreads_or(anyw != 0u)) return;  // no dirty flag in the tile (uniform)
+  // bins of the tile's first and last slot (independent scalar loads, no loop chain)
+  int bt0 = kFcntUnits, bt1 = kFcntUnits;
+  if (!units) {
+    const int64_t tl = min(t0 + kListTile, n) - 1;
+    bt0 = bt1 = 0;
+#pragma unroll
+    for (int k = 1; k < LPA_NBINS; ++k) {
+      bt0 += bb.b[k] <= t0;
+      bt1 += bb.b[k] <= tl;
+    }
+  }
+  if (bt0 == bt1) {
+    // the common case, a tile inside one bin: block scan of the per-thread counts,
+    // one global atomic, every lane writes its rows at its offset
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < kListSub; ++j) c += __popc(msk[j]);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += t;
+    }
+    __shared__ int wtot[4];
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      before += k < w ? wtot[k] : 0;
+      total += wtot[k];
+    }
+    if (threadIdx.x == 0) gbase[0] = atomicAdd(&fcnt[bt0], total);
+    __syncthreads();
+    if (!c) return;
+    int32_t pos = gbase[0] + before + incl - c;
+    int32_t* out = units ? ulist : flist + bb.b[bt0];
+#pragma unroll
+    for (int j = 0; j < kListSub; ++j) {
+      const u32 m = msk[j];
+      if (!m) continue;
+      const int64_t i0 = t0 + (int64_t)j * 4096 + (int64_t)threadIdx.x * 16;
+      for (u32 x = m; x; x &= x - 1u) out[pos++] = (int32_t)(i0 + __ffs(x) - 1);
+      *reinterpret_cast<uint4*>(flags + i0) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    return;
+  }
+  // a tile across a bin boundary (at most LPA_NBINS of them): per-lane bins,
+  // pass 1 counts per bin, pass 2 positions
+  if (anyw) {
+#pragma unroll
+    for (int j = 0; j < kListSub; ++j) {
+      const u32 m = msk[j];
+      if (!m) continue;
+      const int64_t i0 = t0 + (int64_t)j * 4096 + (int64_t)threadIdx.x * 16;
+      const int b0 = flag_bin(sbb, i0 + __ffs(m) - 1), b1 = flag_bin(sbb, i0 + 31 - __clz(m));
+      for (int b = b0; b <= b1; ++b) {
+        const int c = __popc(bin_bits(m, i0, sbb[b], sbb[b + 1]));
+        if (c) atomicAdd(&lcnt[b], c);
       }
-      bin[k] = (uint8_t)b;
-      rank[k] = (int16_t)atomicAdd(&lcnt[b], 1);
     }
   }
   __syncthreads();
@@ -900,16 +1022,22 @@ __global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rd
     gbase[threadIdx.x] = c ? atomicAdd(&fcnt[threadIdx.x], c) : 0;
   }
   __syncthreads();
+  if (!anyw) return;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    if (rank[k] >= 0) {
-      const int b = bin[k];
-      const int32_t pos = gbase[b] + rank[k];
-      if (units) ulist[pos] = (int32_t)(i0 + k);
-      else flist[bb.b[b] + pos] = (int32_t)(i0 + k);
+  for (int j = 0; j < kListSub; ++j) {
+    const u32 m = msk[j];
+    if (!m) continue;
+    const int64_t i0 = t0 + (int64_t)j * 4096 + (int64_t)threadIdx.x * 16;
+    const int b0 = flag_bin(sbb, i0 + __ffs(m) - 1), b1 = flag_bin(sbb, i0 + 31 - __clz(m));
+    for (int b = b0; b <= b1; ++b) {
+      const u32 mb = bin_bits(m, i0, sbb[b], sbb[b + 1]);
+      if (!mb) continue;
+      int32_t pos = gbase[b] + atomicAdd(&lpos[b], __popc(mb));
+      int32_t* out = flist + sbb[b];
+      for (u32 x = mb; x; x &= x - 1u) out[pos++] = (int32_t)(i0 + __ffs(x) - 1);
     }
+    *reinterpret_cast<uint4*>(flags + i0) = make_uint4(0u, 0u, 0u, 0u);
   }
-  if ((raw.x | raw.y | raw.z | raw.w) && i0 < n) *reinterpret_cast<uint4*>(flags + i0) = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // rebuild al[] when the changed vertices touch more than `thr` arcs (host-set)
@@ -1180,7 +1308,7 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
 // tails of the small bins.  bev (nullable): events 2k / 2k+1 bracket tally kernel
 // k on its own stream (0 units, 1 hub combine, 2..11 bins w8 .. g1).
 int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* Ln, int64_t s0,
-                int64_t s1, bool sync, int par);
+                int64_t s1, bool sync, int par, int b0 = 0, int b1 = 0);
 
 // diff (P = 1, concurrent schedule): each stream diffs the slots its own bins
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
@@ -1281,9 +1409,9 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_TRY(mark(3, s));
   if (diff) {
     // inside the concurrent tally: no Lc sync here, the scatter refresh does it
-    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2], false, g->par));
-    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], g->vpad, false, g->par));
-    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par));
+    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2], false, g->par, BIN_W16, BIN_W2));
+    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], g->vpad, false, g->par, BIN_W2, BIN_ISO));
+    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par, BIN_SEG, BIN_W16));
   }
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_join[0], sb));
@@ -1337,12 +1465,18 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
 // changed slots in [s0, s1) -> position chunks + dirty-arc count (counters of this
 // superstep's parity)
 int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* Ln, int64_t s0,
-                int64_t s1, bool sync, int par) {
+                int64_t s1, bool sync, int par, int b0, int b1) {
   if (s1 <= s0) return LPA_OK;
   const int64_t nq = (s1 + 3) / 4 - s0 / 4;
+  BinBounds bnd;
+  for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = g->bin_begin[b];
+  // bins [b0, b1) given: the frontier list mode is available (the concurrent tally
+  // of this superstep; its lists are those of g->par)
+  const bool lists = b1 > b0;
   hipLaunchKernelGGL(k_diff, dim3((unsigned)((nq + kDiffQuads - 1) / kDiffQuads)), dim3(256), 0, st,
                      (const int4*)Lc, (const int4*)Ln, sync ? const_cast<int32_t*>(Lc) : nullptr, s0, s1,
-                     g->cptr, g->cch, g->chflag, g->chlist, g->counters + 4 * par);
+                     g->cptr, g->cch, g->chflag, g->chlist, g->counters + 4 * par, bnd, b0, b1,
+                     lists ? g->flist : nullptr, g->fcnt + 16 * g->par, g->fr_all + g->par);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }

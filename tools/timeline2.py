@@ -25,7 +25,7 @@ for r in rows:
         steps[-1].append((n, int(r['Start_Timestamp']), int(r['End_Timestamp']), r.get('Queue_Id', '')))
 spans = [(s[-1][2] - s[0][1]) / 1e6 for s in steps]
 print('supersteps:', len(steps))
-print('spans ms:', ' '.join(f"{x:.3f}" for x in spans[:40]))
+print('spans ms:', ' '.join(f"{x:.3f}" for x in spans[:80]))
 for idx in [int(x) for x in sys.argv[2:]]:
     s = steps[idx]
     t0 = s[0][1]
