@@ -136,6 +136,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_HUB_WAVES")) g->hub_waves = atoi(f) == 4 ? 4 : 8;
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
+  if (const char* f = getenv("LPA_FRONTIER_FRAC")) g->frontier_frac = atof(f);
+  if (const char* f = getenv("LPA_MID_MERGED")) g->mid_merged = atoi(f) ? 1 : 0;
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {

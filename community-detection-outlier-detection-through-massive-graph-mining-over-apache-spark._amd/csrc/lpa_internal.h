@@ -42,6 +42,7 @@ constexpr int kChunkPos = 256;        // arc positions per scatter chunk of a ch
 // replicated-label refresh: scatter the changed vertices' labels while they touch at
 // most this fraction of the arcs, otherwise rebuild al[] with one gather pass
 constexpr double kRebuildFrac = 0.25;
+constexpr double kFrontierFrac = 0.005;  // default of lpa_graph::frontier_frac
 
 struct Segment {   // one unit of a seg-bin row
   int64_t begin;  // first arc (local CSR index)
@@ -165,6 +166,9 @@ struct lpa_graph {
   int32_t* ulist = nullptr;       // [n_segs] dirty hub units of this superstep
   int32_t* fcnt = nullptr;        // [2][16] per parity: list lengths (bins 0..12, units at 13)
   int frontier = 1;               // LPA_FRONTIER / lpa_set_frontier
+  // the al[] scatter marks dirty rows while <= this fraction of the arcs changed;
+  // above it the next superstep tallies every row (LPA_FRONTIER_FRAC overrides)
+  double frontier_frac = lpa::kFrontierFrac;
 
   // replicated neighbour labels (GraphX ReplicatedVertexView analogue):
   // al[i] = L_cur[col[i]]; kept current by scatter (few changes) or rebuild
@@ -186,6 +190,7 @@ struct lpa_graph {
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   hipGraphExec_t gexec[4] = {};             // captured converged superstep per (cur, par)
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
+  int mid_merged = 1;                       // LPA_MID_MERGED=0: the three mid tiers as separate launches
   int hub_waves = 8;                        // LPA_HUB_WAVES: waves per block of the 8K-slot hub combine (4 or 8)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 

@@ -72,9 +72,6 @@ namespace {
 // launch_hub_combine)
 constexpr int kDenseSupersteps = 2;
 
-// frontier: mark the rows the al[] scatter makes dirty while <= this fraction of the
-// arcs changed; above it the next superstep tallies every row
-constexpr double kFrontierFrac = 0.005;
 
 constexpr int kChunks = 8;    // 64-arc chunks per wave: a wave-bin row / a quarter segment
 constexpr u32 kNone = 0xFFFFFFFFu;  // empty lane
@@ -1503,7 +1500,7 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
                      (g->n_chunk_scan + 15) / 16, g->cowner, g->cch, ctr,
                      g->counters + 4 * (par ^ 1), g->cptr,
                      g->cpos, Ln, g->al, thr, fm, g->fr_all + (par ^ 1), g->frontier,
-                     (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc));
+                     (int64_t)(g->frontier_frac * (double)g->arcs), const_cast<int32_t*>(Lc));
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
