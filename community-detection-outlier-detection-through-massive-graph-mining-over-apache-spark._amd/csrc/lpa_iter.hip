@@ -42,6 +42,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "lpa_internal.h"
 
 // LPA_TRACE (diagnostic build only): synchronise and log after every kernel
@@ -1514,6 +1516,29 @@ int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool 
   return launch_refresh(g, Lc, Ln, diff_done, par);
 }
 
+// Capture `body` (launches on the handle's stream and the streams it forks) into an
+// executable graph.  Captures are serialised process-wide (several handles of one
+// process, e.g. virtual ranks driven from threads, crashed capturing at once).
+template <typename Body>
+int capture_graph(lpa_graph* g, hipGraphExec_t* out, Body body) {
+  static std::mutex capture_mu;
+  std::lock_guard<std::mutex> lk(capture_mu);
+  hipStream_t s = g->stream;
+  hipGraph_t graph = nullptr;
+  LPA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+  const int rc = body();
+  hipError_t ec = hipStreamEndCapture(s, &graph);
+  if (rc != LPA_OK) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  LPA_HIP(ec);
+  ec = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  LPA_HIP(ec);
+  return LPA_OK;
+}
+
 int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
   hipStream_t s = g->stream;
   const bool timed = st != nullptr;
@@ -1546,18 +1571,12 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // the label / counter buffers, so there is one per (cur, par) state.
     if (g->use_graphs && g->nranks == 1 && !g->serial && g->since_reset >= kDenseSupersteps) {
       const int key = g->cur * 2 + g->par;
-      if (!g->gexec[key]) {
-        hipGraph_t graph = nullptr;
-        LPA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
-        int rc = launch_tally(g, Lown, nullptr, Lc, Ln, true);
-        if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true, g->par);
-        hipError_t ec = hipStreamEndCapture(s, &graph);
-        if (rc != LPA_OK) return rc;
-        LPA_HIP(ec);
-        ec = hipGraphInstantiate(&g->gexec[key], graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        LPA_HIP(ec);
-      }
+      if (!g->gexec[key])
+        LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
+          int rc = launch_tally(g, Lown, nullptr, Lc, Ln, true);
+          if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true, g->par);
+          return rc;
+        }));
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
       if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
       g->cur ^= 1;
@@ -1565,7 +1584,22 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       ++g->since_reset;
       continue;
     }
-    LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
+    if (g->use_graphs && g->nranks > 1 && g->loop == nullptr && !g->serial &&
+        g->since_reset >= kDenseSupersteps) {
+      // P > 1: the tally (no collective inside) replays a captured graph per
+      // (cur, par); the exchange, whose delta size the host reads, and the refresh
+      // follow on the stream.  Not for a loopback group: its ranks are threads of one
+      // process, and a capture on one rank's stream while another rank's thread waits
+      // on the group's events fails in the runtime ("dependency created on uncaptured
+      // work", P = 8) -- one process per GPU (RCCL) never has two handles.
+      const int key = g->cur * 2 + g->par;
+      if (!g->gexec[key])
+        LPA_TRY(capture_graph(g, &g->gexec[key],
+                              [&]() -> int { return launch_tally(g, Lown, nullptr, Lc, Ln, diff_in_tally); }));
+      LPA_HIP(hipGraphLaunch(g->gexec[key], s));
+    } else {
+      LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
+    }
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
     bool changes_listed = false;
     if (g->nranks > 1 && has_collective(g))

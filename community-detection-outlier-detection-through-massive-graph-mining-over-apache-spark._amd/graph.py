@@ -241,18 +241,20 @@ class Loopback:
 
 def run_ranks(graphs, fn):
     """Call ``fn(rank, graph)`` for every rank of a loopback group on its own thread;
-    returns the results in rank order, re-raising the first failure (after aborting
-    the group so no thread stays blocked in a collective)."""
+    returns the results in rank order, re-raising the first failure in time (after
+    aborting the group so no thread stays blocked in a collective)."""
     import threading
 
     res = [None] * len(graphs)
-    err = [None] * len(graphs)
+    errs = []   # in the order the ranks failed: the first is the cause, the rest
+    lock = threading.Lock()   # are peers released by the abort
 
     def work(r):
         try:
             res[r] = fn(r, graphs[r])
         except BaseException as e:  # noqa: BLE001 -- re-raised below
-            err[r] = e
+            with lock:
+                errs.append(e)
             lb = graphs[r]._loopback
             if lb is not None:
                 lb.abort()
@@ -262,9 +264,8 @@ def run_ranks(graphs, fn):
         t.start()
     for t in th:
         t.join()
-    for e in err:
-        if e is not None:
-            raise e
+    if errs:
+        raise errs[0]
     return res
 
 

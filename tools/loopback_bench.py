@@ -1,0 +1,47 @@
+"""P in-process ranks on ONE GPU (loopback collective): wall time of supersteps
+2..10 of labelPropagation(10), all ranks' handles driven from their own threads.
+Measures the multi-rank control path (exchange, host syncs, launches), not scaling.
+
+    python tools/loopback_bench.py [P] [scale] [reps]
+"""
+import sys
+import time
+
+sys.path.insert(0, ".")
+import graphframes_amd as gfa  # noqa: E402
+import torch  # noqa: E402
+
+P = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+scale = int(sys.argv[2]) if len(sys.argv) > 2 else 22
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+V = 1 << scale
+s, d = gfa.gen_rmat(scale, 16, seed=1)
+lb = gfa.Loopback(P)
+gs = [gfa.Graph(s, d, V, rank=r, loopback=lb) for r in range(P)]
+del s, d
+torch.cuda.empty_cache()
+
+
+def one(r, g):
+    g.reset()
+    g.step(1)
+    torch.cuda.synchronize()
+    return None
+
+
+ts = []
+for k in range(reps + 1):
+    gfa.run_ranks(gs, one)
+    t0 = time.perf_counter()
+    gfa.run_ranks(gs, lambda r, g: g.step(9))
+    torch.cuda.synchronize()
+    if k:
+        ts.append(time.perf_counter() - t0)
+ts.sort()
+med = ts[len(ts) // 2]
+info = gs[0].info()
+print(f"P={P} scale={scale}: supersteps 2..10 median {med * 1e3:.2f} ms "
+      f"({med / 9 * 1e3:.3f} ms/superstep), exchanges full {info['exchanges_full']} delta {info['exchanges_delta']}")
+for g in gs:
+    g.close()
+lb.close()

@@ -65,6 +65,29 @@ __global__ __launch_bounds__(1024) void k_hot(const int32_t* __restrict__ col, i
     }
   }
 }
+template <int kHot, int kMode>
+__global__ __launch_bounds__(1024) void k_hot_nt(const int32_t* __restrict__ col, int64_t arcs, const int32_t* __restrict__ L,
+                                                 int32_t* __restrict__ al, int32_t cold) {
+  __shared__ int32_t hot[kHot];
+  for (int i = threadIdx.x; i < kHot; i += 1024) hot[i] = L[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512; base + 512 <= arcs; base += nw * 512) {
+    int32_t c[8], r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + base + k * 64 + lane);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int32_t x = c[k];
+      if (x < kHot) r[k] = hot[x];
+      else if (kMode == 1 ? x >= cold : true) r[k] = __builtin_nontemporal_load(L + x);
+      else r[k] = L[x];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
+  }
+}
 // columns sorted inside each row (rows = degree runs, rank order)
 __global__ void k_row_bounds(const int64_t* cdeg, int64_t V, int64_t* rows_off) {}
 
@@ -136,6 +159,13 @@ int main(int argc, char** argv) {
   timeit("hot LDS 40960 (NT) [shipped]", [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
   timeit("hot LDS 40960 (cached streams)", [&] { hipLaunchKernelGGL((k_hot<40960, false>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
   timeit("hot LDS, 2 blocks/CU grid", [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(2 * cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
+  timeit("hot LDS, all gathers NT", [&] { hipLaunchKernelGGL((k_hot_nt<40960, 2>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0); });
+  for (int32_t T : {1 << 19, 1 << 20, 1 << 21, 1 << 22}) {
+    if (T >= V) continue;
+    char nm[80];
+    snprintf(nm, 80, "hot LDS, NT gathers for col >= %d", T);
+    timeit(nm, [&] { hipLaunchKernelGGL((k_hot_nt<40960, 1>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, T); });
+  }
   for (int32_t T : {1 << 20, 1 << 22, 1 << 23}) {
     if (T >= V) continue;
     char nm[80];
