@@ -333,6 +333,46 @@ __device__ __forceinline__ BinRows bin_rows(int64_t vbeg, int64_t vend, const in
   return br;
 }
 
+// Mode of each G-lane group's labels (one label per lane, kNone = empty) by sorting:
+// a bitonic network across the group's lanes (log2 G (log2 G + 1) / 2 exchange
+// stages; a group's direction may come out descending, which leaves equal labels
+// contiguous all the same), then run lengths from the ballot of run starts, then a
+// group max of the run tally words.  Every lane of a group returns its group's word.
+// The ballot peel costs one dependent round per distinct label; in the label-dense
+// supersteps a 32-lane row holds ~20-30 distinct labels, where the fixed ~15-stage
+// network is several times cheaper.
+template <int G>
+__device__ __forceinline__ u64 group_mode_sort(u32 v, int lane) {
+  static_assert(G >= 2 && G <= 64 && (G & (G - 1)) == 0, "group width");
+#pragma unroll
+  for (int k = 2; k <= G; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const u32 o = (u32)__shfl_xor((int)v, j, 64);
+      const bool up = (lane & k) == 0, low = (lane & j) == 0;
+      v = (low == up) ? (v < o ? v : o) : (v > o ? v : o);
+    }
+  }
+  const int gj = lane & (G - 1);
+  const int gbase = lane - gj;
+  const u32 prev = (u32)__shfl_up((int)v, 1, 64);
+  const bool start = gj == 0 || v != prev;
+  const u64 bm = __ballot(start);
+  const u64 above = lane == 63 ? 0ull : (bm & ~((2ull << lane) - 1ull));
+  int nxt = above ? __ffsll((unsigned long long)above) - 1 : 64;
+  nxt = nxt < gbase + G ? nxt : gbase + G;
+  u64 w = (start && v != kNone) ? tally((u32)(nxt - lane), v) : 0ull;
+#pragma unroll
+  for (int off = G >> 1; off > 0; off >>= 1) {
+    const u64 o = ((u64)(u32)__shfl_xor((int)(u32)(w >> 32), off, 64) << 32) |
+                  (u64)(u32)__shfl_xor((int)(u32)w, off, 64);
+    w = umax64(w, o);
+  }
+  return w;
+}
+// peel rounds after which a chunk whose groups are still unresolved is sorted instead
+constexpr int kPeelSortAfter = 3;
+
 // G lanes per row (G <= 64, all 64 lanes of the wave call it: ballot peel)
 template <int G>
 __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
@@ -355,7 +395,11 @@ __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const 
     const u64 gm = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
     u64 act = __ballot(lab != kNone);
     u64 best = 0ull;
-    while (act) {
+    for (int round = 0; act; ++round) {
+      if (G >= 8 && round == kPeelSortAfter) {  // uniform: a label-dense chunk
+        best = group_mode_sort<G>(lab, lane);
+        break;
+      }
       const u64 my = (act >> gbase) & gm;
       const int lead = gbase + (my ? (__ffsll((unsigned long long)my) - 1) : 0);
       const u32 x = (u32)__shfl((int)lab, lead, 64);
@@ -612,7 +656,11 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       const u32 lb = lab[c];
       u64 act = __ballot(lb != kNone);
       u64 best = 0ull;
-      while (act) {
+      for (int round = 0; act; ++round) {
+        if (round == kPeelSortAfter) {  // uniform: a label-dense chunk
+          best = group_mode_sort<G>(lb, lane);
+          break;
+        }
         const u64 my = (act >> gbase) & gm;
         const int lead = gbase + (my ? (__ffsll((unsigned long long)my) - 1) : 0);
         const u32 x = group_lead<G>(lb, act, lane, lead);
