@@ -31,8 +31,11 @@ constexpr int kBinMaxDeg[LPA_NBINS] = {1 << 30, 1024, 512, 256, 128, 64, 32, 16,
 constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 64 < deg <= 512
 constexpr int kWideMaxDeg = 1024;     // ... and (w16, 16 chunks, 2048-slot table) up to 1024
 constexpr int kSegArcs = 512;         // arcs per unit of a seg-bin row (one wave)
-constexpr int kTallyEv = 2 * (LPA_NKERNELS - 1);  // events bracketing each tally kernel
-constexpr int kBinEvents = kTallyEv + 3;           // + join, exchange, refresh marks
+constexpr int kTallyKernels = 13;                  // stats kernels 0..12: the tally
+constexpr int kTallyEv = 2 * kTallyKernels;        // events bracketing each tally kernel
+// + join, after exchange, after scatter, after rebuild, lists start, lists end
+constexpr int kBinEvents = kTallyEv + 6;
+static_assert(LPA_NKERNELS == kTallyKernels + 3, "stats: tally kernels + refresh, rebuild, lists");
 constexpr int kCombWords = 2048;      // expected staged words per combine bucket
 constexpr int kCombSlots = 8192;      // LDS table slots of a combine block
 constexpr int kCombDirect = 6144;     // <= this many staged words: one block, no buckets

@@ -1370,6 +1370,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   const int32_t* fr_all = g->fr_all + g->par;
   int32_t* fcnt = g->fcnt + 16 * g->par;
   // frontier lists of this superstep (no-op when every row is tallied)
+  if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 4], s));
   {
     BinBounds bnd;
     for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = bb[b];
@@ -1380,6 +1381,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
                        g->fcnt + 16 * (g->par ^ 1), nbr);
     LPA_HIP(hipGetLastError());
   }
+  if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
     LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
@@ -1531,7 +1533,8 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // refresh al[] for L_next (after the exchange, so every rank sees all changes) of the
 // superstep of parity `par`; diff_done: the tally schedule already ran the diff per
 // stream (launch_tally) or the exchange listed the changes
-int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par) {
+int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par,
+                   hipEvent_t ev_scatter = nullptr) {
   if (g->arcs == 0) return LPA_OK;
   hipStream_t s = g->stream;
   // this superstep's counters (zeroed by the previous k_al_scatter or at build)
@@ -1553,6 +1556,7 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
                      (int64_t)(g->frontier_frac * (double)g->arcs), const_cast<int32_t*>(Lc));
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
+  if (ev_scatter) LPA_HIP(hipEventRecord(ev_scatter, s));  // profiling: scatter | rebuild
   LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
   LPA_HIP(hipGetLastError());
   return LPA_OK;
@@ -1600,8 +1604,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS], s));
   }
   // per timed superstep t, bin_ev[t*kBinEvents + i]: 2k / 2k+1 around tally kernel
-  // k (k < LPA_NKERNELS - 1), then kTallyEv after the join, +1 after the exchange,
-  // +2 after the refresh
+  // k (k < kTallyKernels), then kTallyEv after the join, +1 after the exchange, +2
+  // after the diff + scatter, +3 after the rebuild, +4 / +5 around the frontier lists
   for (int32_t t = 0; t < n; ++t) {
     const int32_t* Lc = g->lab[g->cur];
     int32_t* Ln = g->lab[g->cur ^ 1];
@@ -1656,9 +1660,11 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // P > 1 without a communicator: the caller completes the superstep with
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
     // (changes + refresh); a refresh here would see a partial vector
+    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));  // stays if there is no refresh
     if (g->nranks == 1 || has_collective(g))
-      LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par));
-    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));
+      LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par,
+                             bev ? bev[kTallyEv + 2] : nullptr));
+    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 3], s));
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     g->cur ^= 1;
     g->par ^= 1;
@@ -1685,14 +1691,18 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       if (!g->serial) continue;  // per-kernel times: serialized schedule only
       hipEvent_t* bev = &g->bin_ev[t * kBinEvents];
       float ms;
-      for (int k = 0; k < LPA_NKERNELS - 1; ++k) {
+      for (int k = 0; k < kTallyKernels; ++k) {
         LPA_HIP(hipEventElapsedTime(&ms, bev[2 * k], bev[2 * k + 1]));
         st->kernel_ms[k] += ms;
       }
       LPA_HIP(hipEventElapsedTime(&ms, bev[kTallyEv], bev[kTallyEv + 1]));
       st->exchange_ms += ms;
       LPA_HIP(hipEventElapsedTime(&ms, bev[kTallyEv + 1], bev[kTallyEv + 2]));
-      st->kernel_ms[LPA_NKERNELS - 1] += ms;
+      st->kernel_ms[kTallyKernels] += ms;
+      LPA_HIP(hipEventElapsedTime(&ms, bev[kTallyEv + 2], bev[kTallyEv + 3]));
+      st->kernel_ms[kTallyKernels + 1] += ms;
+      LPA_HIP(hipEventElapsedTime(&ms, bev[kTallyEv + 4], bev[kTallyEv + 5]));
+      st->kernel_ms[kTallyKernels + 2] += ms;
     }
     float tot;
     LPA_HIP(hipEventElapsedTime(&tot, g->ev[2 * LPA_STATS_MAX_ITERS], g->ev[2 * LPA_STATS_MAX_ITERS + 1]));
