@@ -6,17 +6,22 @@
 //     L_next[v] = min{ l : cnt_v(l) = max_l' cnt_v(l') },  cnt_v(l) = #{arcs v->u : L_cur[u] = l}
 //
 // Data flow of a superstep (one handle = one rank's slice of the degree-sorted CSR):
+//   0. lists    the rows (and hub units) the previous refresh marked dirty -> per-bin
+//               row lists (k_frontier_lists); none after L0, a rebuild or many changes
 //   1. tally    every arc's vote comes from al[i] = L_cur[col[i]], the replicated
 //               neighbour label (GraphX ReplicatedVertexView: edge partitions hold
 //               copies of the endpoint attributes).  al[] is STREAMED (coalesced,
-//               non-temporal), so the dense superstep has no random gathers.
-//   2. exchange (P > 1) RCCL allgather of the owned label slices.
-//   3. refresh  diff L_next vs L_cur over all vertex slots; the changed vertices'
-//               new labels are scattered into al[] through the CSC position index
-//               (cptr/cpos) while they touch <= rebuild_frac of the arcs, otherwise
-//               al[] is rebuilt with one gather pass al[i] = L_next[col[i]].
-//   Every superstep tallies every arc of every vertex; the refresh only keeps the
-//   replica exact, so labels are bit-identical to the plain gather formulation.
+//               non-temporal), so the tally has no random gathers.  With a frontier
+//               only the listed rows are tallied: a row none of whose neighbours
+//               changed keeps its label (exact, see lpa_internal.h).
+//   2. exchange (P > 1) allgather of the owned label slices or of the changes.
+//   3. refresh  the changed vertices (k_diff, or the exchange's change list) have
+//               their new labels scattered into al[] through the CSC position index
+//               (cptr/cpos) while they touch <= rebuild_frac of the arcs -- marking the
+//               rows they dirty while <= frontier_frac -- otherwise al[] is rebuilt with
+//               one gather pass al[i] = L_next[col[i]].
+//   The refresh keeps the replica exact, so labels are bit-identical to the plain
+//   gather formulation.
 //
 // A vote tally is packed into one 64-bit word  (count << 32) | ~label : the
 // maximum word is the highest count and, among equal counts, the smallest label,
@@ -29,15 +34,12 @@
 //   g2   deg == 2       min of the two labels (1-1 tie or equal)
 //   g4 .. g64 deg <= G  G lanes per vertex, ballot "peel": each round takes the
 //                       group's first unresolved label, counts its lanes with one
-//                       64-bit ballot, retires them (rounds = distinct labels)
-//   w2/w4/w8 deg <= 64*NC  one wave per vertex, NC chunks: cross-chunk peel in
-//                       registers; a row the peel does not resolve completely goes
-//                       through a per-wave LDS hash (64-bit CAS/add)
-//   seg  deg > 512      one 256-thread block per <= 2048-arc segment, block LDS hash;
-//                       single-segment rows finish in-block, longer rows merge their
-//                       segment tallies into a per-vertex global hash (batched 64-bit
-//                       device atomics) that k_lpa_hub_final reduces in 2048-entry
-//                       chunks (so one giant hub is spread over many blocks)
+//                       64-bit ballot, retires them; a chunk still unresolved after
+//                       3 rounds (label-dense) sorts each group's lanes instead
+//   w2..w16 deg <= 64*NC  one wave per vertex, NC chunks: cross-chunk peel in
+//                       registers, the residual through a per-wave LDS hash
+//   seg  deg > 1024     one wave per 512-arc unit (staged unit tally words), merged
+//                       per row by the hub combine (lpa_hub.hip)
 // Tables keep a touched-slot list: finishing a vertex costs O(distinct labels).
 #include <stdio.h>
 #include <string.h>
