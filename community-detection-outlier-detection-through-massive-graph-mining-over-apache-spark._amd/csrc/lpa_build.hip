@@ -283,6 +283,7 @@ int init_labels(lpa_graph* g) {
   LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 8, g->stream));
   g->cur = 0;
   g->since_reset = 0;
+  g->force_all_next = false;
   g->prev_delta_ok = false;  // the exchange's delta chain restarts from L0
   return rebuild_arc_labels(g);
 }
@@ -531,6 +532,10 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     LPA_HIP(hipFree(nseg));
     LPA_TRY(dev_alloc(g, (void**)&g->ucnt, sizeof(int32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
     g->hub_uoff = seg_off;  // the seg bin is exactly the hub rows (deg > kSegArcs)
+    // first unit of the k_lpa_block rows
+    LPA_HIP(hipMemcpyAsync(&g->unit_lane_begin, seg_off + g->hub_lane_begin, sizeof(int64_t),
+                           hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
     g->device_bytes += (int64_t)sizeof(int64_t) * (n0 + 1);
   }
   LPA_HIP(hipFree(deg_own));

@@ -37,7 +37,7 @@ constexpr int kSmallWords = 512;    // k_hub_small capacity (8 chunks x 64 lanes
 constexpr int kSmallSlots = 1024;   // its per-wave LDS table
 constexpr int kChunkUnits = 8;      // units per k_hub_count / k_hub_scatter work item
 constexpr int kPeelRounds = 8;
-constexpr int kLaneUnits = 8;       // k_hub_lanes: rows of <= 8 units (deg <= 4096)
+constexpr int kLaneUnits = kBlockMaxDeg / kSegArcs;  // k_hub_lanes / k_lpa_block rows: <= 8 units
 
 __device__ __forceinline__ u32 comb_bucket(u32 label, int lg) {
   return lg == 0 ? 0u : (label * 0x85EBCA77u) >> (32 - lg);
@@ -1083,7 +1083,7 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
     LPA_HIP(hipStreamWaitEvent(sd, g->ev_fork2, 0));
     LPA_TRY(bucket_path());
   }
-  if (hl < n) {
+  if (hl < n && !block_mode_now(g)) {  // block mode: k_lpa_block tallied these rows
     hipLaunchKernelGGL(k_hub_lanes, dim3(grid_cap((n - hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
                        g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, lists, n, g->hub_wcount, lcnt,
                        g->flist, g->fcnt + 16 * g->par, g->fr_all + g->par);

@@ -31,6 +31,7 @@ constexpr int kBinMaxDeg[LPA_NBINS] = {1 << 30, 1024, 512, 256, 128, 64, 32, 16,
 constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 64 < deg <= 512
 constexpr int kWideMaxDeg = 1024;     // ... and (w16, 16 chunks, 2048-slot table) up to 1024
 constexpr int kSegArcs = 512;         // arcs per unit of a seg-bin row (one wave)
+constexpr int kBlockMaxDeg = 4096;    // seg rows up to this degree: k_lpa_block in the label-dense supersteps
 constexpr int kTallyKernels = 13;                  // stats kernels 0..12: the tally
 constexpr int kTallyEv = 2 * kTallyKernels;        // events bracketing each tally kernel
 // + join, after exchange, after scatter, after rebuild, lists start, lists end
@@ -147,6 +148,10 @@ struct lpa_graph {
   int32_t* hub_lcnt = nullptr;    // [2][8] per parity, queue lengths: mid1, bucketed, bucket items,
                                   //   chunk items, wave path, mid2, mid3, small (list S)
   int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
+  int block_rows = 1;             // LPA_BLOCK=0: label-dense supersteps also stage the rows above by units
+  int block_at = 0;               // LPA_BLOCK_AT: k_lpa_block before (0) or after (1) k_lpa_units
+  int64_t unit_lane_begin = 0;    // hub_uoff[hub_lane_begin]
+  bool force_all_next = false;    // the next superstep tallies every row (after block mode)
   lpa::u64* items_cb = nullptr;   // [n_hub_buckets] (hub << 32 | bucket)
   lpa::u64* items_cc = nullptr;   // [n_hub_chunks]  (hub << 32 | 8-unit chunk)
   int64_t n_hub_buckets = 0, n_hub_chunks = 0;
@@ -240,6 +245,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
 int init_labels(lpa_graph* g);
 int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
 int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork);  // lpa_hub.hip
+bool block_mode_now(const lpa_graph* g);  // lpa_iter.hip
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
 int frontier_all(lpa_graph* g, int par);  // next tally of parity `par` takes every row
 

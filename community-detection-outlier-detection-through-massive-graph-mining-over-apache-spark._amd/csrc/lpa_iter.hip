@@ -76,6 +76,17 @@ namespace {
 // launch_hub_combine)
 constexpr int kDenseSupersteps = 2;
 
+}  // namespace
+
+// the label-dense supersteps tally the rows [hub_lane_begin, n_hub) with k_lpa_block
+// and skip their units; the superstep after them tallies every row (their units'
+// staged words are stale)
+bool block_mode_now(const lpa_graph* g) {
+  return g->block_rows && g->since_reset < kDenseSupersteps && g->hub_lane_begin < g->n_hub;
+}
+
+namespace {
+
 
 constexpr int kChunks = 8;    // 64-arc chunks per wave: a wave-bin row / a quarter segment
 constexpr u32 kNone = 0xFFFFFFFFu;  // empty lane
@@ -244,13 +255,14 @@ __device__ __forceinline__ void peel_batch(Batch<NC>& bt, const u32 (&lab)[NC], 
   bt.any = __ballot(mask != 0u) != 0ull;
 }
 
-template <int NC>
+// kList = false: a shared (block) table scanned at the end, no touched-slot list
+template <int NC, bool kList = true>
 __device__ __forceinline__ void hash_batch(u64* tab, uint16_t* lst, int& cnt, int shift, u32 mask,
                                            const Batch<NC>& bt, const u32 (&lab)[NC], int nch,
                                            int lane, u64 lt) {
   int pslot = -1;
   if (lane < bt.npeel) pslot = lds_insert(tab, shift, mask, ~(u32)bt.pword, (u32)(bt.pword >> 32));
-  {
+  if constexpr (kList) {
     const u64 cm = __ballot(pslot >= 0);
     if (pslot >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)pslot;
     cnt += __popcll(cm);
@@ -288,12 +300,14 @@ __device__ __forceinline__ void hash_batch(u64* tab, uint16_t* lst, int& cnt, in
         }
       }
     }
+    if constexpr (kList) {
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      if (h0 + k < nch) {
-        const u64 cm = __ballot(slot[k] >= 0);
-        if (slot[k] >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)slot[k];
-        cnt += __popcll(cm);
+      for (int k = 0; k < H; ++k) {
+        if (h0 + k < nch) {
+          const u64 cm = __ballot(slot[k] >= 0);
+          if (slot[k] >= 0) lst[cnt + __popcll(cm & lt)] = (uint16_t)slot[k];
+          cnt += __popcll(cm);
+        }
       }
     }
   }
@@ -547,6 +561,78 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
     s0 = s3;
     s1 = s4;
     s2 = s5;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Label-dense supersteps only: seg-bin rows of kSegArcs < deg <= kBlockMaxDeg (the hub
+// rows [hub_lane_begin, n_hub), degree-descending), one block per row, tallied
+// straight from al[].  Wave w takes the row's 512-arc batch w (ballot peel in
+// registers, residual votes into the block's shared LDS table of 2^ceil(log2(2 deg))
+// slots), then the block scans and clears the table.  When nearly every vote is a
+// distinct label, staging a unit's words and re-tallying them in the combine costs
+// about twice the direct tally; once labels settle the unit path is cheaper (a dirty
+// row re-tallies only its dirty units), so the converged supersteps keep it.
+// Grid-stride over the rows (frontier: over the listed bin-0 rows, those below h0
+// belong to the hub combine).
+// ---------------------------------------------------------------------------
+constexpr int kBlockWaves = kBlockMaxDeg / kSegArcs;
+template <int kLg>
+__global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* __restrict__ rp,
+                                                               const int32_t* __restrict__ al,
+                                                               int32_t* __restrict__ Ln, int64_t h0,
+                                                               int64_t h1,
+                                                               const int32_t* __restrict__ flist,
+                                                               const int32_t* __restrict__ fcnt0,
+                                                               const int32_t* __restrict__ fr_all) {
+  static_assert((1 << kLg) >= 2 * kBlockMaxDeg, "table load <= 1/2");
+  constexpr int kSlots = 1 << kLg;
+  constexpr int kT = 64 * kBlockWaves;
+  __shared__ u64 tab[kSlots];
+  __shared__ u64 redw[kBlockWaves];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 lt = (1ull << lane) - 1ull;
+  const bool all = *fr_all != 0;
+  const int64_t n = all ? h1 - h0 : (int64_t)*fcnt0;
+  if ((int64_t)blockIdx.x >= n) return;  // uniform
+  for (int i = threadIdx.x; i < kSlots; i += kT) tab[i] = 0ull;
+  __syncthreads();
+  for (int64_t q = blockIdx.x; q < n; q += gridDim.x) {
+    const int64_t h = all ? h0 + q : (int64_t)flist[q];
+    if (h < h0 || h >= h1) continue;  // uniform over the block
+    const int64_t b = rp[h], e = rp[h + 1];
+    const int d = (int)(e - b);
+    int lg = ceil_log2(2u * (u32)d);
+    lg = lg < 6 ? 6 : lg;
+    const int64_t c0 = b + (int64_t)w * kSegArcs;
+    if (c0 < e) {
+      u32 lab[kChunks];
+      load_labels<kChunks>(lab, al, c0, e, lane);
+      const int nch = (int)min<int64_t>(kChunks, (e - c0 + 63) >> 6);
+      Batch<kChunks> bt;
+      peel_batch<kChunks>(bt, lab, nch, lane);
+      int unused = 0;
+      hash_batch<kChunks, false>(tab, nullptr, unused, 32 - lg, (1u << lg) - 1u, bt, lab, nch, lane, lt);
+    }
+    __syncthreads();
+    u64 best = 0ull;
+    for (int i = threadIdx.x; i < (1 << lg); i += kT) {
+      const u64 t = tab[i];
+      if (t) {
+        best = umax64(best, t);
+        tab[i] = 0ull;
+      }
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) redw[w] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      u64 m = redw[0];
+#pragma unroll
+      for (int k = 1; k < kBlockWaves; ++k) m = umax64(m, redw[k]);
+      Ln[h] = (int32_t)(~(u32)m);
+    }
   }
 }
 
@@ -1395,12 +1481,25 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     return LPA_OK;
   };
   LPA_TRY(mark(0, s));
-  if (g->n_segs > 0) {
-    hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
-                       g->al, g->segs, g->n_segs, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all);
+  // label-dense supersteps: the rows of <= kBlockMaxDeg arcs by k_lpa_block, only
+  // the longer rows' units by k_lpa_units (block_mode_now)
+  const bool blk = block_mode_now(g);
+  auto launch_block = [&]() -> int {
+    const int64_t nb = g->n_hub - g->hub_lane_begin;
+    hipLaunchKernelGGL(k_lpa_block<13>, dim3(cap_grid(nb, 2048)), dim3(64 * kBlockWaves), 0, s, g->rp, g->al,
+                       Lown, g->hub_lane_begin, g->n_hub, g->flist, fcnt, fr_all);
+    LPA_HIP(hipGetLastError());
+    return LPA_OK;
+  };
+  if (blk && g->block_at == 0) LPA_TRY(launch_block());
+  const int64_t n_units = blk ? g->unit_lane_begin : g->n_segs;
+  if (n_units > 0) {
+    hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
+                       g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all);
     LPA_HIP(hipGetLastError());
     LPA_TRACE_POINT("seg");
   }
+  if (blk && g->block_at == 1) LPA_TRY(launch_block());
   LPA_TRY(mark(1, s));
 #define LPA_WAVE_LAUNCH(BIN, NC, ST)                                                              \
   {                                                                                           \
@@ -1613,6 +1712,10 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     int32_t* Ln = g->lab[g->cur ^ 1];
     int32_t* Lown = Ln + g->own_begin;
     const bool tt = timed && t < nt;
+    if (g->force_all_next) {  // a stream op ahead of the superstep (never captured)
+      LPA_TRY(frontier_all(g, g->par));
+      g->force_all_next = false;
+    }
     // per-kernel events only in the serialized profiling schedule (lpa_set_serial):
     // there they give standalone kernel times; the concurrent schedule is timed per
     // superstep only, so a timed converged superstep still replays its graph
@@ -1667,6 +1770,10 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par,
                              bev ? bev[kTallyEv + 2] : nullptr));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 3], s));
+    // after the last block-mode superstep the next one tallies every row and unit:
+    // the block rows' units staged nothing while k_lpa_block tallied them (set at the
+    // next superstep's start, after any caller-driven refresh has written fr_all)
+    if (block_mode_now(g) && g->since_reset + 1 == kDenseSupersteps) g->force_all_next = true;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     g->cur ^= 1;
     g->par ^= 1;

@@ -19,7 +19,7 @@ def short(n):
 steps = []
 for r in rows:
     n = short(r['Kernel_Name'])
-    if n == 'k_lpa_units':
+    if n == 'k_frontier_lists':
         steps.append([])
     if steps:
         steps[-1].append((n, int(r['Start_Timestamp']), int(r['End_Timestamp']), r.get('Queue_Id', '')))
