@@ -102,3 +102,28 @@ def adversarial_hub(n_nb=20000, seed=0):
     bs = rng.choice(sel, size=n_nb)
     bd = rng.choice(sel, size=n_nb)
     return V, np.concatenate([s, bs]).astype(np.int32), np.concatenate([nb, bd]).astype(np.int32)
+
+
+def settled_hubs(seed=0, V=20000, n_hub=30, n_mover=40):
+    """Nearly every vertex keeps its L0 label in superstep 1 (a self-loop = 2 votes
+    for itself against single votes from distinct neighbours), so only the few
+    `movers` (no self-loop) change and superstep 2 already runs on a frontier list
+    -- with hub rows of 1024 < deg <= 4096, the rows the label-dense supersteps tally
+    with one block each (k_lpa_block in list mode)."""
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(V)
+    hubs, movers = perm[:n_hub], perm[n_hub:n_hub + n_mover]
+    src, dst = [], []
+    for h in hubs:
+        nb = rng.choice(V, size=int(rng.integers(1100, 3000)), replace=False)
+        nb = nb[nb != h]
+        src.append(np.full(nb.size, h)), dst.append(nb)
+    bg = rng.integers(0, V, size=(2 * V, 2))
+    src.append(bg[:, 0]), dst.append(bg[:, 1])
+    keep = np.setdiff1d(np.arange(V), movers)
+    src.append(keep), dst.append(keep)                      # one self-loop each
+    src.append(np.repeat(hubs, 2)), dst.append(np.repeat(hubs, 2))   # hubs: 3 in all
+    for m in movers:                                        # 4 distinct hubs each
+        hs = rng.choice(hubs, size=4, replace=False)
+        src.append(np.full(4, m)), dst.append(hs)
+    return V, np.concatenate(src).astype(np.int32), np.concatenate(dst).astype(np.int32)

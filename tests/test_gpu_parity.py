@@ -4,7 +4,7 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from graphs import adversarial_hub, degree_mix, giant_hub, random_multigraph, star, two_cliques
+from graphs import adversarial_hub, degree_mix, giant_hub, random_multigraph, settled_hubs, star, two_cliques
 
 pytestmark = pytest.mark.gpu
 
@@ -437,3 +437,20 @@ def test_hub_spill_adversarial_bucket(gfa, oracle, seed):
     for t in range(3):
         bad = np.flatnonzero(got[t] != hist[t])
         assert bad.size == 0, f"superstep {t + 1}: {bad.size} differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_frontier_from_superstep_2_with_block_rows(gfa, oracle, seed):
+    """A graph where superstep 1 changes ~0.25 % of the arcs' labels (self-loops keep
+    almost every L0 label): superstep 2 -- a label-dense superstep, whose hub rows of
+    1024 < deg <= 4096 are tallied one block per row -- already runs on the frontier
+    lists, and superstep 3 must re-tally every row (the block rows staged no unit
+    words).  Bit-exact per superstep, and lpa_run agrees."""
+    V, s, d = settled_hubs(seed)
+    _, hist, _ = oracle.lpa(V, s, d, 8, per_iter=True)
+    got = _per_step(gfa, V, s, d, 8)
+    for t in range(8):
+        bad = np.flatnonzero(got[t] != hist[t])
+        assert bad.size == 0, f"superstep {t + 1}: {bad.size} differ, first {bad[:5]}"
+    with gfa.Graph(s, d, V) as g:
+        assert np.array_equal(g.run(8), hist[7])
