@@ -21,14 +21,14 @@ LPA_ERCCL = -2000
 LPA_EOVERFLOW = -75
 LPA_INPUT_DEVICE = 0x1
 LPA_NBINS = 13
-LPA_NKERNELS = 16
+LPA_NKERNELS = 17
 LPA_STATS_MAX_ITERS = 64
 BIN_NAMES = ("seg", "w16", "w8", "w4", "w2", "g64", "g32", "g16", "g8", "g4", "g2", "g1", "isolated")
 # timed kernels: the bin kernels plus the hub combine ("hub") and the al[] refresh
 KERNEL_NAMES = ("k_lpa_units", "hub", "k_lpa_wave<16>", "k_lpa_wave<8>", "k_lpa_wave<4>", "k_lpa_wave<2>",
                 "k_lpa_rows<64>", "k_lpa_rows<32>", "k_lpa_rows<16>", "k_lpa_rows<8>",
                 "k_lpa_group<4>", "k_lpa_group<2>", "k_lpa_group<1>", "refresh", "k_al_rebuild_hot",
-                "k_frontier_lists")
+                "k_frontier_lists", "k_lpa_block")
 KERNEL_BIN = {"k_lpa_units": "seg", "k_lpa_wave<16>": "w16", "k_lpa_wave<8>": "w8", "k_lpa_wave<4>": "w4", "k_lpa_wave<2>": "w2",
               "k_lpa_rows<64>": "g64", "k_lpa_rows<32>": "g32", "k_lpa_rows<16>": "g16",
               "k_lpa_rows<8>": "g8", "k_lpa_group<4>": "g4", "k_lpa_group<2>": "g2",

@@ -139,7 +139,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_FRONTIER_FRAC")) g->frontier_frac = atof(f);
   if (const char* f = getenv("LPA_MID_MERGED")) g->mid_merged = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_BLOCK")) g->block_rows = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_BLOCK_AT")) g->block_at = atoi(f) ? 1 : 0;
+  if (const char* f = getenv("LPA_BLOCK_AT")) g->block_at = atoi(f) < 0 ? 0 : (atoi(f) > 2 ? 2 : atoi(f));
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {

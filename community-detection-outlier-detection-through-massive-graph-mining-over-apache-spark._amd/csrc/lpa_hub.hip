@@ -1042,7 +1042,9 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   // fork (label-dense supersteps): classify the > 8-unit rows first and start the
   // bucket path on its own stream; the mid tiers follow k_hub_small on the main
   // stream.  Otherwise everything runs in order on the main stream.
-  hipStream_t sd = fork ? g->aux_stream[2] : s;
+  // (the fourth stream runs k_lpa_block when block_at == 2: the bucket path then
+  // follows the row bins on the third)
+  hipStream_t sd = !fork ? s : (block_mode_now(g) && g->block_at == 2) ? g->aux_stream[1] : g->aux_stream[2];
   const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
   auto bucket_path = [&]() -> int {
     hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,

@@ -34,9 +34,10 @@ constexpr int kSegArcs = 512;         // arcs per unit of a seg-bin row (one wav
 constexpr int kBlockMaxDeg = 4096;    // seg rows up to this degree: k_lpa_block in the label-dense supersteps
 constexpr int kTallyKernels = 13;                  // stats kernels 0..12: the tally
 constexpr int kTallyEv = 2 * kTallyKernels;        // events bracketing each tally kernel
-// + join, after exchange, after scatter, after rebuild, lists start, lists end
-constexpr int kBinEvents = kTallyEv + 6;
-static_assert(LPA_NKERNELS == kTallyKernels + 3, "stats: tally kernels + refresh, rebuild, lists");
+// + join, after exchange, after scatter, after rebuild, lists start, lists end,
+// k_lpa_block start, end
+constexpr int kBinEvents = kTallyEv + 8;
+static_assert(LPA_NKERNELS == kTallyKernels + 4, "stats: tally kernels + refresh, rebuild, lists, block");
 constexpr int kCombWords = 2048;      // expected staged words per combine bucket
 constexpr int kCombSlots = 8192;      // LDS table slots of a combine block
 constexpr int kCombDirect = 6144;     // <= this many staged words: one block, no buckets
@@ -149,7 +150,8 @@ struct lpa_graph {
                                   //   chunk items, wave path, mid2, mid3, small (list S)
   int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
   int block_rows = 1;             // LPA_BLOCK=0: label-dense supersteps also stage the rows above by units
-  int block_at = 0;               // LPA_BLOCK_AT: k_lpa_block before (0) or after (1) k_lpa_units
+  int block_at = 0;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the
+                                  // main stream, or (2) on the fourth stream, concurrent with them
   int64_t unit_lane_begin = 0;    // hub_uoff[hub_lane_begin]
   bool force_all_next = false;    // the next superstep tallies every row (after block mode)
   lpa::u64* items_cb = nullptr;   // [n_hub_buckets] (hub << 32 | bucket)

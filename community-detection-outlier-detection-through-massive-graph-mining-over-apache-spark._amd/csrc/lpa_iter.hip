@@ -1480,18 +1480,29 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     if (bev) LPA_HIP(hipEventRecord(bev[i], st));
     return LPA_OK;
   };
-  LPA_TRY(mark(0, s));
   // label-dense supersteps: the rows of <= kBlockMaxDeg arcs by k_lpa_block, only
   // the longer rows' units by k_lpa_units (block_mode_now)
   const bool blk = block_mode_now(g);
-  auto launch_block = [&]() -> int {
+  auto launch_block = [&](hipStream_t st) -> int {
     const int64_t nb = g->n_hub - g->hub_lane_begin;
-    hipLaunchKernelGGL(k_lpa_block<13>, dim3(cap_grid(nb, 2048)), dim3(64 * kBlockWaves), 0, s, g->rp, g->al,
+    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 6], st));
+    hipLaunchKernelGGL(k_lpa_block<13>, dim3(cap_grid(nb, 2048)), dim3(64 * kBlockWaves), 0, st, g->rp, g->al,
                        Lown, g->hub_lane_begin, g->n_hub, g->flist, fcnt, fr_all);
     LPA_HIP(hipGetLastError());
+    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 7], st));
     return LPA_OK;
   };
-  if (blk && g->block_at == 0) LPA_TRY(launch_block());
+  // serialized profiling: the block kernel bracketed on its own (stats kernel 16),
+  // ahead of the seg units' marks
+  if (blk && (g->block_at == 0 || g->serial)) LPA_TRY(launch_block(s));
+  // block_at 2: on the fourth stream (idle until the hub combine forks its bucket path
+  // there, after this kernel in stream order; the combine's join then covers it)
+  if (blk && g->block_at == 2 && !g->serial) {
+    LPA_HIP(hipStreamWaitEvent(g->aux_stream[2], g->ev_fork, 0));
+    LPA_TRY(launch_block(g->aux_stream[2]));
+    LPA_HIP(hipEventRecord(g->ev_join2[1], g->aux_stream[2]));
+  }
+  LPA_TRY(mark(0, s));
   const int64_t n_units = blk ? g->unit_lane_begin : g->n_segs;
   if (n_units > 0) {
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
@@ -1499,8 +1510,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_HIP(hipGetLastError());
     LPA_TRACE_POINT("seg");
   }
-  if (blk && g->block_at == 1) LPA_TRY(launch_block());
   LPA_TRY(mark(1, s));
+  if (blk && g->block_at == 1 && !g->serial) LPA_TRY(launch_block(s));
 #define LPA_WAVE_LAUNCH(BIN, NC, ST)                                                              \
   {                                                                                           \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                  \
@@ -1556,6 +1567,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_TRY(mark(2, s));
   LPA_TRY(launch_hub_combine(g, Lown, !g->serial && g->since_reset < kDenseSupersteps));
   LPA_TRACE_POINT("hub_combine");
+  // the block rows' labels are seg-bin slots: joined before the main stream's diff
+  if (blk && g->block_at == 2 && !g->serial) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[1], 0));
   LPA_TRY(mark(3, s));
   if (diff) {
     // inside the concurrent tally: no Lc sync here, the scatter refresh does it
@@ -1707,7 +1720,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
   // per timed superstep t, bin_ev[t*kBinEvents + i]: 2k / 2k+1 around tally kernel
   // k (k < kTallyKernels), then kTallyEv after the join, +1 after the exchange, +2
   // after the diff + scatter, +3 after the rebuild, +4 / +5 around the frontier lists
+  bool blk_ran[LPA_STATS_MAX_ITERS] = {};  // serialized stats: k_lpa_block ran in superstep t
   for (int32_t t = 0; t < n; ++t) {
+    if (t < nt) blk_ran[t] = block_mode_now(g);
     const int32_t* Lc = g->lab[g->cur];
     int32_t* Ln = g->lab[g->cur ^ 1];
     int32_t* Lown = Ln + g->own_begin;
@@ -1812,6 +1827,10 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       st->kernel_ms[kTallyKernels + 1] += ms;
       LPA_HIP(hipEventElapsedTime(&ms, bev[kTallyEv + 4], bev[kTallyEv + 5]));
       st->kernel_ms[kTallyKernels + 2] += ms;
+      if (blk_ran[t]) {
+        LPA_HIP(hipEventElapsedTime(&ms, bev[kTallyEv + 6], bev[kTallyEv + 7]));
+        st->kernel_ms[kTallyKernels + 3] += ms;
+      }
     }
     float tot;
     LPA_HIP(hipEventElapsedTime(&tot, g->ev[2 * LPA_STATS_MAX_ITERS], g->ev[2 * LPA_STATS_MAX_ITERS + 1]));

@@ -41,8 +41,9 @@ extern "C" {
 #define LPA_INPUT_DEVICE 0x1u /* src/dst are device pointers on `device`        */
 
 #define LPA_NBINS 13   /* 0 seg 1 w16 2 w8 3 w4 4 w2 5 g64 6 g32 7 g16 8 g8 9 g4 10 g2 11 g1 12 isolated */
-#define LPA_NKERNELS 16 /* timed: 0 seg 1 hub 2 w16 3 w8 4 w4 5 w2 6 g64 7 g32 8 g16 9 g8 10 g4 11 g2 12 g1
-                          13 refresh (diff + al[] scatter) 14 al[] rebuild 15 frontier lists */
+#define LPA_NKERNELS 17 /* timed: 0 seg 1 hub 2 w16 3 w8 4 w4 5 w2 6 g64 7 g32 8 g16 9 g8 10 g4 11 g2 12 g1
+                          13 refresh (diff + al[] scatter) 14 al[] rebuild 15 frontier lists
+                          16 block-per-row hub tally (label-dense supersteps) */
 #define LPA_STATS_MAX_ITERS 64
 
 typedef struct lpa_graph lpa_graph;
