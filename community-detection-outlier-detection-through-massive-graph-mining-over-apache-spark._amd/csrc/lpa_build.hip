@@ -15,24 +15,44 @@
 //   4. row_ptr = exclusive scan of owned degrees (int64: >2^31 arcs at scale 26).
 //   5. degree bins = contiguous slot ranges (binary search on the sorted degrees),
 //      hub segments, their tally staging and the combine work items.
-#include "lpa_internal.h"
+#include "lpa_device.h"
 
 namespace lpa {
 
 namespace {
 
-__global__ void k_degree(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
-                         int64_t m, int32_t V, int32_t* __restrict__ deg, int32_t* err) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    int32_t s = src[e], d = dst[e];
-    if ((u32)s >= (u32)V || (u32)d >= (u32)V) {
-      atomicOr(err, 1);
-      continue;
+using dev::BlockHist;
+using dev::kBhSlots;
+
+// grid of the block-aggregated histogram kernels: few blocks, each over a long
+// stretch of the input, so its LDS table absorbs the repeats before the flush
+constexpr unsigned kBhGrid = 2048;
+inline unsigned cap_bh(unsigned g) { return g < kBhGrid ? g : kBhGrid; }
+
+// symmetrised degrees: a hub's counter took one device atomic per arc (same-address
+// serialisation: 30 ms at R-MAT-24); block-aggregated in LDS instead
+__global__ __launch_bounds__(256) void k_degree(const int32_t* __restrict__ src,
+                                                const int32_t* __restrict__ dst, int64_t m, int32_t V,
+                                                int32_t* __restrict__ deg, int32_t* err) {
+  __shared__ u32 bk[kBhSlots];
+  __shared__ int32_t bv[kBhSlots];
+  BlockHist<int32_t> bh{bk, bv};
+  bh.init();
+  const int lane = threadIdx.x & 63;
+  for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x; e0 < m; e0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = e0 + threadIdx.x;
+    u32 s = 0u, d = 0u;
+    bool ok = false;
+    if (e < m) {
+      s = (u32)src[e];
+      d = (u32)dst[e];
+      ok = s < (u32)V && d < (u32)V;
+      if (!ok) atomicOr(err, 1);
     }
-    atomicAdd(&deg[s], 1);
-    atomicAdd(&deg[d], 1);
+    bh.add1(deg, ok, s, lane);
+    bh.add1(deg, ok, d, lane);
   }
+  bh.flush(deg);
 }
 
 __global__ void k_maxdeg(const int32_t* __restrict__ deg, int64_t V, int32_t* out) {
@@ -177,13 +197,30 @@ __global__ void k_keys_to_col(const u64* __restrict__ keys, int64_t n, int32_t* 
 
 // CSC keys: (column << 32 | position), generated in position order so a stable
 // sort on the column bits alone leaves positions ascending within a column
-__global__ void k_csc_keys(const int32_t* __restrict__ col, int64_t n, u64* __restrict__ keys,
-                           int32_t* __restrict__ colcnt) {
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += (int64_t)gridDim.x * blockDim.x) {
-    keys[j] = ((u64)(u32)col[j] << 32) | (u64)j;
-    atomicAdd(&colcnt[col[j]], 1);
+// (colcnt == nullptr: keys only -- at P = 1 the column counts are the degrees;
+// otherwise block-aggregated: a hub column is one device atomic per block)
+__global__ __launch_bounds__(256) void k_csc_keys(const int32_t* __restrict__ col, int64_t n,
+                                                  u64* __restrict__ keys, int32_t* __restrict__ colcnt) {
+  if (!colcnt) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+      keys[j] = ((u64)(u32)col[j] << 32) | (u64)j;
+    return;
   }
+  __shared__ u32 bk[kBhSlots];
+  __shared__ int32_t bv[kBhSlots];
+  BlockHist<int32_t> bh{bk, bv};
+  bh.init();
+  const int lane = threadIdx.x & 63;
+  for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = j0 + threadIdx.x;
+    u32 c = 0u;
+    if (j < n) {
+      c = (u32)col[j];
+      keys[j] = ((u64)c << 32) | (u64)j;
+    }
+    bh.add1(colcnt, j < n, c, lane);
+  }
+  bh.flush(colcnt);
 }
 
 // scatter chunks of every column: count, then owner of each chunk
@@ -319,7 +356,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   LPA_TRY(dev_alloc(g, (void**)&g->deg, sizeof(int32_t) * (V > 0 ? V : 1)));
   LPA_HIP(hipMemsetAsync(g->deg, 0, sizeof(int32_t) * (V > 0 ? V : 1), s));
   if (m > 0) {
-    hipLaunchKernelGGL(k_degree, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, V,
+    hipLaunchKernelGGL(k_degree, dim3(cap_bh(grid_for(m))), dim3(256), 0, s, g->e_src, g->e_dst, m, V,
                        g->deg, d_err);
     LPA_HIP(hipGetLastError());
   }
@@ -426,8 +463,14 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     }
     int32_t* colcnt = nullptr;
     LPA_HIP(hipMalloc((void**)&colcnt, sizeof(int32_t) * g->vpad));
-    LPA_HIP(hipMemsetAsync(colcnt, 0, sizeof(int32_t) * g->vpad, s));
-    hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(arcs)), dim3(256), 0, s, g->col, arcs, keys, colcnt);
+    if (P == 1) {
+      // one rank: column u occurs once per arc of u, i.e. deg_own[u] times
+      LPA_HIP(hipMemcpyAsync(colcnt, deg_own, sizeof(int32_t) * g->vpad, hipMemcpyDeviceToDevice, s));
+      hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(arcs)), dim3(256), 0, s, g->col, arcs, keys, (int32_t*)nullptr);
+    } else {
+      LPA_HIP(hipMemsetAsync(colcnt, 0, sizeof(int32_t) * g->vpad, s));
+      hipLaunchKernelGGL(k_csc_keys, dim3(cap_bh(grid_for(arcs))), dim3(256), 0, s, g->col, arcs, keys, colcnt);
+    }
     LPA_HIP(hipGetLastError());
     int cs[8], ncs = 0;
     for (int b = 0; b < bits_for((uint64_t)(g->vpad - 1)); b += 8) cs[ncs++] = 32 + b;

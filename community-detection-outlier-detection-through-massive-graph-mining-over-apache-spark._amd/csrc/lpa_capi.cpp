@@ -57,7 +57,7 @@ void destroy(lpa_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   void* bufs[] = {g->rp,   g->col,   g->new_of, g->old_of, g->deg,   g->lab[0], g->lab[1],
-                  g->segs, g->e_src,  g->e_dst, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
+                  g->segs, g->e_src,  g->e_dst, g->de_keys, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
                   g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
@@ -140,6 +140,10 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_MID_MERGED")) g->mid_merged = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_BLOCK")) g->block_rows = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_BLOCK_AT")) g->block_at = atoi(f) < 0 ? 0 : (atoi(f) > 2 ? 2 : atoi(f));
+  // internal builds (the outlier stage's L2 sub-graph): the locality order is a
+  // gather-locality heuristic worth its two atomic passes only on a graph that runs
+  // many supersteps; labels do not depend on the vertex order
+  if (flags & kFlagNoLocality) g->locality = 0;
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {
@@ -492,7 +496,12 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   return LPA_OK;
 }
 
-void lpa_graph_destroy(lpa_graph* g) { destroy(g); }
+void lpa_graph_destroy(lpa_graph* g) {
+  if (!g) return;
+  const int dev = g->device;
+  destroy(g);
+  tmp_trim(dev);  // the stream-ordered temporaries' cached memory goes back to the device
+}
 
 int lpa_gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t scramble, int32_t* d_src,
                  int32_t* d_dst, int32_t device, void* hip_stream) {

@@ -225,5 +225,72 @@ __device__ __forceinline__ void list_append(uint16_t* lst, int* lcount, int slot
   if (slot >= 0) lst[base + __popcll(cm & ((1ull << lane) - 1ull))] = (uint16_t)slot;
 }
 
+// ---------------------------------------------------------------------------
+// Block-aggregated histogram: hist[key] += val over a stream of (key, val) without
+// the two costs of plain device atomics here -- same-address serialisation (hub
+// degrees, giant communities: every wave adding into one counter) and one
+// memory-side atomic per element.  The block sums into a small LDS open-addressing
+// table (kBhSlots keys, at most kBhProbes probes per key) and flushes it at the end
+// with one device atomic per distinct key; a key that finds no slot goes straight
+// to the device histogram.  add1 first merges the lanes of a wave that hold the same
+// key (ballot rounds), so a hub repeated across a wave is one LDS atomic.
+// Every lane of the block must call init / add* / flush (they contain barriers or
+// wave-wide ballots); keys must differ from kBhEmpty.
+// ---------------------------------------------------------------------------
+constexpr int kBhLg = 12;
+constexpr int kBhSlots = 1 << kBhLg;
+constexpr int kBhProbes = 8;
+constexpr u32 kBhEmpty = 0xFFFFFFFFu;
+template <typename T>
+struct BlockHist {
+  u32* key;  // LDS [kBhSlots]
+  T* val;    // LDS [kBhSlots]
+  __device__ __forceinline__ void init() {
+    for (int i = threadIdx.x; i < kBhSlots; i += blockDim.x) {
+      key[i] = kBhEmpty;
+      val[i] = (T)0;
+    }
+    __syncthreads();
+  }
+  __device__ __forceinline__ bool lds_add(u32 k, T v) {
+    u32 h = (k * 0x9E3779B1u) >> (32 - kBhLg);
+#pragma unroll 1
+    for (int p = 0; p < kBhProbes; ++p) {
+      const u32 old = atomicCAS(&key[h], kBhEmpty, k);
+      if (old == kBhEmpty || old == k) {
+        atomicAdd(&val[h], v);
+        return true;
+      }
+      h = (h + 1u) & (u32)(kBhSlots - 1);
+    }
+    return false;
+  }
+  // weighted: lanes with act add v to hist[k]
+  __device__ __forceinline__ void addw(T* __restrict__ hist, bool act, u32 k, T v) {
+    if (act && !lds_add(k, v)) atomicAdd(&hist[k], v);
+  }
+  // count: lanes with act add 1 to hist[k] (all 64 lanes of the wave call it)
+  __device__ __forceinline__ void add1(T* __restrict__ hist, bool act, u32 k, int lane) {
+    bool mine = act;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const u64 pend = __ballot(mine);
+      if (pend == 0ull) return;  // uniform
+      const int lead = __ffsll((unsigned long long)pend) - 1;
+      const u32 kk = (u32)__builtin_amdgcn_readlane((int)k, lead);
+      const bool eq = mine && k == kk;
+      const u64 em = __ballot(eq);
+      if (lane == lead) addw(hist, true, kk, (T)__popcll(em));
+      if (eq) mine = false;
+    }
+    addw(hist, mine, k, (T)1);
+  }
+  __device__ __forceinline__ void flush(T* __restrict__ hist) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kBhSlots; i += blockDim.x)
+      if (key[i] != kBhEmpty) atomicAdd(&hist[key[i]], val[i]);
+  }
+};
+
 }  // namespace dev
 }  // namespace lpa

@@ -38,6 +38,7 @@ constexpr int kTallyEv = 2 * kTallyKernels;        // events bracketing each tal
 // k_lpa_block start, end
 constexpr int kBinEvents = kTallyEv + 8;
 static_assert(LPA_NKERNELS == kTallyKernels + 4, "stats: tally kernels + refresh, rebuild, lists, block");
+constexpr uint32_t kFlagNoLocality = 0x100u;  // internal create flag (not in lpa.h)
 constexpr int kCombWords = 2048;      // expected staged words per combine bucket
 constexpr int kCombSlots = 8192;      // LDS table slots of a combine block
 constexpr int kCombDirect = 6144;     // <= this many staged words: one block, no buckets
@@ -219,6 +220,10 @@ struct lpa_graph {
   // original edge list kept for the outlier stage (device, dense ids)
   int32_t* e_src = nullptr;
   int32_t* e_dst = nullptr;
+  // its distinct directed edges (s << 32 | d), sorted: built by the first outlier call
+  // and kept (label-independent topology, as GraphFrames' cachedTopologyGraphX)
+  lpa::u64* de_keys = nullptr;
+  int64_t de_n = -1;                        // -1: not built yet
 
   int64_t device_bytes = 0;
   hipEvent_t ev[2 * LPA_STATS_MAX_ITERS + 2] = {};
@@ -229,6 +234,11 @@ namespace lpa {
 
 // allocation helpers (track bytes on the handle)
 int dev_alloc(lpa_graph* g, void** p, size_t bytes);
+// stream-ordered temporaries (lpa_prims.hip); tmp_trim returns the pool's cached
+// memory to the device
+int tmp_alloc(void** p, size_t bytes, hipStream_t s);
+void tmp_free(void* p, hipStream_t s);
+void tmp_trim(int device);
 void dev_free(lpa_graph* g, void* p);
 
 // primitives (lpa_prims.hip)

@@ -16,7 +16,7 @@
 // A sub-label L'[v] is the id of a vertex of v's own community (E' never
 // crosses communities), so the group (L[v], L'[v]) is identified by L'[v] alone
 // and its community is L[L'[v]].
-#include "lpa_internal.h"
+#include "lpa_device.h"
 
 namespace lpa {
 
@@ -33,6 +33,16 @@ inline unsigned grid_for(int64_t n) {
   return (unsigned)b;
 }
 
+// block-aggregated histograms: few blocks, each over a long stretch of the input
+inline unsigned grid_bh(int64_t n) {
+  const unsigned g = grid_for(n);
+  return g < 2048u ? g : 2048u;
+}
+inline unsigned grid_cnt(int64_t n) {
+  const unsigned g = grid_for(n);
+  return g < 4096u ? g : 4096u;
+}
+
 #define GRID_STRIDE(i, n) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
 // uniform variant: every lane of a wave runs every trip (wave-level ballots inside);
@@ -42,29 +52,6 @@ inline unsigned grid_for(int64_t n) {
        i##_b += (int64_t)gridDim.x * blockDim.x) {                                   \
     const int64_t i = i##_b + threadIdx.x;                                           \
     const bool act = i < (n);
-
-// Wave-aggregated histogram increment (all 64 lanes call it; lanes with act add 1
-// to hist[key]).  Communities are heavily skewed -- a converged R-MAT labelling
-// puts most vertices in one community -- so a plain atomicAdd per element
-// serialises on a few addresses; here each round the first pending lane's key is
-// counted for the whole wave with one ballot and added by one atomic, and only
-// the lanes still pending after kAggRounds rounds add individually.
-constexpr int kAggRounds = 4;
-__device__ __forceinline__ void hist_inc(int32_t* __restrict__ hist, bool act, u32 key, int lane) {
-  bool mine = act;
-#pragma unroll
-  for (int r = 0; r < kAggRounds; ++r) {
-    const u64 pend = __ballot(mine);
-    if (pend == 0ull) return;  // uniform
-    const int lead = __ffsll((unsigned long long)pend) - 1;
-    const u32 k = (u32)__builtin_amdgcn_readlane((int)key, lead);
-    const bool eq = mine && key == k;
-    const u64 em = __ballot(eq);
-    if (lane == lead) atomicAdd(&hist[k], (int32_t)__popcll(em));
-    if (eq) mine = false;
-  }
-  if (mine) atomicAdd(&hist[key], 1);
-}
 
 __global__ void k_edge_keys(const int32_t* __restrict__ s, const int32_t* __restrict__ d, int64_t m,
                             u64* __restrict__ k) {
@@ -76,28 +63,45 @@ __global__ void k_mark_first(const u64* __restrict__ k, int64_t n, int32_t* __re
   GRID_STRIDE(i, n) mark[i] = (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
 }
 
+__global__ void k_compact_marked(const u64* __restrict__ k, const int32_t* __restrict__ mark,
+                                 const int64_t* __restrict__ pos, int64_t n, u64* __restrict__ out) {
+  GRID_STRIDE(i, n) if (mark[i]) out[pos[i]] = k[i];
+}
+
 // size[l] = members of community l; labels outside [0, V) are counted in *bad and
 // skipped (reported after the final sync instead of a host round trip up front)
+// (block-aggregated: the giant communities of a converged labelling took one device
+// atomic per wave on the same counter, 7.5 ms at R-MAT-24)
 __global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ lab, int64_t V,
                                                    int32_t* __restrict__ hist,
                                                    unsigned long long* __restrict__ bad) {
+  __shared__ u32 bk[dev::kBhSlots];
+  __shared__ int32_t bv[dev::kBhSlots];
+  dev::BlockHist<int32_t> bh{bk, bv};
+  bh.init();
   const int lane = threadIdx.x & 63;
   GRID_STRIDE_UNIFORM_BEGIN(v, act, V)
     u32 l = act ? (u32)lab[v] : 0u;
     const bool oob = act && l >= (u32)V;
     if (oob) atomicAdd(bad, 1ull);
-    hist_inc(hist, act && !oob, l, lane);
+    bh.add1(hist, act && !oob, l, lane);
   }
+  bh.flush(hist);
 }
 
 // incident distinct edges per community, over the sorted edge keys (distinct =
 // first occurrences): +1 for L[s], +1 for L[d] when it differs
-__global__ __launch_bounds__(256) void k_incident(const u64* __restrict__ ek, const int32_t* __restrict__ first,
-                                                  int64_t n, const int32_t* __restrict__ L, int64_t nv,
+// (ek: the distinct directed edges)
+__global__ __launch_bounds__(256) void k_incident(const u64* __restrict__ ek, int64_t n,
+                                                  const int32_t* __restrict__ L, int64_t nv,
                                                   int32_t* __restrict__ inc) {
+  __shared__ u32 bk[dev::kBhSlots];
+  __shared__ int32_t bv[dev::kBhSlots];
+  dev::BlockHist<int32_t> bh{bk, bv};
+  bh.init();
   const int lane = threadIdx.x & 63;
   GRID_STRIDE_UNIFORM_BEGIN(i, act, n)
-    bool a = act && first[i];
+    const bool a = act;
     u32 ls = 0u, ld = 0u;
     if (a) {
       const u64 k = ek[i];
@@ -105,15 +109,16 @@ __global__ __launch_bounds__(256) void k_incident(const u64* __restrict__ ek, co
       ld = (u32)L[(int32_t)(u32)k];
     }
     const u32 V = (u32)nv;   // out-of-range labels (reported by k_histogram) are skipped
-    hist_inc(inc, a && ls < V, ls, lane);
-    hist_inc(inc, a && ld != ls && ld < V, ld, lane);
+    bh.add1(inc, a && ls < V, ls, lane);
+    bh.add1(inc, a && ld != ls && ld < V, ld, lane);
   }
+  bh.flush(inc);
 }
 
-// E' edges: distinct keys whose endpoints share a label
-__global__ void k_mark_intra(const u64* __restrict__ ek, const int32_t* __restrict__ first, int64_t n,
-                             const int32_t* __restrict__ L, int32_t* __restrict__ mark) {
-  GRID_STRIDE(i, n) mark[i] = (first[i] && L[(int32_t)(ek[i] >> 32)] == L[(int32_t)(u32)ek[i]]) ? 1 : 0;
+// E' edges: distinct edges whose endpoints share a label
+__global__ void k_mark_intra(const u64* __restrict__ ek, int64_t n, const int32_t* __restrict__ L,
+                             int32_t* __restrict__ mark) {
+  GRID_STRIDE(i, n) mark[i] = (L[(int32_t)(ek[i] >> 32)] == L[(int32_t)(u32)ek[i]]) ? 1 : 0;
 }
 
 __global__ void k_split_marked(const u64* __restrict__ ek, const int32_t* __restrict__ mark,
@@ -190,11 +195,19 @@ __global__ __launch_bounds__(256) void k_flag(const int32_t* __restrict__ group_
   }
 }
 
-__global__ void k_count_nonzero(const int32_t* __restrict__ a, int64_t n, unsigned long long* out) {
+// one device atomic per block (per wave, 4 M same-address atomics took 3-6 ms)
+__global__ __launch_bounds__(256) void k_count_nonzero(const int32_t* __restrict__ a, int64_t n,
+                                                       unsigned long long* out) {
+  __shared__ unsigned long long ws[4];
   unsigned long long c = 0;
   GRID_STRIDE(i, n) c += a[i] != 0;
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    c = ws[0] + ws[1] + ws[2] + ws[3];
+    if (c) atomicAdd(out, c);
+  }
 }
 
 __global__ void k_widen(const int32_t* __restrict__ a, int64_t n, int64_t* __restrict__ out) {
@@ -209,7 +222,7 @@ struct Scratch {
   template <typename T>
   int get(T** p, int64_t count) {
     if (count < 1) count = 1;
-    if (hipMalloc((void**)p, sizeof(T) * count) != hipSuccess) {
+    if (tmp_alloc((void**)p, sizeof(T) * count, s) != LPA_OK) {
       set_error("outlier: out of device memory (%lld x %zu B)", (long long)count, sizeof(T));
       return LPA_ENOMEM;
     }
@@ -217,7 +230,7 @@ struct Scratch {
     return LPA_OK;
   }
   ~Scratch() {
-    for (int i = 0; i < n; ++i) (void)hipFree(ptrs[i]);
+    for (int i = 0; i < n; ++i) tmp_free(ptrs[i], s);
   }
 };
 
@@ -228,21 +241,40 @@ int sort_keys(u64* keys, u64* tmp, int64_t n, int bits_lo, int bits_hi, hipStrea
   return radix_sort_u64(keys, tmp, n, shifts, ns, s);
 }
 
-// the handle's edges as sorted (s << 32 | d) keys plus first-occurrence marks
-// (distinct directed edges = the marked keys; their count = sum of the marks)
-int sorted_edges(lpa_graph* g, Scratch& sc, u64** keys, int32_t** first) {
+// The handle's distinct directed edges as sorted (s << 32 | d) keys, g->de_keys[0,
+// g->de_n): sort, mark first occurrences, compact.  Built by the first outlier call
+// and kept with the handle: it is topology (label-independent), like the CSR, and
+// its sort is most of an L1 call otherwise (20 ms of 55 at R-MAT-24).
+int distinct_edges(lpa_graph* g) {
+  if (g->de_n >= 0) return LPA_OK;
   hipStream_t s = g->stream;
   const int64_t m = g->m;
-  LPA_TRY(sc.get(keys, 2 * m));
-  LPA_TRY(sc.get(first, m));
-  if (m > 0) {
-    hipLaunchKernelGGL(k_edge_keys, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, *keys);
-    LPA_HIP(hipGetLastError());
-    const int b = bits_for((uint64_t)(g->V > 0 ? g->V - 1 : 0));
-    LPA_TRY(sort_keys(*keys, *keys + m, m, b, b, s));
-    hipLaunchKernelGGL(k_mark_first, dim3(grid_for(m)), dim3(256), 0, s, *keys, m, *first);
-    LPA_HIP(hipGetLastError());
+  if (m == 0) {
+    g->de_n = 0;
+    return LPA_OK;
   }
+  Scratch sc(s);
+  u64* keys = nullptr;
+  int32_t* first = nullptr;
+  int64_t* pos = nullptr;
+  LPA_TRY(sc.get(&keys, 2 * m));
+  LPA_TRY(sc.get(&first, m));
+  LPA_TRY(sc.get(&pos, m + 1));
+  hipLaunchKernelGGL(k_edge_keys, dim3(grid_for(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, keys);
+  LPA_HIP(hipGetLastError());
+  const int b = bits_for((uint64_t)(g->V > 0 ? g->V - 1 : 0));
+  LPA_TRY(sort_keys(keys, keys + m, m, b, b, s));
+  hipLaunchKernelGGL(k_mark_first, dim3(grid_for(m)), dim3(256), 0, s, keys, m, first);
+  LPA_HIP(hipGetLastError());
+  LPA_TRY(exclusive_scan_i32_i64(first, pos, m, s));
+  int64_t n = 0;
+  LPA_HIP(hipMemcpyAsync(&n, pos + m, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  LPA_TRY(dev_alloc(g, (void**)&g->de_keys, sizeof(u64) * (n > 0 ? n : 1)));
+  hipLaunchKernelGGL(k_compact_marked, dim3(grid_for(m)), dim3(256), 0, s, keys, first, pos, m, g->de_keys);
+  LPA_HIP(hipGetLastError());
+  LPA_HIP(hipStreamSynchronize(s));   // the scratch is freed on return
+  g->de_n = n;
   return LPA_OK;
 }
 
@@ -275,8 +307,9 @@ int bad_labels(unsigned long long n, int64_t V) {
 
 }  // namespace
 
-// Host round trips: none in L1 before the results are copied out; one in L2 (the
-// size of E', which the second LPA's graph build needs).
+// Host round trips: the first call on a handle builds its distinct edge set (one);
+// then none in L1 before the results are copied out, one in L2 (the size of E',
+// which the second LPA's graph build needs).
 int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
             int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
             uint8_t* flags, lpa_outlier_summary* summary) {
@@ -289,14 +322,14 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     return LPA_EINVAL;
   }
   hipStream_t s = g->stream;
-  const int64_t V = g->V, m = g->m;
+  const int64_t V = g->V;
   Scratch sc(s);
   lpa_outlier_summary sum = {};
   int32_t *L = nullptr, *size = nullptr, *inc = nullptr, *thr = nullptr, *segflag = nullptr;
   uint8_t* fl = nullptr;
   int64_t* wide = nullptr;
   // cnt: 0 communities, 1 flagged, 2 communities flagged, 3 bad labels, 4 groups,
-  //      5 distinct edges
+  //      (distinct edges: g->de_n)
   unsigned long long* cnt = nullptr;
   LPA_TRY(sc.get(&L, V));
   LPA_TRY(sc.get(&size, V));
@@ -317,21 +350,16 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
   LPA_HIP(hipMemsetAsync(segflag, 0, sizeof(int32_t) * V, s));
   LPA_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 8, s));
 
-  hipLaunchKernelGGL(k_histogram, dim3(grid_for(V)), dim3(256), 0, s, L, V, size, cnt + 3);
+  hipLaunchKernelGGL(k_histogram, dim3(grid_bh(V)), dim3(256), 0, s, L, V, size, cnt + 3);
   LPA_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(V)), dim3(256), 0, s, size, V, cnt);
+  hipLaunchKernelGGL(k_count_nonzero, dim3(grid_cnt(V)), dim3(256), 0, s, size, V, cnt);
   LPA_HIP(hipGetLastError());
 
-  u64* ek = nullptr;
-  int32_t* first = nullptr;
-  LPA_TRY(sorted_edges(g, sc, &ek, &first));
-  if (m > 0) {
-    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(m)), dim3(256), 0, s, first, m, cnt + 5);
-    LPA_HIP(hipGetLastError());
-  }
-
-  if (m > 0) {
-    hipLaunchKernelGGL(k_incident, dim3(grid_for(m)), dim3(256), 0, s, ek, first, m, L, V, inc);
+  LPA_TRY(distinct_edges(g));
+  const u64* ek = g->de_keys;
+  const int64_t md = g->de_n;   // distinct directed edges
+  if (md > 0) {
+    hipLaunchKernelGGL(k_incident, dim3(grid_bh(md)), dim3(256), 0, s, ek, md, L, V, inc);
     LPA_HIP(hipGetLastError());
   }
 
@@ -352,22 +380,22 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     sum.n_flagged = (int64_t)h_cnt[1];
     sum.n_communities = (int64_t)h_cnt[0];
     sum.n_communities_flagged = sum.n_flagged > 0 ? 1 : 0;
-    sum.distinct_edges = (int64_t)h_cnt[5];
+    sum.distinct_edges = md;
   } else {
     // E' = distinct intra-community edges (compacted: the second LPA builds on it)
     int32_t* mark = nullptr;
     int64_t* pos = nullptr;
     int32_t *s2 = nullptr, *d2 = nullptr, *sub = nullptr, *subsize = nullptr;
-    LPA_TRY(sc.get(&mark, m));
-    LPA_TRY(sc.get(&pos, m + 1));
-    if (m > 0) {
-      hipLaunchKernelGGL(k_mark_intra, dim3(grid_for(m)), dim3(256), 0, s, ek, first, m, L, mark);
+    LPA_TRY(sc.get(&mark, md));
+    LPA_TRY(sc.get(&pos, md + 1));
+    if (md > 0) {
+      hipLaunchKernelGGL(k_mark_intra, dim3(grid_for(md)), dim3(256), 0, s, ek, md, L, mark);
       LPA_HIP(hipGetLastError());
     }
-    LPA_TRY(exclusive_scan_i32_i64(mark, pos, m, s));
+    LPA_TRY(exclusive_scan_i32_i64(mark, pos, md, s));
     int64_t m2 = 0;
     unsigned long long nbad = 0;
-    LPA_HIP(hipMemcpyAsync(&m2, pos + m, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipMemcpyAsync(&m2, pos + md, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipMemcpyAsync(&nbad, cnt + 3, sizeof(nbad), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));   // the one round trip: E' size for the build
     if (nbad) return bad_labels(nbad, V);
@@ -375,27 +403,27 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     LPA_TRY(sc.get(&d2, m2));
     LPA_TRY(sc.get(&sub, V));
     LPA_TRY(sc.get(&subsize, V));
-    if (m > 0) {
-      hipLaunchKernelGGL(k_split_marked, dim3(grid_for(m)), dim3(256), 0, s, ek, mark, pos, m, s2, d2);
+    if (md > 0) {
+      hipLaunchKernelGGL(k_split_marked, dim3(grid_for(md)), dim3(256), 0, s, ek, mark, pos, md, s2, d2);
       LPA_HIP(hipGetLastError());
     }
     // second LPA on the induced simple subgraph (same device, same stream)
     lpa_graph* h = nullptr;
-    LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE, &h));
+    LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE | kFlagNoLocality, &h));
     int rc = run_supersteps(h, sub_iter, nullptr);
     if (rc == LPA_OK) rc = gather_labels(h, sub);
     if (rc == LPA_OK && hipStreamSynchronize(s) != hipSuccess) rc = LPA_EHIP;
     destroy(h);
     if (rc != LPA_OK) return rc;
     LPA_HIP(hipMemsetAsync(subsize, 0, sizeof(int32_t) * V, s));
-    hipLaunchKernelGGL(k_histogram, dim3(grid_for(V)), dim3(256), 0, s, sub, V, subsize, cnt + 3);
+    hipLaunchKernelGGL(k_histogram, dim3(grid_bh(V)), dim3(256), 0, s, sub, V, subsize, cnt + 3);
     LPA_HIP(hipGetLastError());
     // segment of a sub-label group = the community of the sub-label vertex: L itself
     LPA_TRY(segmented_threshold(g, sc, subsize, L, V, thr, cnt + 4));
     hipLaunchKernelGGL(k_flag, dim3(grid_for(V)), dim3(256), 0, s, sub, subsize, L, thr, V, fl,
                        segflag, cnt + 1);
     LPA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(V)), dim3(256), 0, s, segflag, V, cnt + 2);
+    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_cnt(V)), dim3(256), 0, s, segflag, V, cnt + 2);
     LPA_HIP(hipGetLastError());
     unsigned long long h_cnt[8];
     LPA_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
@@ -407,7 +435,7 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     sum.n_flagged = (int64_t)h_cnt[1];
     sum.n_communities = (int64_t)h_cnt[0];
     sum.n_communities_flagged = (int64_t)h_cnt[2];
-    sum.distinct_edges = (int64_t)h_cnt[5];
+    sum.distinct_edges = md;
   }
 
   if (size_hist) {

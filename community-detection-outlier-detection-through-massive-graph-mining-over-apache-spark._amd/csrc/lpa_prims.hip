@@ -4,6 +4,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <mutex>
+
 #include "lpa_internal.h"
 
 namespace lpa {
@@ -103,8 +105,8 @@ int scan_impl(const Tin* in, Tout* out, int64_t n, hipStream_t s) {
   }
   Tout* part = nullptr;
   Tout* partx = nullptr;
-  LPA_HIP(hipMalloc((void**)&part, sizeof(Tout) * nblk));
-  LPA_HIP(hipMalloc((void**)&partx, sizeof(Tout) * (nblk + 1)));
+  LPA_TRY(tmp_alloc((void**)&part, sizeof(Tout) * nblk, s));
+  LPA_TRY(tmp_alloc((void**)&partx, sizeof(Tout) * (nblk + 1), s));
   hipLaunchKernelGGL((k_scan_reduce<Tin, Tout>), dim3((unsigned)nblk), dim3(kThreads), 0, s, in,
                      n, part);
   LPA_HIP(hipGetLastError());
@@ -114,8 +116,8 @@ int scan_impl(const Tin* in, Tout* out, int64_t n, hipStream_t s) {
                        n, out, (const Tout*)partx);
     LPA_HIP(hipGetLastError());
   }
-  LPA_HIP(hipFree(part));
-  LPA_HIP(hipFree(partx));
+  tmp_free(part, s);
+  tmp_free(partx, s);
   return rc;
 }
 
@@ -196,6 +198,41 @@ __global__ __launch_bounds__(kThreads) void k_rs_scatter(const u64* __restrict__
 
 }  // namespace
 
+// Stream-ordered scratch on the device's default memory pool, whose release threshold
+// is raised once per device so that repeated calls reuse the memory (the pool is
+// trimmed when a handle is destroyed): hipFree synchronised the device on every
+// temporary -- 530 frees, 345 ms of host time in the C3 outlier profile.
+int tmp_alloc(void** p, size_t bytes, hipStream_t s) {
+  static std::once_flag once[64];
+  int dev = 0;
+  LPA_HIP(hipGetDevice(&dev));
+  if (dev >= 0 && dev < 64)
+    std::call_once(once[dev], [dev]() {
+      hipMemPool_t pool = nullptr;
+      if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+      }
+    });
+  hipError_t e = hipMallocAsync(p, bytes > 0 ? bytes : 1, s);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    (void)hipGetLastError();
+    set_error("hipMallocAsync(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+    return LPA_ENOMEM;
+  }
+  return LPA_OK;
+}
+
+void tmp_free(void* p, hipStream_t s) {
+  if (p) (void)hipFreeAsync(p, s);
+}
+
+void tmp_trim(int device) {
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) (void)hipMemPoolTrimTo(pool, 0);
+}
+
 int bits_for(uint64_t maxval) { return maxval == 0 ? 0 : 64 - __builtin_clzll(maxval); }
 
 int exclusive_scan_i32_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s) {
@@ -217,8 +254,8 @@ int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshift
   const int64_t nh = 256 * nblk;
   u32* hist = nullptr;
   u32* offs = nullptr;
-  LPA_HIP(hipMalloc((void**)&hist, sizeof(u32) * nh));
-  LPA_HIP(hipMalloc((void**)&offs, sizeof(u32) * (nh + 1)));
+  LPA_TRY(tmp_alloc((void**)&hist, sizeof(u32) * nh, s));
+  LPA_TRY(tmp_alloc((void**)&offs, sizeof(u32) * (nh + 1), s));
   u64* a = keys;
   u64* b = tmp;
   int rc = LPA_OK;
@@ -236,8 +273,8 @@ int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshift
     b = t;
   }
   if (rc == LPA_OK && a != keys) LPA_HIP(hipMemcpyAsync(keys, a, sizeof(u64) * n, hipMemcpyDeviceToDevice, s));
-  LPA_HIP(hipFree(hist));
-  LPA_HIP(hipFree(offs));
+  tmp_free(hist, s);
+  tmp_free(offs, s);
   return rc;
 }
 
