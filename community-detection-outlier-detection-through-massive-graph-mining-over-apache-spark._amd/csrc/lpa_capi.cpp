@@ -59,7 +59,7 @@ void destroy(lpa_graph* g) {
   void* bufs[] = {g->rp,   g->col,   g->new_of, g->old_of, g->deg,   g->lab[0], g->lab[1],
                   g->segs, g->e_src,  g->e_dst, g->de_keys, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
                   g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
-                  g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->items_cb,
+                  g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
                   g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt};
   for (void* p : bufs) dev_free(g, p);
@@ -138,6 +138,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FRONTIER_FRAC")) g->frontier_frac = atof(f);
   if (const char* f = getenv("LPA_MID_MERGED")) g->mid_merged = atoi(f) ? 1 : 0;
+  if (const char* f = getenv("LPA_HUB_FUSE")) g->hub_fuse = atoi(f) ? 1 : 0;
+  if (const char* f = getenv("LPA_FOLD_REBUILD")) g->fold_rebuild = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_BLOCK")) g->block_rows = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_BLOCK_AT")) g->block_at = atoi(f) < 0 ? 0 : (atoi(f) > 2 ? 2 : atoi(f));
   // internal builds (the outlier stage's L2 sub-graph): the locality order is a

@@ -718,6 +718,74 @@ __global__ __launch_bounds__(64 * kW) void k_hub_mid_all(const int32_t* __restri
 // T > kCombDirect: bucket partition of the staged words, kChunkUnits units per
 // count / scatter work item.
 // ---------------------------------------------------------------------------
+// Last-block hand-off (the converged supersteps fuse count + scan and bucket + final,
+// two dependent launches fewer).  What is handed off was built only by device-scope
+// atomics, which execute at the memory side, past the per-XCD L2s: so every wave
+// waits for its atomics to complete (vmcnt), the block takes a ticket, and the block
+// that draws the last one reads the totals with agent-scope loads, does the follow-up
+// pass and resets the tickets.  No release / acquire fences: at agent scope they write
+// back / invalidate the whole L2 of the XCD, and 2048 blocks doing so cost ~90 us.
+// Tickets are two-level (kTicketGroups counters, one 64-B line each, then one for the
+// groups): returning atomics on ONE address serialise at ~88 M/s, 2048 of them ~23 us.
+constexpr int kTicketGroups = 16;
+constexpr int kTicketStride = 16;  // uint32 per ticket line
+constexpr int kTicketWords = (kTicketGroups + 1) * kTicketStride;
+__device__ __forceinline__ bool last_block(uint32_t* tk) {
+  __shared__ int last;
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's device atomics have completed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u32 G = gridDim.x < (u32)kTicketGroups ? gridDim.x : (u32)kTicketGroups;
+    const u32 gi = blockIdx.x % G;
+    const u32 in_group = (gridDim.x - gi + G - 1) / G;
+    uint32_t* t1 = tk + gi * kTicketStride;
+    uint32_t* t2 = tk + kTicketGroups * kTicketStride;
+    last = 0;
+    if (__hip_atomic_fetch_add(t1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1) {
+      __hip_atomic_store(t1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(t2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+        __hip_atomic_store(t2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = 1;
+      }
+    }
+  }
+  __syncthreads();
+  return last != 0;
+}
+__device__ __forceinline__ int32_t ld_agent(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 ld_agent(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// gcur[k] = exclusive prefix of ghist[k] for every queued row, by the waves of one
+// block (k_hub_scan, or the last block of a fused k_hub_count)
+template <bool kAgent>
+__device__ __forceinline__ void scan_rows(int q0, int qstep, int nC, const int32_t* __restrict__ listC,
+                                          const int32_t* __restrict__ wcount, const int64_t* __restrict__ hoff,
+                                          const int32_t* __restrict__ ghist, int32_t* __restrict__ gcur) {
+  const int lane = threadIdx.x & 63;
+  for (int q = q0; q < nC; q += qstep) {
+    const int64_t h = listC[q];
+    const int K = 1 << comb_lgK(wcount[h]);
+    const int32_t* gh = ghist + hoff[h];
+    int32_t* gc = gcur + hoff[h];
+    int carry = 0;
+    for (int k0 = 0; k0 < K; k0 += 64) {
+      const int v = k0 + lane < K ? (kAgent ? ld_agent(gh + k0 + lane) : gh[k0 + lane]) : 0;
+      int incl = v;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+      }
+      if (k0 + lane < K) gc[k0 + lane] = carry + incl - v;
+      carry += __shfl(incl, 63, 64);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_hub_count(const u64* __restrict__ itemsCC,
                                                    const int32_t* __restrict__ lcnt,
                                                    const int64_t* __restrict__ rp,
@@ -726,7 +794,10 @@ __global__ __launch_bounds__(256) void k_hub_count(const u64* __restrict__ items
                                                    const u64* __restrict__ stage,
                                                    const int32_t* __restrict__ wcount,
                                                    const int64_t* __restrict__ hoff,
-                                                   int32_t* __restrict__ ghist) {
+                                                   int32_t* __restrict__ ghist,
+                                                   uint32_t* __restrict__ ticket,  // fused scan: non-null
+                                                   const int32_t* __restrict__ listC,
+                                                   int32_t* __restrict__ gcur) {
   __shared__ int hist[kMaxBuckets];
   constexpr int NC = kSegArcs / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -759,6 +830,7 @@ __global__ __launch_bounds__(256) void k_hub_count(const u64* __restrict__ items
       if (hist[k]) atomicAdd(&gh[k], hist[k]);
     __syncthreads();
   }
+  if (ticket && last_block(ticket)) scan_rows<true>(threadIdx.x >> 6, 4, lcnt[1], listC, wcount, hoff, ghist, gcur);
 }
 
 // one wave per queued row: gcur[k] = exclusive prefix of ghist[k]
@@ -768,26 +840,7 @@ __global__ __launch_bounds__(256) void k_hub_scan(const int32_t* __restrict__ li
                                                   const int64_t* __restrict__ hoff,
                                                   const int32_t* __restrict__ ghist,
                                                   int32_t* __restrict__ gcur) {
-  const int lane = threadIdx.x & 63;
-  const int nC = lcnt[1];
-  for (int q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nC; q += gridDim.x * 4) {
-    const int64_t h = listC[q];
-    const int K = 1 << comb_lgK(wcount[h]);
-    const int32_t* gh = ghist + hoff[h];
-    int32_t* gc = gcur + hoff[h];
-    int carry = 0;
-    for (int k0 = 0; k0 < K; k0 += 64) {
-      const int v = k0 + lane < K ? gh[k0 + lane] : 0;
-      int incl = v;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o;
-      }
-      if (k0 + lane < K) gc[k0 + lane] = carry + incl - v;
-      carry += __shfl(incl, 63, 64);
-    }
-  }
+  scan_rows<false>(blockIdx.x * 4 + (threadIdx.x >> 6), gridDim.x * 4, lcnt[1], listC, wcount, hoff, ghist, gcur);
 }
 
 __global__ __launch_bounds__(256) void k_hub_scatter(const u64* __restrict__ itemsCC,
@@ -853,6 +906,27 @@ __global__ __launch_bounds__(256) void k_hub_scatter(const u64* __restrict__ ite
   }
 }
 
+// write the bucketed rows' labels and reset their combine state, by waves
+// [q0, q0 + qstep ...) (k_hub_final, or the last block of a fused k_hub_bucket)
+template <bool kAgent>
+__device__ __forceinline__ void final_rows(int q0, int qstep, int nC, const int32_t* __restrict__ listC,
+                                           int32_t* __restrict__ wcount, const int64_t* __restrict__ hoff,
+                                           int32_t* __restrict__ ghist, u64* __restrict__ hub_best,
+                                           int32_t* __restrict__ Ln) {
+  const int lane = threadIdx.x & 63;
+  for (int q = q0; q < nC; q += qstep) {
+    const int64_t h = listC[q];
+    const int K = 1 << comb_lgK(wcount[h]);
+    int32_t* gh = ghist + hoff[h];
+    for (int k = lane; k < K; k += 64) gh[k] = 0;
+    if (lane == 0) {
+      Ln[h] = (int32_t)(~(u32)(kAgent ? ld_agent(hub_best + h) : hub_best[h]));
+      hub_best[h] = 0ull;
+      wcount[h] = 0;
+    }
+  }
+}
+
 // one block per (row, bucket): after the scatter, bucket k of row h is
 // scat[rp[h] + gcur[k] - ghist[k], rp[h] + gcur[k])
 // kW waves per block (64.03 KB blocks: two per CU; kW = 8 gives 16 resident waves)
@@ -862,18 +936,27 @@ __global__ __launch_bounds__(64 * kW) void k_hub_bucket(const u64* __restrict__ 
                                                     const int64_t* __restrict__ rp,
                                                     const u64* __restrict__ scat,
                                                     const int64_t* __restrict__ hoff,
-                                                    const int32_t* __restrict__ ghist,
+                                                    const int32_t* ghist,  // also ghist_w (fused final)
                                                     const int32_t* __restrict__ gcur,
                                                     u64* __restrict__ hub_best,
-                                                    int32_t* __restrict__ err) {
+                                                    int32_t* __restrict__ err,
+                                                    // fused final (non-null ticket): the last block
+                                                    uint32_t* __restrict__ ticket,
+                                                    const int32_t* __restrict__ listC,
+                                                    int32_t* __restrict__ wcount,
+                                                    int32_t* ghist_w,
+                                                    int32_t* __restrict__ Ln,
+                                                    int32_t* __restrict__ lcnt_next) {
   __shared__ u64 tab[kCombSlots];
   __shared__ u64 redw[kW];
   __shared__ int32_t ovf;  // a pass whose distinct labels overflowed the table
   const int n = lcnt[2];
-  if ((int)blockIdx.x >= n) return;
-  for (int i = threadIdx.x; i < kCombSlots; i += 64 * kW) tab[i] = 0ull;
-  if (threadIdx.x == 0) ovf = 0;
-  __syncthreads();
+  if ((int)blockIdx.x >= n && !ticket) return;
+  if ((int)blockIdx.x < n) {  // uniform (blocks without items only take their ticket)
+    for (int i = threadIdx.x; i < kCombSlots; i += 64 * kW) tab[i] = 0ull;
+    if (threadIdx.x == 0) ovf = 0;
+    __syncthreads();
+  }
   for (int it = blockIdx.x; it < n; it += gridDim.x) {
     const u64 item = itemsCB[it];
     const int64_t h = (int64_t)(item >> 32);
@@ -912,6 +995,10 @@ __global__ __launch_bounds__(64 * kW) void k_hub_bucket(const u64* __restrict__ 
     }
     if (threadIdx.x == 0 && best) atomicMax(&hub_best[h], best);
   }
+  if (ticket && last_block(ticket)) {
+    if (threadIdx.x < 8) lcnt_next[threadIdx.x] = 0;
+    final_rows<true>(threadIdx.x >> 6, kW, lcnt[1], listC, wcount, hoff, ghist_w, hub_best, Ln);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_hub_final(const int32_t* __restrict__ listC,
@@ -922,21 +1009,10 @@ __global__ __launch_bounds__(256) void k_hub_final(const int32_t* __restrict__ l
                                                    u64* __restrict__ hub_best,
                                                    int32_t* __restrict__ Ln,
                                                    int32_t* __restrict__ lcnt_next) {
-  const int lane = threadIdx.x & 63;
   // the next superstep's queue counters (the other parity; no memset launch)
   if (blockIdx.x == 0 && threadIdx.x < 8) lcnt_next[threadIdx.x] = 0;
-  const int nC = lcnt[1];
-  for (int q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nC; q += gridDim.x * 4) {
-    const int64_t h = listC[q];
-    const int K = 1 << comb_lgK(wcount[h]);
-    int32_t* gh = ghist + hoff[h];
-    for (int k = lane; k < K; k += 64) gh[k] = 0;
-    if (lane == 0) {
-      Ln[h] = (int32_t)(~(u32)hub_best[h]);
-      hub_best[h] = 0ull;
-      wcount[h] = 0;
-    }
-  }
+  final_rows<false>(blockIdx.x * 4 + (threadIdx.x >> 6), gridDim.x * 4, lcnt[1], listC, wcount, hoff, ghist,
+                    hub_best, Ln);
 }
 
 __global__ void k_hub_bounds(const int32_t* __restrict__ deg_own, int64_t n_hub,
@@ -1012,6 +1088,9 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   LPA_TRY(dev_alloc(g, (void**)&g->hub_lists, sizeof(int32_t) * 6 * n));
   LPA_TRY(dev_alloc(g, (void**)&g->hub_lcnt, sizeof(int32_t) * 16));
   LPA_HIP(hipMemsetAsync(g->hub_lcnt, 0, sizeof(int32_t) * 16, s));
+  // the fused count / bucket kernels' two-level tickets
+  LPA_TRY(dev_alloc(g, (void**)&g->hub_tickets, sizeof(uint32_t) * 2 * kTicketWords));
+  LPA_HIP(hipMemsetAsync(g->hub_tickets, 0, sizeof(uint32_t) * 2 * kTicketWords, s));
   {
     // rows [hub_lane_begin, n_hub) have <= kLaneUnits units (degree-descending order)
     int64_t* d_pos = nullptr;
@@ -1046,29 +1125,44 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   // follows the row bins on the third)
   hipStream_t sd = !fork ? s : (block_mode_now(g) && g->block_at == 2) ? g->aux_stream[1] : g->aux_stream[2];
   const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
+  // fused (converged supersteps, few bucketed rows): the scan by the last block of
+  // k_hub_count, the final pass by the last block of k_hub_bucket -- 5 dependent
+  // launches -> 3; the label-dense supersteps, with ~10^2 bucketed rows of up to 4K
+  // buckets each, keep the parallel k_hub_scan / k_hub_final
+  const bool fuse = g->hub_fuse && !fork;
+  uint32_t* tickets = g->hub_tickets;
+  int32_t* lcnt_next = g->hub_lcnt + 8 * (g->par ^ 1);
   auto bucket_path = [&]() -> int {
-    hipLaunchKernelGGL(k_hub_count, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
-                       g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->ghist);
+    // fused: grids of one resident wave of blocks (fewer tickets)
+    hipLaunchKernelGGL(k_hub_count, dim3(fuse ? grid_cap(g->n_hub_chunks, 1024) : ncl), dim3(256), 0, sd,
+                       g->items_cc, lcnt, g->rp,
+                       g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->ghist,
+                       fuse ? tickets : (uint32_t*)nullptr, listC, g->gcur);
     LPA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_hub_scan, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
-                       lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->gcur);
-    LPA_HIP(hipGetLastError());
+    if (!fuse) {
+      hipLaunchKernelGGL(k_hub_scan, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
+                         lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->gcur);
+      LPA_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_hub_scatter, dim3(ncl), dim3(256), 0, sd, g->items_cc, lcnt, g->rp,
                        g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, g->hub_hoff, g->gcur, g->scat);
     LPA_HIP(hipGetLastError());
+    uint32_t* tb = fuse ? tickets + kTicketWords : (uint32_t*)nullptr;
+    const unsigned nbk = grid_cap(g->n_hub_buckets, fuse ? 512 : 2048);
     if (g->hub_waves == 4)
-      hipLaunchKernelGGL(k_hub_bucket<4>, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(256), 0, sd,
+      hipLaunchKernelGGL(k_hub_bucket<4>, dim3(nbk), dim3(256), 0, sd,
                          g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
-                         g->hub_best, g->dev_err);
+                         g->hub_best, g->dev_err, tb, listC, g->hub_wcount, g->ghist, Lown, lcnt_next);
     else
-      hipLaunchKernelGGL(k_hub_bucket<8>, dim3(grid_cap(g->n_hub_buckets, 2048)), dim3(512), 0, sd,
+      hipLaunchKernelGGL(k_hub_bucket<8>, dim3(nbk), dim3(512), 0, sd,
                          g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
-                         g->hub_best, g->dev_err);
+                         g->hub_best, g->dev_err, tb, listC, g->hub_wcount, g->ghist, Lown, lcnt_next);
     LPA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
-                       lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown,
-                       g->hub_lcnt + 8 * (g->par ^ 1));
-    LPA_HIP(hipGetLastError());
+    if (!fuse) {
+      hipLaunchKernelGGL(k_hub_final, dim3(grid_cap((n + 3) / 4, 256)), dim3(256), 0, sd, listC,
+                         lcnt, g->hub_wcount, g->hub_hoff, g->ghist, g->hub_best, Lown, lcnt_next);
+      LPA_HIP(hipGetLastError());
+    }
     return LPA_OK;
   };
   if (fork) {

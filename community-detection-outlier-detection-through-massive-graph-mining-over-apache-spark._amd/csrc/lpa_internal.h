@@ -147,10 +147,13 @@ struct lpa_graph {
   int32_t* gcur = nullptr;        // [n_hub_buckets] bucket offsets / scatter cursors
   int32_t* hub_lists = nullptr;   // [6 n_hub] queued rows: mid (T <= 1024), bucketed, wave path,
                                   //   mid (T <= 2048), mid (T <= 6144), small (list S)
+  uint32_t* hub_tickets = nullptr; // fused hub kernels' last-block tickets (lpa_hub.hip)
   int32_t* hub_lcnt = nullptr;    // [2][8] per parity, queue lengths: mid1, bucketed, bucket items,
                                   //   chunk items, wave path, mid2, mid3, small (list S)
   int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
   int block_rows = 1;             // LPA_BLOCK=0: label-dense supersteps also stage the rows above by units
+  int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches
+  int fold_rebuild = 1;           // LPA_FOLD_REBUILD=0: captured converged supersteps keep the rebuild launch
   int block_at = 0;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the
                                   // main stream, or (2) on the fourth stream, concurrent with them
   int64_t unit_lane_begin = 0;    // hub_uoff[hub_lane_begin]

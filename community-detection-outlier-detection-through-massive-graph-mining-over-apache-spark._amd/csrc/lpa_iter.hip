@@ -1202,6 +1202,37 @@ struct FrontierMarks {
 };
 static_assert(kSegArcs == 512, "unit of a position: (p - rp[row]) >> 9");
 
+// al[i] = L[col[i]] over the whole arc array by the calling grid (grid-stride): each
+// thread keeps 8 gathers in flight (two int4 column quads), col / al streamed
+// non-temporally
+__device__ __forceinline__ void rebuild_all(const int32_t* __restrict__ col, int64_t arcs,
+                                            const int32_t* __restrict__ Ln, int32_t* __restrict__ al) {
+  const int64_t n4 = arcs >> 2;
+  const v4i* __restrict__ c4 = reinterpret_cast<const v4i*>(col);
+  v4i* __restrict__ a4 = reinterpret_cast<v4i*>(al);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; q + stride < n4; q += 2 * stride) {
+    const v4i c0 = __builtin_nontemporal_load(c4 + q);
+    const v4i c1 = __builtin_nontemporal_load(c4 + q + stride);
+    v4i r0, r1;
+    r0.x = Ln[c0.x]; r0.y = Ln[c0.y]; r0.z = Ln[c0.z]; r0.w = Ln[c0.w];
+    r1.x = Ln[c1.x]; r1.y = Ln[c1.y]; r1.z = Ln[c1.z]; r1.w = Ln[c1.w];
+    __builtin_nontemporal_store(r0, a4 + q);
+    __builtin_nontemporal_store(r1, a4 + q + stride);
+  }
+  if (q < n4) {
+    const v4i c0 = __builtin_nontemporal_load(c4 + q);
+    v4i r0;
+    r0.x = Ln[c0.x]; r0.y = Ln[c0.y]; r0.z = Ln[c0.z]; r0.w = Ln[c0.w];
+    __builtin_nontemporal_store(r0, a4 + q);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (arcs & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    al[i] = Ln[col[i]];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ chlist,
                                                     const uint4* __restrict__ chflag16, int64_t ngroups,
                                                     const int32_t* __restrict__ cowner,
@@ -1214,7 +1245,8 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
                                                     int32_t* __restrict__ al, int64_t thr,
                                                     FrontierMarks fm, int32_t* __restrict__ fr_all_next,
                                                     int frontier, int64_t fr_thr,
-                                                    int32_t* __restrict__ Lold) {
+                                                    int32_t* __restrict__ Lold,
+                                                    const int32_t* __restrict__ col_fold, int64_t arcs) {
   // the next superstep's counters (the other parity; no memset launch)
   if (blockIdx.x == 0 && threadIdx.x < 2) counters_next[threadIdx.x] = 0ull;
   const bool rebuild = rebuild_wanted(counters, thr);
@@ -1227,6 +1259,10 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  // col_fold (captured converged supersteps): a wanted rebuild is done here, the plain
+  // form, instead of by a k_al_rebuild_hot launch that nearly always returns at once
+  // (one dependent launch fewer per converged superstep)
+  if (rebuild && col_fold) rebuild_all(col_fold, arcs, Ln, al);
   // one-chunk columns from the list: a lane each, longer rows of positions by the wave
   if (!rebuild) {
     const int64_t nl = (int64_t)counters[0];
@@ -1341,30 +1377,7 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
                                                     const int32_t* __restrict__ Ln,
                                                     int32_t* __restrict__ al) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
-  const int64_t n4 = arcs >> 2;
-  const v4i* __restrict__ c4 = reinterpret_cast<const v4i*>(col);
-  v4i* __restrict__ a4 = reinterpret_cast<v4i*>(al);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; q + stride < n4; q += 2 * stride) {
-    const v4i c0 = __builtin_nontemporal_load(c4 + q);
-    const v4i c1 = __builtin_nontemporal_load(c4 + q + stride);
-    v4i r0, r1;
-    r0.x = Ln[c0.x]; r0.y = Ln[c0.y]; r0.z = Ln[c0.z]; r0.w = Ln[c0.w];
-    r1.x = Ln[c1.x]; r1.y = Ln[c1.y]; r1.z = Ln[c1.z]; r1.w = Ln[c1.w];
-    __builtin_nontemporal_store(r0, a4 + q);
-    __builtin_nontemporal_store(r1, a4 + q + stride);
-  }
-  if (q < n4) {
-    const v4i c0 = __builtin_nontemporal_load(c4 + q);
-    v4i r0;
-    r0.x = Ln[c0.x]; r0.y = Ln[c0.y]; r0.z = Ln[c0.z]; r0.w = Ln[c0.w];
-    __builtin_nontemporal_store(r0, a4 + q);
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (arcs & 3)) {
-    const int64_t i = (n4 << 2) + threadIdx.x;
-    al[i] = Ln[col[i]];
-  }
+  rebuild_all(col, arcs, Ln, al);
 }
 
 // Same with the labels of the kHotLabels highest-degree vertices (slots
@@ -1647,8 +1660,10 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // refresh al[] for L_next (after the exchange, so every rank sees all changes) of the
 // superstep of parity `par`; diff_done: the tally schedule already ran the diff per
 // stream (launch_tally) or the exchange listed the changes
+// fold_rebuild: k_al_scatter does a wanted rebuild itself (captured converged
+// supersteps: saves the rebuild launch, which is almost never wanted there)
 int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par,
-                   hipEvent_t ev_scatter = nullptr) {
+                   hipEvent_t ev_scatter = nullptr, bool fold_rebuild = false) {
   if (g->arcs == 0) return LPA_OK;
   hipStream_t s = g->stream;
   // this superstep's counters (zeroed by the previous k_al_scatter or at build)
@@ -1667,11 +1682,12 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
                      (g->n_chunk_scan + 15) / 16, g->cowner, g->cch, ctr,
                      g->counters + 4 * (par ^ 1), g->cptr,
                      g->cpos, Ln, g->al, thr, fm, g->fr_all + (par ^ 1), g->frontier,
-                     (int64_t)(g->frontier_frac * (double)g->arcs), const_cast<int32_t*>(Lc));
+                     (int64_t)(g->frontier_frac * (double)g->arcs), const_cast<int32_t*>(Lc),
+                     fold_rebuild ? g->col : (const int32_t*)nullptr, g->arcs);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   if (ev_scatter) LPA_HIP(hipEventRecord(ev_scatter, s));  // profiling: scatter | rebuild
-  LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
+  if (!fold_rebuild) LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -1746,7 +1762,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       if (!g->gexec[key])
         LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
           int rc = launch_tally(g, Lown, nullptr, Lc, Ln, true);
-          if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true, g->par);
+          if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true, g->par, nullptr, g->fold_rebuild != 0);
           return rc;
         }));
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
