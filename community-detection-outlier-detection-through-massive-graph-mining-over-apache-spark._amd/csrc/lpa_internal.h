@@ -152,6 +152,8 @@ struct lpa_graph {
                                   //   chunk items, wave path, mid2, mid3, small (list S)
   int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
   int block_rows = 1;             // LPA_BLOCK=0: label-dense supersteps also stage the rows above by units
+  int dense_peel = 2;             // LPA_DENSE_PEEL: peel rounds of the tallies in the label-dense supersteps (2: measured
+                                  // best of 0/2/4/8 at C3, superstep 2 5.82 -> 5.75 ms)
   int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches
   int fold_rebuild = 1;           // LPA_FOLD_REBUILD=0: captured converged supersteps keep the rebuild launch
   int block_at = 0;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the

@@ -220,7 +220,8 @@ struct Batch {
 };
 
 template <int NC>
-__device__ __forceinline__ void peel_batch(Batch<NC>& bt, const u32 (&lab)[NC], int nch, int lane) {
+__device__ __forceinline__ void peel_batch(Batch<NC>& bt, const u32 (&lab)[NC], int nch, int lane,
+                                           int pmax = kPeelMax) {
   u32 mask = 0u;
 #pragma unroll
   for (int u = 0; u < NC; ++u)
@@ -229,7 +230,7 @@ __device__ __forceinline__ void peel_batch(Batch<NC>& bt, const u32 (&lab)[NC], 
   bt.npeel = 0;
   bt.pbest = 0ull;
 #pragma unroll 1
-  for (int p = 0; p < kPeelMax; ++p) {
+  for (int p = 0; p < pmax; ++p) {
     const u64 live = __ballot(mask != 0u);
     if (live == 0ull) break;
     // candidate: the first untallied label of the first lane that has one
@@ -487,7 +488,7 @@ __device__ __forceinline__ void row_load(u32 (&raw)[NC], const int32_t* __restri
 template <int NC>
 __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r, int64_t v,
                                           int32_t* __restrict__ Ln, u64* tab, uint16_t* lst, int lane,
-                                          u64 lt) {
+                                          u64 lt, int pmax) {
   const int d = span_len(r);
   if (d == 0) return;
   u32 lab[NC];
@@ -497,7 +498,7 @@ __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r
   lg = lg < 6 ? 6 : lg;
   const int nch = (d + 63) >> 6;
   Batch<NC> bt;
-  peel_batch<NC>(bt, lab, nch, lane);
+  peel_batch<NC>(bt, lab, nch, lane, pmax);
   if (!bt.any) {
     // every vote is in a peel group: the mode is their maximum, no LDS needed
     if (lane == 0) Ln[v] = (int32_t)(~(u32)bt.pbest);
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend, const int32_t* __restrict__ flist,
                                                   const int32_t* __restrict__ fcnt_b,
-                                                  const int32_t* __restrict__ fr_all) {
+                                                  const int32_t* __restrict__ fr_all, int pmax) {
   constexpr int kCap = 2 * 64 * NC;
   __shared__ u64 tab_all[4][kCap];
   __shared__ uint16_t lst_all[4][64 * NC];
@@ -545,17 +546,17 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   while (true) {
     row_load<NC>(rc, al, s2, lane);
     RowSpan s3 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(ra, s0, br.row(i), Ln, tab, lst, lane, lt);
+    row_tally<NC>(ra, s0, br.row(i), Ln, tab, lst, lane, lt, pmax);
     i += stride;
     if (i >= br.n) break;
     row_load<NC>(ra, al, s3, lane);
     RowSpan s4 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(rb, s1, br.row(i), Ln, tab, lst, lane, lt);
+    row_tally<NC>(rb, s1, br.row(i), Ln, tab, lst, lane, lt, pmax);
     i += stride;
     if (i >= br.n) break;
     row_load<NC>(rb, al, s4, lane);
     RowSpan s5 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(rc, s2, br.row(i), Ln, tab, lst, lane, lt);
+    row_tally<NC>(rc, s2, br.row(i), Ln, tab, lst, lane, lt, pmax);
     i += stride;
     if (i >= br.n) break;
     s0 = s3;
@@ -584,7 +585,7 @@ __global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* _
                                                                int64_t h1,
                                                                const int32_t* __restrict__ flist,
                                                                const int32_t* __restrict__ fcnt0,
-                                                               const int32_t* __restrict__ fr_all) {
+                                                               const int32_t* __restrict__ fr_all, int pmax) {
   static_assert((1 << kLg) >= 2 * kBlockMaxDeg, "table load <= 1/2");
   constexpr int kSlots = 1 << kLg;
   constexpr int kT = 64 * kBlockWaves;
@@ -611,7 +612,7 @@ __global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* _
       load_labels<kChunks>(lab, al, c0, e, lane);
       const int nch = (int)min<int64_t>(kChunks, (e - c0 + 63) >> 6);
       Batch<kChunks> bt;
-      peel_batch<kChunks>(bt, lab, nch, lane);
+      peel_batch<kChunks>(bt, lab, nch, lane, pmax);
       int unused = 0;
       hash_batch<kChunks, false>(tab, nullptr, unused, 32 - lg, (1u << lg) - 1u, bt, lab, nch, lane, lt);
     }
@@ -820,7 +821,7 @@ __device__ __forceinline__ void unit_load(u32 (&raw)[kChunks], const int32_t* __
 // tally one unit whose labels are in `raw` (loaded earlier)
 __device__ __forceinline__ void unit_tally(const u32 (&raw)[kChunks], const Segment& d, int64_t u,
                                            u64* __restrict__ stage, int32_t* __restrict__ ucnt,
-                                           u64* tab, uint16_t* lst, int lane, u64 lt) {
+                                           u64* tab, uint16_t* lst, int lane, u64 lt, int pmax) {
   const int len = d.len & 1023;
   if (len == 0) return;
   u32 lab[kChunks];
@@ -830,7 +831,7 @@ __device__ __forceinline__ void unit_tally(const u32 (&raw)[kChunks], const Segm
   // staging slots of this unit: stage[begin .. begin + words) (words <= len)
   u64* st = stage + d.begin;
   Batch<kChunks> bt;
-  peel_batch<kChunks>(bt, lab, nch, lane);
+  peel_batch<kChunks>(bt, lab, nch, lane, pmax);
   if (!bt.any) {
     // every vote is in a peel group: the unit's words are the peel groups
     if (lane < bt.npeel) st[lane] = bt.pword;
@@ -855,7 +856,7 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
                                                    int32_t* __restrict__ ucnt,
                                                    const int32_t* __restrict__ ulist,
                                                    const int32_t* __restrict__ fcnt_u,
-                                                   const int32_t* __restrict__ fr_all) {
+                                                   const int32_t* __restrict__ fr_all, int pmax) {
   constexpr int kCap = 2 * 64 * kChunks;
   __shared__ u64 tab_all[4][kCap];
   __shared__ uint16_t lst_all[4][64 * kChunks];
@@ -883,17 +884,17 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
   while (true) {
     unit_load(rc, al, d2, lane);
     Segment d3 = load_unit(units, ui, u + 3 * stride);
-    unit_tally(ra, d0, ui.id(u), stage, ucnt, tab, lst, lane, lt);
+    unit_tally(ra, d0, ui.id(u), stage, ucnt, tab, lst, lane, lt, pmax);
     u += stride;
     if (u >= ui.n) break;
     unit_load(ra, al, d3, lane);
     Segment d4 = load_unit(units, ui, u + 3 * stride);
-    unit_tally(rb, d1, ui.id(u), stage, ucnt, tab, lst, lane, lt);
+    unit_tally(rb, d1, ui.id(u), stage, ucnt, tab, lst, lane, lt, pmax);
     u += stride;
     if (u >= ui.n) break;
     unit_load(rb, al, d4, lane);
     Segment d5 = load_unit(units, ui, u + 3 * stride);
-    unit_tally(rc, d2, ui.id(u), stage, ucnt, tab, lst, lane, lt);
+    unit_tally(rc, d2, ui.id(u), stage, ucnt, tab, lst, lane, lt, pmax);
     u += stride;
     if (u >= ui.n) break;
     d0 = d3;
@@ -1496,11 +1497,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // label-dense supersteps: the rows of <= kBlockMaxDeg arcs by k_lpa_block, only
   // the longer rows' units by k_lpa_units (block_mode_now)
   const bool blk = block_mode_now(g);
+  // peel rounds of the wave / unit / block tallies (LPA_DENSE_PEEL in the label-dense
+  // supersteps, where a round rarely retires more than a few votes)
+  const int pmax = g->since_reset < kDenseSupersteps ? g->dense_peel : kPeelMax;
   auto launch_block = [&](hipStream_t st) -> int {
     const int64_t nb = g->n_hub - g->hub_lane_begin;
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 6], st));
     hipLaunchKernelGGL(k_lpa_block<13>, dim3(cap_grid(nb, 2048)), dim3(64 * kBlockWaves), 0, st, g->rp, g->al,
-                       Lown, g->hub_lane_begin, g->n_hub, g->flist, fcnt, fr_all);
+                       Lown, g->hub_lane_begin, g->n_hub, g->flist, fcnt, fr_all, pmax);
     LPA_HIP(hipGetLastError());
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 7], st));
     return LPA_OK;
@@ -1519,7 +1523,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   const int64_t n_units = blk ? g->unit_lane_begin : g->n_segs;
   if (n_units > 0) {
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
-                       g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all);
+                       g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all, pmax);
     LPA_HIP(hipGetLastError());
     LPA_TRACE_POINT("seg");
   }
@@ -1531,7 +1535,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(mark(2 * (BIN + 1), ST));                                                         \
     if (n > 0) {                                                                              \
       hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, ST,  \
-                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all); \
+                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, pmax); \
       LPA_HIP(hipGetLastError());                                                             \
     }                                                                                         \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                     \
