@@ -154,6 +154,8 @@ struct lpa_graph {
   int block_rows = 1;             // LPA_BLOCK=0: label-dense supersteps also stage the rows above by units
   int dense_peel = 2;             // LPA_DENSE_PEEL: peel rounds of the tallies in the label-dense supersteps (2: measured
                                   // best of 0/2/4/8 at C3, superstep 2 5.82 -> 5.75 ms)
+  int dense_sort_after = 0;       // LPA_DENSE_SORT_AFTER: row-bin peel rounds before the sort, label-dense supersteps
+                                  // (0: measured best of 0/1/2/3 at C3, superstep 2 5.75 -> 5.62 ms)
   int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches
   int fold_rebuild = 1;           // LPA_FOLD_REBUILD=0: captured converged supersteps keep the rebuild launch
   int block_at = 0;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the

@@ -700,7 +700,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend, const int32_t* __restrict__ flist,
                                                   const int32_t* __restrict__ fcnt_b,
-                                                  const int32_t* __restrict__ fr_all) {
+                                                  const int32_t* __restrict__ fr_all, int sort_after) {
   static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "lane width");
   constexpr int RB = 512 / G;  // rows per batch
   const int lane = threadIdx.x & 63;
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       u64 act = __ballot(lb != kNone);
       u64 best = 0ull;
       for (int round = 0; act; ++round) {
-        if (round == kPeelSortAfter) {  // uniform: a label-dense chunk
+        if (round == sort_after) {  // uniform: a label-dense chunk
           best = group_mode_sort<G>(lb, lane);
           break;
         }
@@ -1500,6 +1500,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // peel rounds of the wave / unit / block tallies (LPA_DENSE_PEEL in the label-dense
   // supersteps, where a round rarely retires more than a few votes)
   const int pmax = g->since_reset < kDenseSupersteps ? g->dense_peel : kPeelMax;
+  // peel rounds of the row bins before a chunk is sorted (LPA_DENSE_SORT_AFTER)
+  const int sort_after = g->since_reset < kDenseSupersteps ? g->dense_sort_after : kPeelSortAfter;
   auto launch_block = [&](hipStream_t st) -> int {
     const int64_t nb = g->n_hub - g->hub_lane_begin;
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 6], st));
@@ -1558,7 +1560,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     if (n > 0) {                                                                             \
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
       hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
-                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all); \
+                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, \
+                         sort_after);                                                         \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
