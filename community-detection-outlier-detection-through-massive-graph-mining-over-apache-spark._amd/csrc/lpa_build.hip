@@ -578,6 +578,8 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     // first unit of the k_lpa_block rows
     LPA_HIP(hipMemcpyAsync(&g->unit_lane_begin, seg_off + g->hub_lane_begin, sizeof(int64_t),
                            hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipMemcpyAsync(&g->unit_block2_begin, seg_off + g->hub_block2_begin, sizeof(int64_t),
+                           hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
     g->device_bytes += (int64_t)sizeof(int64_t) * (n0 + 1);
   }

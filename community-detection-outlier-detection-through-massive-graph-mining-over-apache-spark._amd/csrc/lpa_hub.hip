@@ -1099,6 +1099,11 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
     LPA_HIP(hipGetLastError());
     LPA_HIP(hipMemcpyAsync(&g->hub_lane_begin, d_pos, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
+    // rows [hub_block2_begin, hub_lane_begin): the wide block tier (<= kBlockMaxDeg2)
+    hipLaunchKernelGGL(k_first_le, dim3(1), dim3(1), 0, s, deg_own, n, kBlockMaxDeg2, d_pos);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipMemcpyAsync(&g->hub_block2_begin, d_pos, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
     LPA_HIP(hipFree(d_pos));
   }
   LPA_TRY(dev_alloc(g, (void**)&g->items_cb, sizeof(u64) * nbk));
@@ -1118,6 +1123,9 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   // queue counters of this superstep's parity (zeroed by the previous k_hub_final)
   int32_t* lcnt = g->hub_lcnt + 8 * g->par;
   const int64_t hl = g->hub_lane_begin;
+  // rows classified for the combine in the fork: in block mode only those above the
+  // block tiers (their units staged nothing)
+  const int64_t hc = block_mode_now(g) ? block_rows_begin(g) : hl;
   // fork (label-dense supersteps): classify the > 8-unit rows first and start the
   // bucket path on its own stream; the mid tiers follow k_hub_small on the main
   // stream.  Otherwise everything runs in order on the main stream.
@@ -1166,12 +1174,12 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
     return LPA_OK;
   };
   if (fork) {
-    if (hl > 0) {
-      hipLaunchKernelGGL(k_hub_classify, dim3(grid_cap((hl + 3) / 4, 2048)), dim3(256), 0, s, hl, n,
+    if (hc > 0) {
+      hipLaunchKernelGGL(k_hub_classify, dim3(grid_cap((hc + 3) / 4, 2048)), dim3(256), 0, s, hc, n,
                          g->rp, g->hub_uoff, g->ucnt, g->hub_wcount, lists, lcnt, g->items_cb,
                          g->items_cc);
       LPA_HIP(hipGetLastError());
-      hipLaunchKernelGGL(k_hub_enqueue, dim3(grid_cap((hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
+      hipLaunchKernelGGL(k_hub_enqueue, dim3(grid_cap((hc + 255) / 256, 2048)), dim3(256), 0, s, hc, n,
                          g->hub_uoff, g->hub_wcount, lists, lcnt);
       LPA_HIP(hipGetLastError());
     }

@@ -32,6 +32,7 @@ constexpr int kWaveMaxDeg = 512;      // wave-per-vertex LDS hash for 64 < deg <
 constexpr int kWideMaxDeg = 1024;     // ... and (w16, 16 chunks, 2048-slot table) up to 1024
 constexpr int kSegArcs = 512;         // arcs per unit of a seg-bin row (one wave)
 constexpr int kBlockMaxDeg = 4096;    // seg rows up to this degree: k_lpa_block in the label-dense supersteps
+constexpr int kBlockMaxDeg2 = 8192;   // ... and up to this one: its 16-wave, 16K-slot form (one block per CU)
 constexpr int kTallyKernels = 13;                  // stats kernels 0..12: the tally
 constexpr int kTallyEv = 2 * kTallyKernels;        // events bracketing each tally kernel
 // + join, after exchange, after scatter, after rebuild, lists start, lists end,
@@ -151,16 +152,19 @@ struct lpa_graph {
   int32_t* hub_lcnt = nullptr;    // [2][8] per parity, queue lengths: mid1, bucketed, bucket items,
                                   //   chunk items, wave path, mid2, mid3, small (list S)
   int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
+  int64_t hub_block2_begin = 0;   // rows [hub_block2_begin, hub_lane_begin) have <= 16 units (wide block tier)
   int block_rows = 1;             // LPA_BLOCK=0: label-dense supersteps also stage the rows above by units
   int dense_peel = 2;             // LPA_DENSE_PEEL: peel rounds of the tallies in the label-dense supersteps (2: measured
                                   // best of 0/2/4/8 at C3, superstep 2 5.82 -> 5.75 ms)
   int dense_sort_after = 0;       // LPA_DENSE_SORT_AFTER: row-bin peel rounds before the sort, label-dense supersteps
                                   // (0: measured best of 0/1/2/3 at C3, superstep 2 5.75 -> 5.62 ms)
+  int block2 = 1;                 // LPA_BLOCK2=0: label-dense supersteps stage the rows of 4096 < deg <= 8192 by units
   int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches
   int fold_rebuild = 1;           // LPA_FOLD_REBUILD=0: captured converged supersteps keep the rebuild launch
   int block_at = 0;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the
                                   // main stream, or (2) on the fourth stream, concurrent with them
   int64_t unit_lane_begin = 0;    // hub_uoff[hub_lane_begin]
+  int64_t unit_block2_begin = 0;  // hub_uoff[hub_block2_begin]
   bool force_all_next = false;    // the next superstep tallies every row (after block mode)
   lpa::u64* items_cb = nullptr;   // [n_hub_buckets] (hub << 32 | bucket)
   lpa::u64* items_cc = nullptr;   // [n_hub_chunks]  (hub << 32 | 8-unit chunk)
@@ -265,6 +269,7 @@ int init_labels(lpa_graph* g);
 int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
 int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork);  // lpa_hub.hip
 bool block_mode_now(const lpa_graph* g);  // lpa_iter.hip
+int64_t block_rows_begin(const lpa_graph* g);  // first row of the block tiers (lpa_iter.hip)
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
 int frontier_all(lpa_graph* g, int par);  // next tally of parity `par` takes every row
 

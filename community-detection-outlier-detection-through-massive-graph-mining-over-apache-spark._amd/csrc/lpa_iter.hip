@@ -84,6 +84,7 @@ constexpr int kDenseSupersteps = 2;
 bool block_mode_now(const lpa_graph* g) {
   return g->block_rows && g->since_reset < kDenseSupersteps && g->hub_lane_begin < g->n_hub;
 }
+int64_t block_rows_begin(const lpa_graph* g) { return g->block2 ? g->hub_block2_begin : g->hub_lane_begin; }
 
 namespace {
 
@@ -577,8 +578,7 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
 // Grid-stride over the rows (frontier: over the listed bin-0 rows, those below h0
 // belong to the hub combine).
 // ---------------------------------------------------------------------------
-constexpr int kBlockWaves = kBlockMaxDeg / kSegArcs;
-template <int kLg>
+template <int kLg, int kBlockWaves>
 __global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* __restrict__ rp,
                                                                const int32_t* __restrict__ al,
                                                                int32_t* __restrict__ Ln, int64_t h0,
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* _
                                                                const int32_t* __restrict__ flist,
                                                                const int32_t* __restrict__ fcnt0,
                                                                const int32_t* __restrict__ fr_all, int pmax) {
-  static_assert((1 << kLg) >= 2 * kBlockMaxDeg, "table load <= 1/2");
+  static_assert((1 << kLg) >= 2 * kBlockWaves * kSegArcs, "table load <= 1/2");
   constexpr int kSlots = 1 << kLg;
   constexpr int kT = 64 * kBlockWaves;
   __shared__ u64 tab[kSlots];
@@ -1505,8 +1505,18 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   auto launch_block = [&](hipStream_t st) -> int {
     const int64_t nb = g->n_hub - g->hub_lane_begin;
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 6], st));
-    hipLaunchKernelGGL(k_lpa_block<13>, dim3(cap_grid(nb, 2048)), dim3(64 * kBlockWaves), 0, st, g->rp, g->al,
-                       Lown, g->hub_lane_begin, g->n_hub, g->flist, fcnt, fr_all, pmax);
+    // wide tier first (rows 4096 < deg <= 8192: 16 waves, a 16K-slot table, one block
+    // per CU), then rows <= 4096 (8 waves, 8K slots, two blocks per CU)
+    const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;
+    if (g->block2 && hl > h2) {
+      hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, 1024)),
+                         dim3(kBlockMaxDeg2 / kSegArcs * 64), 0, st, g->rp, g->al, Lown, h2, hl, g->flist, fcnt,
+                         fr_all, pmax);
+      LPA_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL((k_lpa_block<13, kBlockMaxDeg / kSegArcs>), dim3(cap_grid(nb, 2048)),
+                       dim3(kBlockMaxDeg / kSegArcs * 64), 0, st, g->rp, g->al, Lown, g->hub_lane_begin, g->n_hub,
+                       g->flist, fcnt, fr_all, pmax);
     LPA_HIP(hipGetLastError());
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 7], st));
     return LPA_OK;
@@ -1522,7 +1532,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_HIP(hipEventRecord(g->ev_join2[1], g->aux_stream[2]));
   }
   LPA_TRY(mark(0, s));
-  const int64_t n_units = blk ? g->unit_lane_begin : g->n_segs;
+  const int64_t n_units = blk ? (g->block2 ? g->unit_block2_begin : g->unit_lane_begin) : g->n_segs;
   if (n_units > 0) {
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
                        g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all, pmax);
