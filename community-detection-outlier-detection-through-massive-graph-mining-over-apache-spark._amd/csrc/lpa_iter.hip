@@ -222,7 +222,7 @@ struct Batch {
 
 template <int NC>
 __device__ __forceinline__ void peel_batch(Batch<NC>& bt, const u32 (&lab)[NC], int nch, int lane,
-                                           int pmax = kPeelMax) {
+                                           int pmax = kPeelMax, bool whole_row = false) {
   u32 mask = 0u;
 #pragma unroll
   for (int u = 0; u < NC; ++u)
@@ -251,6 +251,12 @@ __device__ __forceinline__ void peel_batch(Batch<NC>& bt, const u32 (&lab)[NC], 
     if (lane == p) bt.pword = word;
     bt.pbest = umax64(bt.pbest, word);
     bt.npeel = p + 1;
+    // whole_row (the batch is the entire row): decided once the best count exceeds
+    // the untallied votes -- the rest is dropped, no LDS hash
+    if (whole_row && (u32)(bt.pbest >> 32) > wave_sum_u32((u32)__popc(mask))) {
+      mask = 0u;
+      break;
+    }
     if (c < 2) break;
   }
   bt.mask = mask;
@@ -391,6 +397,17 @@ __device__ __forceinline__ u64 group_mode_sort(u32 v, int lane) {
 // peel rounds after which a chunk whose groups are still unresolved is sorted instead
 constexpr int kPeelSortAfter = 3;
 
+// lanes of the groups already decided after a peel round: a group whose best count
+// so far exceeds its untallied votes cannot change its mode (no remaining label can
+// reach, or tie, that count), so its lanes retire without further rounds -- a
+// converged row (one dominant label plus a few strays) stops after one round instead
+// of peeling the strays one by one and then sorting
+template <int G>
+__device__ __forceinline__ u64 decided_groups(u64 act, u64 my, u64 best, int gbase, u64 gm) {
+  const u32 rem = (u32)__popcll((act >> gbase) & gm);
+  return __ballot(my != 0ull && (u32)(best >> 32) > rem);
+}
+
 // G lanes per row (G <= 64, all 64 lanes of the wave call it: ballot peel)
 template <int G>
 __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
@@ -425,6 +442,7 @@ __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const 
       const u32 c = (u32)__popcll((mm >> gbase) & gm);
       if (my) best = umax64(best, tally(c, x));
       act &= ~mm;
+      act &= ~decided_groups<G>(act, my, best, gbase, gm);
     }
     if (live && j == 0) Ln[v] = (int32_t)(~(u32)best);
   }
@@ -499,9 +517,10 @@ __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r
   lg = lg < 6 ? 6 : lg;
   const int nch = (d + 63) >> 6;
   Batch<NC> bt;
-  peel_batch<NC>(bt, lab, nch, lane, pmax);
+  peel_batch<NC>(bt, lab, nch, lane, pmax, true);
   if (!bt.any) {
-    // every vote is in a peel group: the mode is their maximum, no LDS needed
+    // every vote is in a peel group (or the rest cannot win): the mode is their
+    // maximum, no LDS needed
     if (lane == 0) Ln[v] = (int32_t)(~(u32)bt.pbest);
   } else {
     int cnt = 0;
@@ -757,6 +776,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
         const u32 cn = (u32)__popcll((mm >> gbase) & gm);
         if (my) best = umax64(best, tally(cn, x));
         act &= ~mm;
+        act &= ~decided_groups<G>(act, my, best, gbase, gm);
       }
       const int64_t row = r0 + c * (64 / G) + lane / G;
       if ((lane & (G - 1)) == 0 && row < vend && best) Ln[row] = (int32_t)(~(u32)best);
