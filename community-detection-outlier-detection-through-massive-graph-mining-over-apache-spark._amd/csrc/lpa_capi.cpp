@@ -70,7 +70,7 @@ void destroy(lpa_graph* g) {
   for (auto& st : g->aux_stream)
     if (st) (void)hipStreamDestroy(st);
   for (hipEvent_t e : {g->ev_fork, g->ev_join[0], g->ev_join[1], g->ev_fork2, g->ev_join2[0],
-                       g->ev_join2[1]})
+                       g->ev_join2[1], g->ev_join2[2]})
     if (e) (void)hipEventDestroy(e);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   if (g->own_stream) (void)hipStreamDestroy(g->own_stream);
@@ -144,7 +144,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_HUB_FUSE")) g->hub_fuse = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FOLD_REBUILD")) g->fold_rebuild = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_BLOCK")) g->block_rows = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_BLOCK_AT")) g->block_at = atoi(f) < 0 ? 0 : (atoi(f) > 2 ? 2 : atoi(f));
+  if (const char* f = getenv("LPA_BLOCK_STEPS")) g->block_steps = atoi(f) < 0 ? 0 : (atoi(f) > 8 ? 8 : atoi(f));
+  if (const char* f = getenv("LPA_BLOCK_AT")) g->block_at = atoi(f) < 0 ? 0 : (atoi(f) > 4 ? 4 : atoi(f));
   // internal builds (the outlier stage's L2 sub-graph): the locality order is a
   // gather-locality heuristic worth its two atomic passes only on a graph that runs
   // many supersteps; labels do not depend on the vertex order
@@ -167,7 +168,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
     for (auto& st : g->aux_stream)
       if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     for (hipEvent_t* ev : {&g->ev_fork, &g->ev_join[0], &g->ev_join[1], &g->ev_fork2, &g->ev_join2[0],
-                           &g->ev_join2[1]})
+                           &g->ev_join2[1], &g->ev_join2[2]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       set_error("stream/event creation: %s", hipGetErrorString(e));

@@ -1114,7 +1114,7 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   return LPA_OK;
 }
 
-int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
+int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join) {
   const int64_t n = g->n_hub;
   if (n == 0) return LPA_OK;
   hipStream_t s = g->stream;
@@ -1131,7 +1131,13 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   // stream.  Otherwise everything runs in order on the main stream.
   // (the fourth stream runs k_lpa_block when block_at == 2: the bucket path then
   // follows the row bins on the third)
-  hipStream_t sd = !fork ? s : (block_mode_now(g) && g->block_at == 2) ? g->aux_stream[1] : g->aux_stream[2];
+  // (block_at == 3: the fourth stream runs the wide block tier, the third the narrow
+  // one after the row bins: the bucket path follows the wave bins on the second)
+  const bool bm = block_mode_now(g) && !g->serial;
+  hipStream_t sd = !fork                         ? s
+                   : (bm && g->block_at == 2) ? g->aux_stream[1]
+                   : (bm && g->block_at >= 3) ? g->aux_stream[0]
+                                              : g->aux_stream[2];
   const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
   // fused (converged supersteps, few bucketed rows): the scan by the last block of
   // k_hub_count, the final pass by the last block of k_hub_bucket -- 5 dependent
@@ -1193,7 +1199,8 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
                        g->flist, g->fcnt + 16 * g->par, g->fr_all + g->par);
     LPA_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, fork ? (int64_t)0 : hl, n, g->rp,
+  // direct rows [0, nd) when not forked: in block mode only those above the block tiers
+  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, fork ? (int64_t)0 : hc, n, g->rp,
                      g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, lists, lcnt, g->items_cb,
                      g->items_cc, g->flist, g->fcnt + 16 * g->par, g->fr_all + g->par);
   LPA_HIP(hipGetLastError());
@@ -1225,7 +1232,7 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork) {
   if (!fork) LPA_TRY(bucket_path());
   if (fork) {
     LPA_HIP(hipEventRecord(g->ev_join2[0], sd));
-    LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[0], 0));
+    if (join) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[0], 0));
   }
   return LPA_OK;
 }

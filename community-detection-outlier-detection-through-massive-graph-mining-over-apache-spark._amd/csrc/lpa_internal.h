@@ -96,7 +96,7 @@ struct lpa_graph {
   // bucket path (2); 4 streams = the 4 hardware queues of a process
   hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
-  hipEvent_t ev_fork2 = nullptr, ev_join2[2] = {nullptr, nullptr};  // hub combine tail (join2[0] used)
+  hipEvent_t ev_fork2 = nullptr, ev_join2[3] = {nullptr, nullptr, nullptr};  // hub combine tail, block tiers
   int32_t rank = 0, nranks = 1;
   // label-exchange collective backend (P > 1): RCCL communicator (one process per
   // GPU) or the in-process loopback group (P handles on one device, one host thread
@@ -161,8 +161,13 @@ struct lpa_graph {
   int block2 = 1;                 // LPA_BLOCK2=0: label-dense supersteps stage the rows of 4096 < deg <= 8192 by units
   int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches
   int fold_rebuild = 1;           // LPA_FOLD_REBUILD=0: captured converged supersteps keep the rebuild launch
-  int block_at = 0;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the
-                                  // main stream, or (2) on the fourth stream, concurrent with them
+  int block_steps = 2;            // LPA_BLOCK_STEPS: supersteps after L0 in block mode (k_lpa_block rows)
+  int block_at = 4;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the
+                                  // main stream, or (2) on the fourth stream, concurrent with them,
+                                  // or (3) split: the wide tier on the fourth stream, the 8-wave
+                                  // tier after the row bins, the bucket path after the wave bins, or (4) as 3
+                                  // with the narrow tier on the main stream after the hub mid tiers
+                                  // (4: C3 293.8-295.4 -> 299.3-303.1 GTEPS over 0, same-box A/B)
   int64_t unit_lane_begin = 0;    // hub_uoff[hub_lane_begin]
   int64_t unit_block2_begin = 0;  // hub_uoff[hub_block2_begin]
   bool force_all_next = false;    // the next superstep tallies every row (after block mode)
@@ -267,7 +272,9 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
                 uint32_t flags);
 int init_labels(lpa_graph* g);
 int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
-int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork);  // lpa_hub.hip
+// join = false: the forked bucket path's end is recorded in ev_join2[0] and the caller
+// joins it (main-stream work can be queued behind the mid tiers first)
+int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join = true);  // lpa_hub.hip
 bool block_mode_now(const lpa_graph* g);  // lpa_iter.hip
 int64_t block_rows_begin(const lpa_graph* g);  // first row of the block tiers (lpa_iter.hip)
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]

@@ -82,7 +82,7 @@ constexpr int kDenseSupersteps = 2;
 // and skip their units; the superstep after them tallies every row (their units'
 // staged words are stale)
 bool block_mode_now(const lpa_graph* g) {
-  return g->block_rows && g->since_reset < kDenseSupersteps && g->hub_lane_begin < g->n_hub;
+  return g->block_rows && g->since_reset < g->block_steps && g->hub_lane_begin < g->n_hub;
 }
 int64_t block_rows_begin(const lpa_graph* g) { return g->block2 ? g->hub_block2_begin : g->hub_lane_begin; }
 
@@ -1223,6 +1223,54 @@ struct FrontierMarks {
 };
 static_assert(kSegArcs == 512, "unit of a position: (p - rp[row]) >> 9");
 
+// Wave-cooperative scatter of every lane's run: al[cpos[b + i]] = lab, i < n
+// (n <= kChunkPos).  The runs are cut into 16-position pieces dealt over the wave's
+// lanes (lane -> piece by a binary search over the inclusive piece prefix), so a
+// wave whose lanes hold runs of 17..256 positions writes them in parallel instead of
+// run after run with the whole wave.  Every lane of the wave must call it.
+__device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, const uint32_t* __restrict__ cpos,
+                                             int32_t* __restrict__ al, bool all, const FrontierMarks& fm,
+                                             int lane) {
+  const int k = (n + 15) >> 4;
+  int incl = k;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  const int S = __shfl(incl, 63, 64);
+  for (int r0 = 0; r0 < S; r0 += 64) {
+    const int t = r0 + lane;
+    int o = 0;  // the owner: first lane whose inclusive piece count exceeds t
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1) {
+      const int ic = __shfl(incl, o + st - 1, 64);
+      if (ic <= t) o += st;
+    }
+    o = o < 64 ? o : 63;
+    const int excl = __shfl(incl, o, 64) - __shfl(k, o, 64);
+    const int64_t bo = __shfl(b, o, 64);
+    const int no = __shfl(n, o, 64);
+    const int32_t lv = __shfl(lab, o, 64);
+    if (t < S) {
+      const int p0 = (t - excl) * 16;
+      const int cnt = min(16, no - p0);
+      const uint32_t* src = cpos + bo + p0;
+      for (int q = 0; q < cnt; q += 4) {
+        uint32_t p[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = q + u < cnt ? src[q + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (q + u < cnt) {
+            al[p[u]] = lv;
+            if (!all) fm.mark(p[u]);
+          }
+      }
+    }
+  }
+}
+
 // al[i] = L[col[i]] over the whole arc array by the calling grid (grid-stride): each
 // thread keeps 8 gathers in flight (two int4 column quads), col / al streamed
 // non-temporally
@@ -1299,38 +1347,16 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
         lab = Ln[u];
         Lold[u] = lab;  // frontier sync (after the join)
       }
-      const int ns = n <= 16 ? n : 0;
-      for (int k = 0; k < ns; k += 4) {
-        uint32_t p[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) p[t] = k + t < ns ? cpos[b + k + t] : 0u;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (k + t < ns) {
-            al[p[t]] = lab;
-            if (!all) fm.mark(p[t]);
-          }
-      }
-      u64 big = __ballot(n > 16);
-      while (big) {
-        const int bl = __ffsll((unsigned long long)big) - 1;
-        big &= big - 1ull;
-        const int64_t bb = __shfl(b, bl, 64);
-        const int bn = __shfl(n, bl, 64);
-        const int32_t bv = __shfl(lab, bl, 64);
-        for (int i = lane; i < bn; i += 64) {
-          const uint32_t pp = cpos[bb + i];
-          al[pp] = bv;
-          if (!all) fm.mark(pp);
-        }
-      }
+      scatter_runs(b, n, lab, cpos, al, all, fm, lane);
     }
   }
   uint4* __restrict__ flw = const_cast<uint4*>(chflag16);
   // multi-chunk columns: a wave takes 64 groups of 16 chunk flags, one group per lane,
-  // and clears them
-  for (int64_t g0 = wid * 64; g0 < ngroups; g0 += nw * 64) {
-    const int64_t gi = g0 + lane;
+  // and clears them.  Lane l of wave w takes group g0 + l * nw + w: the consecutive
+  // chunks of one changed hub column land in different waves (wave-consecutive
+  // groups would hand a column's hundreds of chunks to one wave, one after another)
+  for (int64_t g0 = 0; g0 < ngroups; g0 += nw * 64) {
+    const int64_t gi = g0 + (int64_t)lane * nw + wid;
     uint4 f = make_uint4(0u, 0u, 0u, 0u);
     if (gi < ngroups) f = chflag16[gi];
     const bool any = (f.x | f.y | f.z | f.w) != 0u;
@@ -1360,31 +1386,7 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
         // (after the join; every changed vertex with local arcs has a chunk 0)
         if (kk == 0) Lold[u] = lab;
       }
-      const int ns = n <= 16 ? n : 0;
-      for (int k = 0; k < ns; k += 4) {
-        uint32_t p[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) p[t] = k + t < ns ? cpos[b + k + t] : 0u;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (k + t < ns) {
-            al[p[t]] = lab;
-            if (!all) fm.mark(p[t]);
-          }
-      }
-      u64 big = __ballot(n > 16);
-      while (big) {
-        const int bl = __ffsll((unsigned long long)big) - 1;
-        big &= big - 1ull;
-        const int64_t bb = __shfl(b, bl, 64);
-        const int bn = __shfl(n, bl, 64);
-        const int32_t bv = __shfl(lab, bl, 64);
-        for (int i = lane; i < bn; i += 64) {
-          const uint32_t pp = cpos[bb + i];
-          al[pp] = bv;
-          if (!all) fm.mark(pp);
-        }
-      }
+      scatter_runs(b, n, lab, cpos, al, all, fm, lane);
     }
   }
 }
@@ -1522,11 +1524,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   const int pmax = g->since_reset < kDenseSupersteps ? g->dense_peel : kPeelMax;
   // peel rounds of the row bins before a chunk is sorted (LPA_DENSE_SORT_AFTER)
   const int sort_after = g->since_reset < kDenseSupersteps ? g->dense_sort_after : kPeelSortAfter;
-  auto launch_block = [&](hipStream_t st) -> int {
-    const int64_t nb = g->n_hub - g->hub_lane_begin;
-    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 6], st));
-    // wide tier first (rows 4096 < deg <= 8192: 16 waves, a 16K-slot table, one block
-    // per CU), then rows <= 4096 (8 waves, 8K slots, two blocks per CU)
+  // wide tier (rows 4096 < deg <= 8192: 16 waves, a 16K-slot table, one block per CU)
+  auto launch_block_wide = [&](hipStream_t st) -> int {
     const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;
     if (g->block2 && hl > h2) {
       hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, 1024)),
@@ -1534,13 +1533,33 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
                          fr_all, pmax);
       LPA_HIP(hipGetLastError());
     }
+    return LPA_OK;
+  };
+  // rows <= 4096 (8 waves, 8K slots, two blocks per CU)
+  auto launch_block_narrow = [&](hipStream_t st) -> int {
+    const int64_t nb = g->n_hub - g->hub_lane_begin;
     hipLaunchKernelGGL((k_lpa_block<13, kBlockMaxDeg / kSegArcs>), dim3(cap_grid(nb, 2048)),
                        dim3(kBlockMaxDeg / kSegArcs * 64), 0, st, g->rp, g->al, Lown, g->hub_lane_begin, g->n_hub,
                        g->flist, fcnt, fr_all, pmax);
     LPA_HIP(hipGetLastError());
+    return LPA_OK;
+  };
+  auto launch_block = [&](hipStream_t st) -> int {
+    if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 6], st));
+    LPA_TRY(launch_block_wide(st));
+    LPA_TRY(launch_block_narrow(st));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 7], st));
     return LPA_OK;
   };
+  // block_at 3 (split): the longest pole of a label-dense superstep is the main
+  // stream's block tiers + units + hub combine; the wide tier goes to the fourth
+  // stream, the narrow tier after the row bins (launched below)
+  const bool split = blk && g->block_at >= 3 && !g->serial;
+  if (split) {
+    LPA_HIP(hipStreamWaitEvent(g->aux_stream[2], g->ev_fork, 0));
+    LPA_TRY(launch_block_wide(g->aux_stream[2]));
+    LPA_HIP(hipEventRecord(g->ev_join2[1], g->aux_stream[2]));
+  }
   // serialized profiling: the block kernel bracketed on its own (stats kernel 16),
   // ahead of the seg units' marks
   if (blk && (g->block_at == 0 || g->serial)) LPA_TRY(launch_block(s));
@@ -1609,16 +1628,26 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_GROUP_LAUNCH(BIN_G4, 4)
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
+  if (split && g->block_at == 3) {
+    LPA_TRY(launch_block_narrow(sc));
+    LPA_HIP(hipEventRecord(g->ev_join2[2], sc));
+  }
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
   // hub combine after the bins are queued: its tail kernels on the aux streams
   // run after those streams' bins
   LPA_TRY(mark(2, s));
-  LPA_TRY(launch_hub_combine(g, Lown, !g->serial && g->since_reset < kDenseSupersteps));
+  const bool hub_fork = !g->serial && g->since_reset < kDenseSupersteps;
+  LPA_TRY(launch_hub_combine(g, Lown, hub_fork, !(split && g->block_at == 4)));
+  if (split && g->block_at == 4) {
+    LPA_TRY(launch_block_narrow(s));
+    if (hub_fork) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[0], 0));
+  }
   LPA_TRACE_POINT("hub_combine");
   // the block rows' labels are seg-bin slots: joined before the main stream's diff
-  if (blk && g->block_at == 2 && !g->serial) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[1], 0));
+  if (blk && g->block_at >= 2 && !g->serial) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[1], 0));
+  if (split && g->block_at == 3) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[2], 0));
   LPA_TRY(mark(3, s));
   if (diff) {
     // inside the concurrent tally: no Lc sync here, the scatter refresh does it
@@ -1794,7 +1823,10 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // superstep (tally on four streams + diff + refresh; ~25 kernels and the
     // fork/join events): one launch instead of ~40 queue operations.  The graph bakes
     // the label / counter buffers, so there is one per (cur, par) state.
-    if (g->use_graphs && g->nranks == 1 && !g->serial && g->since_reset >= kDenseSupersteps) {
+    // supersteps before `eager` are launched stream-ordered (their schedule differs
+    // from the converged one a captured graph bakes)
+    const int eager = kDenseSupersteps > g->block_steps ? kDenseSupersteps : g->block_steps;
+    if (g->use_graphs && g->nranks == 1 && !g->serial && g->since_reset >= eager) {
       const int key = g->cur * 2 + g->par;
       if (!g->gexec[key])
         LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
@@ -1810,7 +1842,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       continue;
     }
     if (g->use_graphs && g->nranks > 1 && g->loop == nullptr && !g->serial &&
-        g->since_reset >= kDenseSupersteps) {
+        g->since_reset >= eager) {
       // P > 1: the tally (no collective inside) replays a captured graph per
       // (cur, par); the exchange, whose delta size the host reads, and the refresh
       // follow on the stream.  Not for a loopback group: its ranks are threads of one
@@ -1841,7 +1873,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // after the last block-mode superstep the next one tallies every row and unit:
     // the block rows' units staged nothing while k_lpa_block tallied them (set at the
     // next superstep's start, after any caller-driven refresh has written fr_all)
-    if (block_mode_now(g) && g->since_reset + 1 == kDenseSupersteps) g->force_all_next = true;
+    if (block_mode_now(g) && g->since_reset + 1 == g->block_steps) g->force_all_next = true;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     g->cur ^= 1;
     g->par ^= 1;

@@ -173,11 +173,16 @@ def test_c2_sbm_full_size(gfa, oracle):
     assert nmi(truth, lab) > 0.9
 
 
-def test_schedules_identical(gfa):
+@pytest.mark.parametrize("graph", ["rmat17", "mix"])
+def test_schedules_identical(gfa, graph):
     """The concurrent four-stream schedule (forked hub combine in the label-dense
-    supersteps) and the serialized profiling schedule give identical labels."""
-    s, d = gfa.gen_rmat(17, 16, seed=3)
-    V = 1 << 17
+    supersteps) and the serialized profiling schedule give identical labels (the
+    degree mix has rows in both block tiers and a bucketed hub)."""
+    if graph == "rmat17":
+        s, d = gfa.gen_rmat(17, 16, seed=3)
+        V = 1 << 17
+    else:
+        V, s, d = degree_mix(0)
     with gfa.Graph(s, d, V) as g:
         conc = [g.labels() for _ in range(6) if g.step(1) is not None or True]
         g.reset()
@@ -185,6 +190,27 @@ def test_schedules_identical(gfa):
         ser = [g.labels() for _ in range(6) if g.step(1) is not None or True]
     for t in range(6):
         assert np.array_equal(conc[t], ser[t]), f"superstep {t + 1}"
+
+
+@pytest.mark.parametrize("env", [{"LPA_BLOCK_STEPS": "3"}, {"LPA_BLOCK_STEPS": "0"}, {"LPA_BLOCK_AT": "3"},
+                                 {"LPA_BLOCK_AT": "4"}, {"LPA_SERIAL": "1"}])
+def test_schedule_options_bit_exact(gfa, oracle, monkeypatch, env):
+    """Schedule options read at graph creation (block-mode superstep count, where the
+    block tiers run, the serialized profiling schedule): labels bit-exact per
+    superstep on the degree mix (both block tiers + a bucketed hub) and R-MAT-16."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    V, s, d = degree_mix(1)
+    _, hist, _ = oracle.lpa(V, s, d, 6, per_iter=True)
+    got = _per_step(gfa, V, s, d, 6)
+    for t in range(6):
+        assert np.array_equal(got[t], hist[t]), f"mix {env} superstep {t + 1}"
+    rs, rd = gfa.gen_rmat(16, 16, seed=5)
+    sn, dn = rs.cpu().numpy(), rd.cpu().numpy()
+    _, hist, _ = oracle.lpa(1 << 16, sn, dn, 6, per_iter=True)
+    got = _per_step(gfa, 1 << 16, rs, rd, 6)
+    for t in range(6):
+        assert np.array_equal(got[t], hist[t]), f"rmat16 {env} superstep {t + 1}"
 
 
 def test_chunglu_generator_matches_oracle(gfa, oracle):
