@@ -88,6 +88,27 @@ __global__ __launch_bounds__(1024) void k_hot_nt(const int32_t* __restrict__ col
     for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
   }
 }
+// cold list: al[cpos[j]] = L[ccol[j]] for the listed arcs (position-ordered or
+// column-ordered lists)
+__global__ __launch_bounds__(256) void k_cold_list(const uint32_t* __restrict__ cpos, const int32_t* __restrict__ ccol,
+                                                   int64_t n, const int32_t* __restrict__ L, int32_t* __restrict__ al) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    uint32_t p[4]; int32_t c[4], r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { p[k] = __builtin_nontemporal_load(cpos + i + k * stride); c[k] = __builtin_nontemporal_load(ccol + i + k * stride); }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = L[c[k]];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) al[p[k]] = r[k];
+  }
+  for (; i < n; i += stride) al[cpos[i]] = L[ccol[i]];
+}
+struct IsCold {
+  const int32_t* col; int32_t T;
+  __host__ __device__ bool operator()(const uint32_t& i) const { return col[i] >= T; }
+};
 // columns sorted inside each row (rows = degree runs, rank order)
 __global__ void k_row_bounds(const int64_t* cdeg, int64_t V, int64_t* rows_off) {}
 
@@ -173,6 +194,58 @@ int main(int argc, char** argv) {
     timeit(nm, [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, T); });
     snprintf(nm, 80, "split at %d: pass B (col >= T)", T);
     timeit(nm, [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, T, BIG); });
+  }
+  // hot pass + cold list: the cold arcs (col >= T) from static (position, column)
+  // lists instead of a second col stream
+  for (int32_t T : {1 << 20, 1 << 21, 1 << 22}) {
+    if (T >= V) continue;
+    uint32_t* idx; uint32_t* cp; int32_t* cc; int64_t* nsel;
+    CK(hipMalloc(&idx, arcs * 4)); CK(hipMalloc(&nsel, 8));
+    hipcub::CountingInputIterator<uint32_t> it(0u);
+    size_t need = 0;
+    IsCold pred{col, T};
+    hipcub::DeviceSelect::If(nullptr, need, it, idx, nsel, (int64_t)arcs, pred);
+    void* tmp; CK(hipMalloc(&tmp, need));
+    hipcub::DeviceSelect::If(tmp, need, it, idx, nsel, (int64_t)arcs, pred);
+    int64_t nc = 0; CK(hipMemcpy(&nc, nsel, 8, hipMemcpyDeviceToHost));
+    CK(hipMalloc(&cp, nc * 4)); CK(hipMalloc(&cc, nc * 4));
+    std::vector<uint32_t> hi(nc); CK(hipMemcpy(hi.data(), idx, nc * 4, hipMemcpyDeviceToHost));
+    std::vector<int32_t> hc(arcs); CK(hipMemcpy(hc.data(), col, arcs * 4, hipMemcpyDeviceToHost));
+    std::vector<int32_t> hcc(nc); for (int64_t j = 0; j < nc; ++j) hcc[j] = hc[hi[j]];
+    CK(hipMemcpy(cp, hi.data(), nc * 4, hipMemcpyHostToDevice)); CK(hipMemcpy(cc, hcc.data(), nc * 4, hipMemcpyHostToDevice));
+    char nm[96];
+    snprintf(nm, 96, "hot pass (col < %d) + cold list by position", T);
+    timeit(nm, [&] {
+      hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, T);
+      hipLaunchKernelGGL(k_cold_list, dim3(8192), dim3(256), 0, 0, cp, cc, nc, L, al);
+    });
+    snprintf(nm, 96, "  cold list alone (%ld arcs, by position)", (long)nc);
+    timeit(nm, [&] { hipLaunchKernelGGL(k_cold_list, dim3(8192), dim3(256), 0, 0, cp, cc, nc, L, al); });
+    fflush(stdout);
+    // column order (CSC of the cold arcs): sequential label reads, scattered writes
+    if (nc > 300000000) { CK(hipFree(idx)); CK(hipFree(nsel)); CK(hipFree(tmp)); CK(hipFree(cp)); CK(hipFree(cc)); continue; }
+    std::vector<int64_t> ord(nc); for (int64_t j = 0; j < nc; ++j) ord[j] = j;
+    std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return hcc[a] < hcc[b]; });
+    std::vector<uint32_t> p2(nc); std::vector<int32_t> c2(nc);
+    for (int64_t j = 0; j < nc; ++j) { p2[j] = hi[ord[j]]; c2[j] = hcc[ord[j]]; }
+    CK(hipMemcpy(cp, p2.data(), nc * 4, hipMemcpyHostToDevice)); CK(hipMemcpy(cc, c2.data(), nc * 4, hipMemcpyHostToDevice));
+    snprintf(nm, 96, "  cold list alone (by column)");
+    timeit(nm, [&] { hipLaunchKernelGGL(k_cold_list, dim3(8192), dim3(256), 0, 0, cp, cc, nc, L, al); });
+    CK(hipFree(idx)); CK(hipFree(nsel)); CK(hipFree(tmp)); CK(hipFree(cp)); CK(hipFree(cc));
+  }
+  // column windows: pass k gathers only the arcs whose column lies in
+  // [k W, (k + 1) W) (the window's labels stay cache-resident while col streams past)
+  for (int64_t W : {1ll << 22, 1ll << 23, 1ll << 24, 1ll << 25}) {
+    if (W >= V) continue;
+    char nm[80];
+    snprintf(nm, 80, "windows of %ld labels (%ld passes)", (long)W, (long)((V + W - 1) / W));
+    timeit(nm, [&] {
+      for (int64_t lo = 0; lo < V; lo += W) {
+        const int32_t hi = (int32_t)std::min<int64_t>(V, lo + W);
+        if (lo == 0) hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, hi);
+        else hipLaunchKernelGGL((k_hot<0, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, (int32_t)lo, hi);
+      }
+    });
   }
   return 0;
 }
