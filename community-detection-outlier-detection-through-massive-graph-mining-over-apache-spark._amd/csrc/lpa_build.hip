@@ -350,7 +350,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   // ---- 1. degrees ----
   int32_t* d_err = nullptr;
   int32_t* d_max = nullptr;
-  LPA_HIP(hipMalloc((void**)&d_err, 2 * sizeof(int32_t)));
+  LPA_TRY(scratch_alloc(g, (void**)&d_err, 2 * sizeof(int32_t)));
   d_max = d_err + 1;
   LPA_HIP(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), s));
   LPA_TRY(dev_alloc(g, (void**)&g->deg, sizeof(int32_t) * (V > 0 ? V : 1)));
@@ -367,7 +367,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   int32_t h_err[2] = {0, 0};
   LPA_HIP(hipMemcpyAsync(h_err, d_err, sizeof(h_err), hipMemcpyDeviceToHost, s));
   LPA_HIP(hipStreamSynchronize(s));
-  LPA_HIP(hipFree(d_err));
+  scratch_free(g, d_err);
   if (h_err[0]) {
     set_error("edge endpoint outside [0, V=%d)", V);
     return LPA_EINVAL;
@@ -380,7 +380,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   LPA_HIP(hipMemsetAsync(g->old_of, 0xFF, sizeof(int32_t) * g->vpad, s));
   if (V > 0) {
     u64* vk = nullptr;
-    LPA_HIP(hipMalloc((void**)&vk, sizeof(u64) * 2 * V));
+    LPA_TRY(scratch_alloc(g, (void**)&vk, sizeof(u64) * 2 * V));
     hipLaunchKernelGGL(k_vertex_keys, dim3(grid_for(V)), dim3(256), 0, s, g->deg, (int64_t)V,
                        g->max_degree, vk);
     LPA_HIP(hipGetLastError());
@@ -392,7 +392,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     if (g->locality > 0 && m > 0 && V < (1 << 28)) {
       const int K = g->locality < 4 ? g->locality : 4;  // neighbour keys (LPA_LOCALITY)
       int32_t* rank_of = nullptr;
-      LPA_HIP(hipMalloc((void**)&rank_of, sizeof(int32_t) * (1 + K) * (size_t)V));
+      LPA_TRY(scratch_alloc(g, (void**)&rank_of, sizeof(int32_t) * (1 + K) * (size_t)V));
       int32_t* nk[4] = {rank_of + V, rank_of + 2 * V, rank_of + 3 * V, rank_of + 4 * V};
       hipLaunchKernelGGL(k_rank_of, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, rank_of);
       LPA_HIP(hipMemsetAsync(nk[0], 0x7F, sizeof(int32_t) * K * (size_t)V, s));
@@ -407,17 +407,17 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
         LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
       }
       LPA_HIP(hipGetLastError());
-      LPA_HIP(hipFree(rank_of));
+      scratch_free(g, rank_of);
     }
     hipLaunchKernelGGL(k_vertex_order, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, P, S,
                        g->new_of, g->old_of);
     LPA_HIP(hipGetLastError());
-    LPA_HIP(hipFree(vk));
+    scratch_free(g, vk);
   }
 
   // ---- owned degrees, row_ptr ----
   int32_t* deg_own = nullptr;
-  LPA_HIP(hipMalloc((void**)&deg_own, sizeof(int32_t) * S));
+  LPA_TRY(scratch_alloc(g, (void**)&deg_own, sizeof(int32_t) * S));
   hipLaunchKernelGGL(k_owned_degree, dim3(grid_for(S)), dim3(256), 0, s, g->old_of + g->own_begin,
                      g->deg, S, deg_own);
   LPA_HIP(hipGetLastError());
@@ -432,7 +432,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
   if (arcs > 0) {
     u64* keys = nullptr;
-    if (hipMalloc((void**)&keys, sizeof(u64) * 2 * arcs) != hipSuccess) {
+    if (scratch_alloc(g, (void**)&keys, sizeof(u64) * 2 * arcs) != LPA_OK) {
       set_error("out of device memory for %lld arc keys", (long long)(2 * arcs));
       return LPA_ENOMEM;
     }
@@ -441,11 +441,11 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
                          g->e_dst, m, g->new_of, keys);
     } else {
       unsigned long long* cursor = nullptr;
-      LPA_HIP(hipMalloc((void**)&cursor, sizeof(unsigned long long)));
+      LPA_TRY(scratch_alloc(g, (void**)&cursor, sizeof(unsigned long long)));
       LPA_HIP(hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
       hipLaunchKernelGGL(k_emit_arcs_owned, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
                          g->e_dst, m, g->new_of, g->own_begin, g->own_begin + S, keys, cursor);
-      LPA_HIP(hipFree(cursor));
+      scratch_free(g, cursor);
     }
     LPA_HIP(hipGetLastError());
     int shifts[16], ns = 0;
@@ -462,7 +462,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
       return LPA_EINVAL;
     }
     int32_t* colcnt = nullptr;
-    LPA_HIP(hipMalloc((void**)&colcnt, sizeof(int32_t) * g->vpad));
+    LPA_TRY(scratch_alloc(g, (void**)&colcnt, sizeof(int32_t) * g->vpad));
     if (P == 1) {
       // one rank: column u occurs once per arc of u, i.e. deg_own[u] times
       LPA_HIP(hipMemcpyAsync(colcnt, deg_own, sizeof(int32_t) * g->vpad, hipMemcpyDeviceToDevice, s));
@@ -492,7 +492,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
       // multi-chunk columns are the high-degree ones, i.e. the first slots at P = 1:
       // the scatter scans the chunk flags only up to the last such column's chunks
       unsigned long long* d_end = nullptr;
-      LPA_HIP(hipMalloc((void**)&d_end, sizeof(unsigned long long)));
+      LPA_TRY(scratch_alloc(g, (void**)&d_end, sizeof(unsigned long long)));
       LPA_HIP(hipMemsetAsync(d_end, 0, sizeof(unsigned long long), s));
       hipLaunchKernelGGL(k_chunk_owner, dim3(grid_for(g->vpad)), dim3(256), 0, s, g->cch, g->vpad,
                          g->cowner, d_end);
@@ -500,11 +500,11 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
       unsigned long long h_end = 0;
       LPA_HIP(hipMemcpyAsync(&h_end, d_end, sizeof(h_end), hipMemcpyDeviceToHost, s));
       LPA_HIP(hipStreamSynchronize(s));
-      LPA_HIP(hipFree(d_end));
+      scratch_free(g, d_end);
       g->n_chunk_scan = (int64_t)h_end;
     }
-    LPA_HIP(hipFree(colcnt));
-    LPA_HIP(hipFree(keys));
+    scratch_free(g, colcnt);
+    scratch_free(g, keys);
   } else {
     LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
     LPA_HIP(hipMemsetAsync(g->cptr, 0, sizeof(int64_t) * (g->vpad + 1), s));
@@ -533,16 +533,16 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     thr_h[LPA_NBINS - 1] = kWideMaxDeg;
     int32_t* d_thr = nullptr;
     int64_t* d_bb = nullptr;
-    LPA_HIP(hipMalloc((void**)&d_thr, sizeof(thr_h)));
-    LPA_HIP(hipMalloc((void**)&d_bb, sizeof(int64_t) * LPA_NBINS));
+    LPA_TRY(scratch_alloc(g, (void**)&d_thr, sizeof(thr_h)));
+    LPA_TRY(scratch_alloc(g, (void**)&d_bb, sizeof(int64_t) * LPA_NBINS));
     LPA_HIP(hipMemcpyAsync(d_thr, thr_h, sizeof(thr_h), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_bin_bounds, dim3(1), dim3(64), 0, s, deg_own, S, d_thr, LPA_NBINS, d_bb);
     LPA_HIP(hipGetLastError());
     int64_t bb[LPA_NBINS];
     LPA_HIP(hipMemcpyAsync(bb, d_bb, sizeof(bb), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
-    LPA_HIP(hipFree(d_thr));
-    LPA_HIP(hipFree(d_bb));
+    scratch_free(g, d_thr);
+    scratch_free(g, d_bb);
     g->bin_begin[0] = 0;
     for (int b = 1; b < LPA_NBINS; ++b) g->bin_begin[b] = bb[b - 1];
     g->bin_begin[LPA_NBINS] = S;
@@ -560,8 +560,8 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   if (n0 > 0) {
     int32_t* nseg = nullptr;
     int64_t* seg_off = nullptr;
-    LPA_HIP(hipMalloc((void**)&nseg, sizeof(int32_t) * n0));
-    LPA_HIP(hipMalloc((void**)&seg_off, sizeof(int64_t) * (n0 + 1)));
+    LPA_TRY(scratch_alloc(g, (void**)&nseg, sizeof(int32_t) * n0));
+    LPA_TRY(scratch_alloc(g, (void**)&seg_off, sizeof(int64_t) * (n0 + 1)));
     hipLaunchKernelGGL(k_seg_counts, dim3(grid_for(n0)), dim3(256), 0, s, deg_own, n0, nseg);
     LPA_HIP(hipGetLastError());
     LPA_TRY(exclusive_scan_i32_i64(nseg, seg_off, n0, s));
@@ -572,7 +572,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
                        n0, g->n_hub, g->segs);
     LPA_HIP(hipGetLastError());
     LPA_TRY(build_hub_tables(g, deg_own));
-    LPA_HIP(hipFree(nseg));
+    scratch_free(g, nseg);
     LPA_TRY(dev_alloc(g, (void**)&g->ucnt, sizeof(int32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
     g->hub_uoff = seg_off;  // the seg bin is exactly the hub rows (deg > kSegArcs)
     // first unit of the k_lpa_block rows
@@ -583,7 +583,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     LPA_HIP(hipStreamSynchronize(s));
     g->device_bytes += (int64_t)sizeof(int64_t) * (n0 + 1);
   }
-  LPA_HIP(hipFree(deg_own));
+  scratch_free(g, deg_own);
 
   LPA_TRY(dev_alloc(g, (void**)&g->dev_err, sizeof(int32_t)));
   LPA_HIP(hipMemsetAsync(g->dev_err, 0, sizeof(int32_t), s));

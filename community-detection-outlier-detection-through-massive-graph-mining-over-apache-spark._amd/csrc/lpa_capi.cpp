@@ -24,6 +24,11 @@ void set_error(const char* fmt, ...) {
 
 int dev_alloc(lpa_graph* g, void** p, size_t bytes) {
   if (bytes == 0) bytes = 1;
+  if (g->pooled) {
+    LPA_TRY(tmp_alloc(p, bytes, g->stream));
+    g->device_bytes += (int64_t)bytes;
+    return LPA_OK;
+  }
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) {
     *p = nullptr;
@@ -36,8 +41,27 @@ int dev_alloc(lpa_graph* g, void** p, size_t bytes) {
 }
 
 void dev_free(lpa_graph* g, void* p) {
-  (void)g;
-  if (p) (void)hipFree(p);
+  if (!p) return;
+  if (g->pooled) tmp_free(p, g->stream);
+  else (void)hipFree(p);
+}
+
+int scratch_alloc(lpa_graph* g, void** p, size_t bytes) {
+  if (g->pooled) return tmp_alloc(p, bytes > 0 ? bytes : 1, g->stream);
+  hipError_t e = hipMalloc(p, bytes > 0 ? bytes : 1);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    (void)hipGetLastError();
+    set_error("hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+    return LPA_ENOMEM;
+  }
+  return LPA_OK;
+}
+
+void scratch_free(lpa_graph* g, void* p) {
+  if (!p) return;
+  if (g->pooled) tmp_free(p, g->stream);
+  else (void)hipFree(p);
 }
 
 int gen_rmat(int32_t scale, int64_t m, uint64_t seed, int32_t do_scramble, int32_t* d_src,
@@ -150,6 +174,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   // gather-locality heuristic worth its two atomic passes only on a graph that runs
   // many supersteps; labels do not depend on the vertex order
   if (flags & kFlagNoLocality) g->locality = 0;
+  g->pooled = (flags & kFlagPooled) && stream != nullptr;
   g->rank = rank;
   g->nranks = nranks;
   if (stream) {

@@ -1056,9 +1056,9 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   LPA_HIP(hipMemcpyAsync(&hub_arcs, g->rp + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   int32_t *nb = nullptr, *nc = nullptr;
   int64_t* coff = nullptr;
-  LPA_HIP(hipMalloc((void**)&nb, sizeof(int32_t) * n));
-  LPA_HIP(hipMalloc((void**)&nc, sizeof(int32_t) * n));
-  LPA_HIP(hipMalloc((void**)&coff, sizeof(int64_t) * (n + 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&nb, sizeof(int32_t) * n));
+  LPA_TRY(scratch_alloc(g, (void**)&nc, sizeof(int32_t) * n));
+  LPA_TRY(scratch_alloc(g, (void**)&coff, sizeof(int64_t) * (n + 1)));
   hipLaunchKernelGGL(k_hub_bounds, dim3(grid_cap((n + 255) / 256, 65536)), dim3(256), 0, s, deg_own,
                      n, nb, nc);
   LPA_HIP(hipGetLastError());
@@ -1069,9 +1069,9 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   LPA_HIP(hipMemcpyAsync(&nbk, g->hub_hoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   LPA_HIP(hipMemcpyAsync(&nch, coff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   LPA_HIP(hipStreamSynchronize(s));
-  LPA_HIP(hipFree(nb));
-  LPA_HIP(hipFree(nc));
-  LPA_HIP(hipFree(coff));
+  scratch_free(g, nb);
+  scratch_free(g, nc);
+  scratch_free(g, coff);
   if (nbk > INT32_MAX || nch > INT32_MAX || hub_arcs > ((int64_t)1 << 40)) {
     set_error("hub combine tables too large (%lld buckets, %lld chunks)", (long long)nbk,
               (long long)nch);
@@ -1094,7 +1094,7 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   {
     // rows [hub_lane_begin, n_hub) have <= kLaneUnits units (degree-descending order)
     int64_t* d_pos = nullptr;
-    LPA_HIP(hipMalloc((void**)&d_pos, sizeof(int64_t)));
+    LPA_TRY(scratch_alloc(g, (void**)&d_pos, sizeof(int64_t)));
     hipLaunchKernelGGL(k_first_le, dim3(1), dim3(1), 0, s, deg_own, n, kLaneUnits * kSegArcs, d_pos);
     LPA_HIP(hipGetLastError());
     LPA_HIP(hipMemcpyAsync(&g->hub_lane_begin, d_pos, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -1104,7 +1104,7 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
     LPA_HIP(hipGetLastError());
     LPA_HIP(hipMemcpyAsync(&g->hub_block2_begin, d_pos, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
-    LPA_HIP(hipFree(d_pos));
+    scratch_free(g, d_pos);
   }
   LPA_TRY(dev_alloc(g, (void**)&g->items_cb, sizeof(u64) * nbk));
   LPA_TRY(dev_alloc(g, (void**)&g->items_cc, sizeof(u64) * nch));

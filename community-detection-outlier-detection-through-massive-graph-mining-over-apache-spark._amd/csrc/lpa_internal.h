@@ -40,6 +40,10 @@ constexpr int kTallyEv = 2 * kTallyKernels;        // events bracketing each tal
 constexpr int kBinEvents = kTallyEv + 8;
 static_assert(LPA_NKERNELS == kTallyKernels + 4, "stats: tally kernels + refresh, rebuild, lists, block");
 constexpr uint32_t kFlagNoLocality = 0x100u;  // internal create flag (not in lpa.h)
+// internal create flag: every device array of the handle comes from the stream-ordered
+// pool on the creator's stream (the outlier stage's per-call L2 sub-graph: its memory is
+// reused from call to call instead of hipMalloc / hipFree, which synchronise the device)
+constexpr uint32_t kFlagPooled = 0x200u;
 constexpr int kCombWords = 2048;      // expected staged words per combine bucket
 constexpr int kCombSlots = 8192;      // LDS table slots of a combine block
 constexpr int kCombDirect = 6144;     // <= this many staged words: one block, no buckets
@@ -242,6 +246,7 @@ struct lpa_graph {
   int64_t de_n = -1;                        // -1: not built yet
 
   int64_t device_bytes = 0;
+  bool pooled = false;                      // kFlagPooled: arrays from the stream-ordered pool
   hipEvent_t ev[2 * LPA_STATS_MAX_ITERS + 2] = {};
   hipEvent_t bin_ev[LPA_STATS_MAX_ITERS * lpa::kBinEvents] = {};
 };
@@ -256,6 +261,10 @@ int tmp_alloc(void** p, size_t bytes, hipStream_t s);
 void tmp_free(void* p, hipStream_t s);
 void tmp_trim(int device);
 void dev_free(lpa_graph* g, void* p);
+// build temporaries: like dev_alloc / dev_free without the accounting (both draw on the
+// stream-ordered pool for a pooled handle)
+int scratch_alloc(lpa_graph* g, void** p, size_t bytes);
+void scratch_free(lpa_graph* g, void* p);
 
 // primitives (lpa_prims.hip)
 // LSD radix sort of u64 keys in place (tmp: same length); sorts digits at the

@@ -409,7 +409,7 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     }
     // second LPA on the induced simple subgraph (same device, same stream)
     lpa_graph* h = nullptr;
-    LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE | kFlagNoLocality, &h));
+    LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE | kFlagNoLocality | kFlagPooled, &h));
     int rc = run_supersteps(h, sub_iter, nullptr);
     if (rc == LPA_OK) rc = gather_labels(h, sub);
     if (rc == LPA_OK && hipStreamSynchronize(s) != hipSuccess) rc = LPA_EHIP;
