@@ -91,11 +91,13 @@ void destroy(lpa_graph* g) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : g->bin_ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto& st : g->aux_stream)
-    if (st) (void)hipStreamDestroy(st);
-  for (hipEvent_t e : {g->ev_fork, g->ev_join[0], g->ev_join[1], g->ev_fork2, g->ev_join2[0],
-                       g->ev_join2[1], g->ev_join2[2]})
-    if (e) (void)hipEventDestroy(e);
+  if (!g->borrowed) {
+    for (auto& st : g->aux_stream)
+      if (st) (void)hipStreamDestroy(st);
+    for (hipEvent_t e : {g->ev_fork, g->ev_join[0], g->ev_join[1], g->ev_fork2, g->ev_join2[0],
+                         g->ev_join2[1], g->ev_join2[2]})
+      if (e) (void)hipEventDestroy(e);
+  }
   if (g->comm) (void)ncclCommDestroy(g->comm);
   if (g->own_stream) (void)hipStreamDestroy(g->own_stream);
   delete g;
@@ -134,7 +136,8 @@ static int check_edges(const int32_t* src, const int32_t* dst, int64_t m, int32_
 
 int create_common(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
                   int64_t m, int32_t V, uint32_t flags, int32_t rank, int32_t nranks,
-                  const uint8_t* comm_id, Loopback* loop, lpa_graph** out) {
+                  const uint8_t* comm_id, Loopback* loop, lpa_graph** out,
+                  const lpa_graph* borrow = nullptr) {
   if (!out) {
     set_error("out must be non-null");
     return LPA_EINVAL;
@@ -188,7 +191,18 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
     }
     g->stream = g->own_stream;
   }
-  {
+  if (borrow) {
+    // a handle used strictly in sequence with `borrow` on its stream (the outlier
+    // stage's L2 sub-graph): its aux streams and fork/join events are the parent's
+    // (creating and destroying three streams per call cost ~10 ms)
+    for (int i = 0; i < 3; ++i) g->aux_stream[i] = borrow->aux_stream[i];
+    g->ev_fork = borrow->ev_fork;
+    g->ev_join[0] = borrow->ev_join[0];
+    g->ev_join[1] = borrow->ev_join[1];
+    g->ev_fork2 = borrow->ev_fork2;
+    for (int i = 0; i < 3; ++i) g->ev_join2[i] = borrow->ev_join2[i];
+    g->borrowed = true;
+  } else {
     hipError_t e = hipSuccess;
     for (auto& st : g->aux_stream)
       if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
@@ -229,8 +243,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
 }
 
 int create_local(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
-                 int64_t m, int32_t V, uint32_t flags, lpa_graph** out) {
-  return create_common(device, stream, src, dst, m, V, flags, 0, 1, nullptr, nullptr, out);
+                 int64_t m, int32_t V, uint32_t flags, lpa_graph** out, const lpa_graph* borrow) {
+  return create_common(device, stream, src, dst, m, V, flags, 0, 1, nullptr, nullptr, out, borrow);
 }
 
 }  // namespace lpa

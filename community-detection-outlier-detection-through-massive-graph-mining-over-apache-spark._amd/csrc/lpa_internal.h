@@ -247,6 +247,7 @@ struct lpa_graph {
 
   int64_t device_bytes = 0;
   bool pooled = false;                      // kFlagPooled: arrays from the stream-ordered pool
+  bool borrowed = false;                    // aux streams / fork-join events belong to a parent handle
   hipEvent_t ev[2 * LPA_STATS_MAX_ITERS + 2] = {};
   hipEvent_t bin_ev[LPA_STATS_MAX_ITERS * lpa::kBinEvents] = {};
 };

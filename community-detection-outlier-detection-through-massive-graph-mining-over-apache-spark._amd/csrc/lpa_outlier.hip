@@ -21,7 +21,7 @@
 namespace lpa {
 
 int create_local(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
-                 int64_t m, int32_t V, uint32_t flags, lpa_graph** out);
+                 int64_t m, int32_t V, uint32_t flags, lpa_graph** out, const lpa_graph* borrow);
 void destroy(lpa_graph* g);
 
 namespace {
@@ -409,7 +409,8 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     }
     // second LPA on the induced simple subgraph (same device, same stream)
     lpa_graph* h = nullptr;
-    LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE | kFlagNoLocality | kFlagPooled, &h));
+    LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE | kFlagNoLocality | kFlagPooled, &h,
+                               g));
     int rc = run_supersteps(h, sub_iter, nullptr);
     if (rc == LPA_OK) rc = gather_labels(h, sub);
     if (rc == LPA_OK && hipStreamSynchronize(s) != hipSuccess) rc = LPA_EHIP;

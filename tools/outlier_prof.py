@@ -15,7 +15,9 @@ import torch  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "C3"
 src, dst, V = bench.make_edges(gfa, bench.CONFIGS[name], 0)
+t0 = time.perf_counter()
 g = gfa.Graph(src, dst, V)
+print(f"build {1e3 * (time.perf_counter() - t0):.1f} ms", flush=True)
 del src, dst
 torch.cuda.empty_cache()
 lab = g.run(10)
