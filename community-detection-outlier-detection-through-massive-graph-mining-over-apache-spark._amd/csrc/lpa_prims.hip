@@ -151,23 +151,47 @@ __global__ __launch_bounds__(kThreads) void k_rs_hist(const u64* __restrict__ ke
   hist[(int64_t)threadIdx.x * nblk + blockIdx.x] = cnt[threadIdx.x];
 }
 
+// Scatter of one pass: the tile's keys are first ranked stably into LDS in digit
+// order (the block's per-digit counts come from k_rs_hist), then written out in
+// LDS order, so consecutive lanes write consecutive addresses of one digit's run
+// (a direct per-key scatter spread every 256-key step over up to 256 runs).
 __global__ __launch_bounds__(kThreads) void k_rs_scatter(const u64* __restrict__ in,
                                                          u64* __restrict__ out, int64_t n,
                                                          int shift, const u32* __restrict__ offs,
-                                                         int64_t nblk) {
-  __shared__ u32 run[256];
+                                                         const u32* __restrict__ hist, int64_t nblk) {
+  __shared__ u64 sk[kTile];
+  __shared__ u32 lstart[256];  // local (in-tile) start of each digit's run
+  __shared__ u32 run[256];     // next local slot of each digit
+  __shared__ u32 gofs[256];    // the block's global start of each digit's run
+  __shared__ u32 wsum[kThreads / 64];
   __shared__ u32 wcnt[kThreads / 64][256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  run[tid] = offs[(int64_t)tid * nblk + blockIdx.x];
+  gofs[tid] = offs[(int64_t)tid * nblk + blockIdx.x];
+  // exclusive prefix of the block's digit counts: wave scans, then wave totals
+  const u32 c = hist[(int64_t)tid * nblk + blockIdx.x];
+  u32 incl = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const u32 o = (u32)__shfl_up((int)incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
 #pragma unroll
   for (int i = 0; i < kThreads / 64; ++i) wcnt[i][tid] = 0;
   __syncthreads();
+  u32 wbase = 0;
+  for (int ww = 0; ww < w; ++ww) wbase += wsum[ww];
+  lstart[tid] = wbase + incl - c;
+  run[tid] = wbase + incl - c;
+  __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int64_t nv64 = n - base;
+  const int nvalid = nv64 < kTile ? (int)nv64 : kTile;
   const u64 lt = (1ull << lane) - 1ull;
   for (int i = 0; i < kItems; ++i) {
-    const int64_t idx = base + (int64_t)i * kThreads + tid;
-    const bool ok = idx < n;
-    const u64 k = ok ? in[idx] : 0ull;
+    const int q = i * kThreads + tid;
+    const bool ok = q < nvalid;
+    const u64 k = ok ? in[base + q] : 0ull;
     const u32 dg = (u32)((k >> shift) & 255u);
     u64 peers = __ballot(ok);
 #pragma unroll
@@ -180,9 +204,9 @@ __global__ __launch_bounds__(kThreads) void k_rs_scatter(const u64* __restrict__
     if (ok && rank == 0) wcnt[w][dg] = (u32)__popcll(peers);
     __syncthreads();
     if (ok) {
-      u32 off = run[dg] + rank;
-      for (int ww = 0; ww < w; ++ww) off += wcnt[ww][dg];
-      out[off] = k;
+      u32 pos = run[dg] + rank;
+      for (int ww = 0; ww < w; ++ww) pos += wcnt[ww][dg];
+      sk[pos] = k;
     }
     __syncthreads();
     u32 tot = 0;
@@ -193,6 +217,14 @@ __global__ __launch_bounds__(kThreads) void k_rs_scatter(const u64* __restrict__
     }
     run[tid] += tot;
     __syncthreads();
+  }
+  for (int i = 0; i < kItems; ++i) {
+    const int q = i * kThreads + tid;
+    if (q < nvalid) {
+      const u64 k = sk[q];
+      const u32 dg = (u32)((k >> shift) & 255u);
+      out[gofs[dg] + (u32)q - lstart[dg]] = k;
+    }
   }
 }
 
@@ -266,7 +298,7 @@ int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshift
     rc = scan_impl<u32, u32>(hist, offs, nh, s);
     if (rc != LPA_OK) break;
     hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nblk), dim3(kThreads), 0, s, a, b, n,
-                       shifts[p], offs, nblk);
+                       shifts[p], offs, hist, nblk);
     LPA_HIP(hipGetLastError());
     u64* t = a;
     a = b;
