@@ -36,7 +36,8 @@ __global__ __launch_bounds__(256) void k_degree(const int32_t* __restrict__ src,
                                                 int32_t* __restrict__ deg, int32_t* err) {
   __shared__ u32 bk[kBhSlots];
   __shared__ int32_t bv[kBhSlots];
-  BlockHist<int32_t> bh{bk, bv};
+  __shared__ int bsat;
+  BlockHist<int32_t> bh{bk, bv, &bsat};
   bh.init();
   const int lane = threadIdx.x & 63;
   for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x; e0 < m; e0 += (int64_t)gridDim.x * blockDim.x) {
@@ -213,7 +214,8 @@ __global__ __launch_bounds__(256) void k_csc_keys(const int32_t* __restrict__ co
   }
   __shared__ u32 bk[kBhSlots];
   __shared__ int32_t bv[kBhSlots];
-  BlockHist<int32_t> bh{bk, bv};
+  __shared__ int bsat;
+  BlockHist<int32_t> bh{bk, bv, &bsat};
   bh.init();
   const int lane = threadIdx.x & 63;
   for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x; j0 < n; j0 += (int64_t)gridDim.x * blockDim.x) {
@@ -456,7 +458,11 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     LPA_HIP(hipGetLastError());
     int shifts[16], ns = 0;
     int blo = bits_for((uint64_t)(g->vpad - 1)), bhi = bits_for((uint64_t)(S - 1));
-    for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
+    // columns sorted inside each row: the rebuild's gathers of a hub row coalesce.  No
+    // kernel needs the order (a mode is order-free), so a pooled internal graph (the
+    // outlier stage's 5-superstep L2 sub-graph) sorts by row only: half the passes.
+    if (!g->pooled)
+      for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
     LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t) * arcs));

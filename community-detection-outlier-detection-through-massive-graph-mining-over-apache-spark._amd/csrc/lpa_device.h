@@ -241,21 +241,27 @@ constexpr int kBhLg = 12;
 constexpr int kBhSlots = 1 << kBhLg;
 constexpr int kBhProbes = 8;
 constexpr u32 kBhEmpty = 0xFFFFFFFFu;
+// Once a key has failed every probe the table is taken as saturated (random keys:
+// most later keys would fail too) and later keys probe their home slot only, where
+// the block's early (hub) keys mostly sit.
 template <typename T>
 struct BlockHist {
   u32* key;  // LDS [kBhSlots]
   T* val;    // LDS [kBhSlots]
+  int* sat;  // LDS: the table has overflowed
   __device__ __forceinline__ void init() {
     for (int i = threadIdx.x; i < kBhSlots; i += blockDim.x) {
       key[i] = kBhEmpty;
       val[i] = (T)0;
     }
+    if (threadIdx.x == 0) *sat = 0;
     __syncthreads();
   }
   __device__ __forceinline__ bool lds_add(u32 k, T v) {
     u32 h = (k * 0x9E3779B1u) >> (32 - kBhLg);
+    const int np = *sat ? 1 : kBhProbes;
 #pragma unroll 1
-    for (int p = 0; p < kBhProbes; ++p) {
+    for (int p = 0; p < np; ++p) {
       const u32 old = atomicCAS(&key[h], kBhEmpty, k);
       if (old == kBhEmpty || old == k) {
         atomicAdd(&val[h], v);
@@ -263,6 +269,7 @@ struct BlockHist {
       }
       h = (h + 1u) & (u32)(kBhSlots - 1);
     }
+    *sat = 1;
     return false;
   }
   // weighted: lanes with act add v to hist[k]

@@ -77,7 +77,8 @@ __global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ l
                                                    unsigned long long* __restrict__ bad) {
   __shared__ u32 bk[dev::kBhSlots];
   __shared__ int32_t bv[dev::kBhSlots];
-  dev::BlockHist<int32_t> bh{bk, bv};
+  __shared__ int bsat;
+  dev::BlockHist<int32_t> bh{bk, bv, &bsat};
   bh.init();
   const int lane = threadIdx.x & 63;
   GRID_STRIDE_UNIFORM_BEGIN(v, act, V)
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(256) void k_incident(const u64* __restrict__ ek, in
                                                   int32_t* __restrict__ inc) {
   __shared__ u32 bk[dev::kBhSlots];
   __shared__ int32_t bv[dev::kBhSlots];
-  dev::BlockHist<int32_t> bh{bk, bv};
+  __shared__ int bsat;
+  dev::BlockHist<int32_t> bh{bk, bv, &bsat};
   bh.init();
   const int lane = threadIdx.x & 63;
   GRID_STRIDE_UNIFORM_BEGIN(i, act, n)
