@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <vector>
 #include <algorithm>
@@ -176,6 +177,12 @@ int main(int argc, char** argv) {
   for (int64_t T : {40960ll, 1ll << 20, 1ll << 22, 1ll << 23}) if (T < V) printf("arcs with col < %ld: %.1f%%\n", (long)T, 100.0 * cdeg[T] / cdeg[V]);
   const int32_t BIG = 0x7fffffff;
   timeit("floor: stream col -> al", [&] { hipLaunchKernelGGL(k_floor, dim3(cus), dim3(1024), 0, 0, col, arcs, al); });
+  // MB_BASIC=1 (PMC calibration passes): the stream floor and the shipped kernel only
+  const bool basic = getenv("MB_BASIC") != nullptr;
+  if (basic) {
+    timeit("hot LDS 40960 (NT) [shipped]", [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
+    return 0;
+  }
   timeit("plain gathers (NT streams)", [&] { hipLaunchKernelGGL((k_hot<0, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
   timeit("hot LDS 40960 (NT) [shipped]", [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
   timeit("hot LDS 40960 (cached streams)", [&] { hipLaunchKernelGGL((k_hot<40960, false>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });

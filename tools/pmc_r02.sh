@@ -12,7 +12,7 @@ TAG=${TAG:-pmc}
 timeout -k 10 200 python3 tools/microbench/dump_deg.py C3 /tmp/deg_c3.bin > /dev/null || exit 1
 for C in FETCH_SIZE WRITE_SIZE; do
   c=$(echo $C | cut -d_ -f1 | tr A-Z a-z)
-  timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex "k_floor|k_hot" -d gpurun_out/${TAG}_pmc_mb_$c -o run --output-format csv -- ./tools/microbench/mb_rebuild /tmp/deg_c3.bin 2 > gpurun_out/${TAG}_pmc_mb_$c.log 2>&1 || { echo "mb pass $C failed"; tail -5 gpurun_out/${TAG}_pmc_mb_$c.log; exit 1; }
+  MB_BASIC=1 timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex "k_floor|k_hot" -d gpurun_out/${TAG}_pmc_mb_$c -o run --output-format csv -- ./tools/microbench/mb_rebuild /tmp/deg_c3.bin 2 > gpurun_out/${TAG}_pmc_mb_$c.log 2>&1 || { echo "mb pass $C failed"; tail -5 gpurun_out/${TAG}_pmc_mb_$c.log; exit 1; }
   timeout -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "k_lpa_units|k_al_rebuild_hot|k_diff|k_lpa_wave|k_lpa_rows" -d gpurun_out/${TAG}_pmc_lib_$c -o run --output-format csv -- python3 tools/pmc_workload.py gpurun_out/${TAG}_info.json > gpurun_out/${TAG}_pmc_lib_$c.log 2>&1 || { echo "lib pass $C failed"; tail -5 gpurun_out/${TAG}_pmc_lib_$c.log; exit 1; }
 done
 python3 tools/pmc_r02.py gpurun_out/${TAG} > gpurun_out/${TAG}_traffic.json && cat gpurun_out/${TAG}_traffic.json
