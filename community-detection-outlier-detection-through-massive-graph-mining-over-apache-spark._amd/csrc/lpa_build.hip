@@ -461,7 +461,8 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     // columns sorted inside each row: the rebuild's gathers of a hub row coalesce.  No
     // kernel needs the order (a mode is order-free), so a pooled internal graph (the
     // outlier stage's 5-superstep L2 sub-graph) sorts by row only: half the passes.
-    if (!g->pooled)
+    g->cols_sorted = !g->pooled;
+    if (g->cols_sorted)
       for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
@@ -608,6 +609,12 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   LPA_TRY(dev_alloc(g, (void**)&g->flist, sizeof(int32_t) * S));
   LPA_TRY(dev_alloc(g, (void**)&g->ulist, sizeof(int32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
   LPA_TRY(dev_alloc(g, (void**)&g->fcnt, sizeof(int32_t) * 32));
+  // superstep-1 column-run tally (lpa_iter.hip k_first_runs): per-row maxima of rows that
+  // span run tiles (zero between uses)
+  if (g->cols_sorted) {
+    LPA_TRY(dev_alloc(g, (void**)&g->first_best, sizeof(u64) * S));
+    LPA_HIP(hipMemsetAsync(g->first_best, 0, sizeof(u64) * S, s));
+  }
   if (g->crow == nullptr) LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t)));
 
   // ---- labels (replicated, ping-pong) ----

@@ -166,6 +166,9 @@ struct lpa_graph {
   int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches
   int fold_rebuild = 1;           // LPA_FOLD_REBUILD=0: captured converged supersteps keep the rebuild launch
   int block_steps = 2;            // LPA_BLOCK_STEPS: supersteps after L0 in block mode (k_lpa_block rows)
+  int first_runs = 1;             // LPA_FIRST_RUNS=0: superstep 1 by the hash tallies, not column runs
+  bool cols_sorted = true;        // columns ascending inside each row (false: row-only sorted build)
+  lpa::u64* first_best = nullptr; // [slice] superstep-1 best run word of rows spanning run tiles
   int block_at = 4;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the
                                   // main stream, or (2) on the fourth stream, concurrent with them,
                                   // or (3) split: the wide tier on the fourth stream, the 8-wave

@@ -1465,6 +1465,105 @@ __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __r
     out[i] = L[new_of[i]];
 }
 
+// ---------------------------------------------------------------------------
+// Superstep 1 from L0 (after a reset): L0 is injective, so two votes of a row carry
+// the same label exactly when they come from the same column, and a row's columns
+// are sorted: its vote counts are the lengths of its runs of equal columns
+// (duplicate edges, a self-loop's two arcs).  The mode -- longest run, ties to the
+// smallest label -- is a segmented max over the arc stream, with no hash table.
+// A wave takes 256-arc tiles (4 chunks of 64 lanes): run lengths from a ballot of
+// the run starts, a per-row segmented max scan by shuffles, carries from chunk to
+// chunk; a row inside the tile is written directly, a row crossing a tile boundary
+// folds each piece into first_best[row] and k_first_final writes it.
+// ---------------------------------------------------------------------------
+constexpr int kRunTile = 256;
+
+__device__ __forceinline__ u64 shfl_up_u64(u64 v, int off) {
+  const u32 lo = (u32)__shfl_up((int)(u32)v, off, 64), hi = (u32)__shfl_up((int)(u32)(v >> 32), off, 64);
+  return ((u64)hi << 32) | lo;
+}
+
+__global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ al,
+                                                    const int32_t* __restrict__ crow,
+                                                    const int64_t* __restrict__ rp, int64_t arcs,
+                                                    int32_t* __restrict__ Ln, u64* __restrict__ best) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRunTile; t0 < arcs;
+       t0 += nw * kRunTile) {
+    const int64_t t1 = t0 + kRunTile < arcs ? t0 + kRunTile : arcs;
+    // carry: row, label, run length and row maximum at the position before the chunk
+    // (the row maximum starts at 0 in a tile: the previous tile folded its part)
+    int32_t cr = -1;
+    u32 ca = kNone, ck = 0u;
+    u64 cw = 0ull;
+    if (t0 > 0) {
+      cr = crow[t0 - 1];
+      ca = (u32)al[t0 - 1];
+      int k = 0;
+      if (lane == 0) {  // the run's length up to t0 - 1 (runs are short)
+        k = 1;
+        while (t0 - 1 - k >= 0 && crow[t0 - 1 - k] == cr && (u32)al[t0 - 1 - k] == ca) ++k;
+      }
+      ck = (u32)__builtin_amdgcn_readfirstlane(k);
+    }
+#pragma unroll
+    for (int c = 0; c < kRunTile / 64; ++c) {
+      const int64_t i = t0 + c * 64 + lane;
+      const bool live = i < t1;  // every lane runs every shuffle
+      const int32_t r = live ? crow[i] : -2;
+      const u32 a = live ? (u32)al[i] : kNone;
+      int32_t rprev = __shfl_up(r, 1, 64);
+      u32 aprev = (u32)__shfl_up((int)a, 1, 64);
+      if (lane == 0) {
+        rprev = cr;
+        aprev = ca;
+      }
+      const u64 starts = __ballot(r != rprev || a != aprev);
+      const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+      const u64 m = starts & upto;
+      const u32 k = m ? (u32)(lane - (63 - __clzll((long long)m)) + 1) : (u32)lane + 1u + ck;
+      u64 w = live ? (((u64)k << 32) | (u64)(~a)) : 0ull;
+      if (r == cr && cw > w) w = cw;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const u64 wo = shfl_up_u64(w, off);
+        const int32_t ro = __shfl_up(r, off, 64);
+        if (lane >= off && ro == r && wo > w) w = wo;
+      }
+      const int32_t rnext = __shfl_down(r, 1, 64);
+      if (live && (lane == 63 || rnext != r)) {  // the row's last lane in this chunk
+        if (i + 1 == rp[r + 1]) {
+          if (rp[r] >= t0) Ln[r] = (int32_t)(~(u32)w);
+          else atomicMax(&best[r], w);
+        } else if (i + 1 == t1) {
+          atomicMax(&best[r], w);  // continues in the next tile
+        }
+      }
+      cr = __shfl(r, 63, 64);
+      ca = (u32)__shfl((int)a, 63, 64);
+      ck = (u32)__shfl((int)k, 63, 64);
+      cw = ((u64)(u32)__shfl((int)(u32)(w >> 32), 63, 64) << 32) | (u64)(u32)__shfl((int)(u32)w, 63, 64);
+    }
+  }
+}
+
+// rows that cross a run tile: label from the folded maximum (reset for the next
+// use); both parities' hub queue counters start from zero (superstep 1 skips the
+// hub combine, whose last kernel otherwise resets the next parity's)
+__global__ void k_first_final(const int64_t* __restrict__ rp, int64_t S, u64* __restrict__ best,
+                              int32_t* __restrict__ Ln, int32_t* __restrict__ hub_lcnt) {
+  if (hub_lcnt && blockIdx.x == 0 && threadIdx.x < 16) hub_lcnt[threadIdx.x] = 0;  // null: no hub rows
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < S;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = rp[r], e = rp[r + 1];
+    if (e > b && b / kRunTile != (e - 1) / kRunTile) {
+      Ln[r] = (int32_t)(~(u32)best[r]);
+      best[r] = 0ull;
+    }
+  }
+}
+
 inline unsigned cap_grid(int64_t want, int64_t cap) {
   if (want < 1) want = 1;
   return (unsigned)(want < cap ? want : cap);
@@ -1484,6 +1583,38 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // diff (P = 1, concurrent schedule): each stream diffs the slots its own bins
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
 // rows after the hub combine), overlapping most of the diff with the tally tail
+// the per-bin dirty-row lists of this superstep (zeroes the other parity's counts)
+int launch_frontier_lists(lpa_graph* g) {
+  BinBounds bnd;
+  for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = g->bin_begin[b];
+  const int64_t nbr = (g->slice + kListTile - 1) / kListTile;
+  const int64_t nbu = (g->n_segs + kListTile - 1) / kListTile;
+  hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, g->stream, g->rdirty[g->par],
+                     g->slice, g->udirty[g->par], g->n_segs, bnd, g->fr_all + g->par, g->flist, g->ulist,
+                     g->fcnt + 16 * g->par, g->fcnt + 16 * (g->par ^ 1), nbr);
+  LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
+
+// superstep 1 from L0 by column runs (k_first_runs); the caller's refresh diffs
+bool first_runs_now(const lpa_graph* g) {
+  return g->first_runs && g->cols_sorted && g->first_best && g->since_reset == 0 && g->arcs > 0 &&
+         !g->serial;
+}
+
+int launch_first(lpa_graph* g, int32_t* Lown) {
+  hipStream_t s = g->stream;
+  LPA_TRY(launch_frontier_lists(g));
+  const int64_t ntiles = (g->arcs + kRunTile - 1) / kRunTile;
+  hipLaunchKernelGGL(k_first_runs, dim3(cap_grid((ntiles + 3) / 4, 8192)), dim3(256), 0, s, g->al, g->crow, g->rp,
+                     g->arcs, Lown, g->first_best);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_first_final, dim3(cap_grid((g->slice + 255) / 256, 4096)), dim3(256), 0, s, g->rp,
+                     g->slice, g->first_best, Lown, g->hub_lcnt);
+  LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
+
 int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc,
                  const int32_t* Ln, bool diff) {
   hipStream_t s = g->stream;
@@ -1495,16 +1626,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   int32_t* fcnt = g->fcnt + 16 * g->par;
   // frontier lists of this superstep (no-op when every row is tallied)
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 4], s));
-  {
-    BinBounds bnd;
-    for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = bb[b];
-    const int64_t nbr = (g->slice + kListTile - 1) / kListTile;
-    const int64_t nbu = (g->n_segs + kListTile - 1) / kListTile;
-    hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, s, g->rdirty[g->par],
-                       g->slice, g->udirty[g->par], g->n_segs, bnd, fr_all, g->flist, g->ulist, fcnt,
-                       g->fcnt + 16 * (g->par ^ 1), nbr);
-    LPA_HIP(hipGetLastError());
-  }
+  LPA_TRY(launch_frontier_lists(g));
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
@@ -1818,7 +1940,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // superstep only, so a timed converged superstep still replays its graph
     hipEvent_t* bev = (tt && g->serial) ? &g->bin_ev[t * kBinEvents] : nullptr;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
-    const bool diff_in_tally = g->nranks == 1 && !g->serial;
+    // superstep 1 from L0: column runs, no hash tallies (its diff runs in the refresh)
+    const bool first = first_runs_now(g);
+    const bool diff_in_tally = g->nranks == 1 && !g->serial && !first;
     // converged supersteps on one GPU replay a captured HIP graph of the whole
     // superstep (tally on four streams + diff + refresh; ~25 kernels and the
     // fork/join events): one launch instead of ~40 queue operations.  The graph bakes
@@ -1854,6 +1978,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
         LPA_TRY(capture_graph(g, &g->gexec[key],
                               [&]() -> int { return launch_tally(g, Lown, nullptr, Lc, Ln, diff_in_tally); }));
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
+    } else if (first) {
+      LPA_TRY(launch_first(g, Lown));
     } else {
       LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
     }
