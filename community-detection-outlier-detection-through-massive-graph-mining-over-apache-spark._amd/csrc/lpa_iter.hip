@@ -1471,12 +1471,12 @@ __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __r
 // are sorted: its vote counts are the lengths of its runs of equal columns
 // (duplicate edges, a self-loop's two arcs).  The mode -- longest run, ties to the
 // smallest label -- is a segmented max over the arc stream, with no hash table.
-// A wave takes 256-arc tiles (4 chunks of 64 lanes): run lengths from a ballot of
+// A wave takes 512-arc tiles (8 chunks of 64 lanes): run lengths from a ballot of
 // the run starts, a per-row segmented max scan by shuffles, carries from chunk to
 // chunk; a row inside the tile is written directly, a row crossing a tile boundary
 // folds each piece into first_best[row] and k_first_final writes it.
 // ---------------------------------------------------------------------------
-constexpr int kRunTile = 256;
+constexpr int kRunTile = 512;
 
 __device__ __forceinline__ u64 shfl_up_u64(u64 v, int off) {
   const u32 lo = (u32)__shfl_up((int)(u32)v, off, 64), hi = (u32)__shfl_up((int)(u32)(v >> 32), off, 64);
@@ -1500,12 +1500,12 @@ __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ 
     if (t0 > 0) {
       cr = crow[t0 - 1];
       ca = (u32)al[t0 - 1];
-      int k = 0;
-      if (lane == 0) {  // the run's length up to t0 - 1 (runs are short)
-        k = 1;
+      if (crow[t0] == cr && (u32)al[t0] == ca) {
+        // a run continues into the tile (rare): its length up to t0 - 1
+        int64_t k = 1;
         while (t0 - 1 - k >= 0 && crow[t0 - 1 - k] == cr && (u32)al[t0 - 1 - k] == ca) ++k;
+        ck = (u32)k;
       }
-      ck = (u32)__builtin_amdgcn_readfirstlane(k);
     }
 #pragma unroll
     for (int c = 0; c < kRunTile / 64; ++c) {
