@@ -1478,14 +1478,22 @@ __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __r
 // ---------------------------------------------------------------------------
 constexpr int kRunTile = 512;
 
-__device__ __forceinline__ u64 shfl_up_u64(u64 v, int off) {
-  const u32 lo = (u32)__shfl_up((int)(u32)v, off, 64), hi = (u32)__shfl_up((int)(u32)(v >> 32), off, 64);
-  return ((u64)hi << 32) | lo;
+// One step of a segmented (by row id) inclusive max scan over the wave, in DPP: the
+// lane's source (row shift within 16-lane rows, or a row broadcast) is moved by VALU
+// lane permutes, no LDS; lanes without a source (or outside ROWMASK) see row
+// INT_MIN and combine nothing.  Rows are contiguous lanes, so an equal row id at
+// the source means every lane in between is the same row.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void seg_max_step(u64& w, int32_t r) {
+  const int32_t ro = __builtin_amdgcn_update_dpp((int)0x80000000, r, kCtrl, kRowMask, 0xF, false);
+  const u32 lo = (u32)__builtin_amdgcn_update_dpp(0, (int)(u32)w, kCtrl, kRowMask, 0xF, false);
+  const u32 hi = (u32)__builtin_amdgcn_update_dpp(0, (int)(u32)(w >> 32), kCtrl, kRowMask, 0xF, false);
+  const u64 wo = ((u64)hi << 32) | lo;
+  if (ro == r && wo > w) w = wo;
 }
 
 __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ al,
-                                                    const int32_t* __restrict__ crow,
-                                                    const int64_t* __restrict__ rp, int64_t arcs,
+                                                    const int32_t* __restrict__ crow, int64_t arcs,
                                                     int32_t* __restrict__ Ln, u64* __restrict__ best) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -1507,43 +1515,55 @@ __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ 
         ck = (u32)k;
       }
     }
+    // the tile's labels and rows, every load in flight before the first chunk's scan;
+    // rows are contiguous, so a row started inside the tile iff it differs from the
+    // row before the tile, and ends at i iff position i + 1 holds another row
+    const int32_t r_before = cr;
+    const int32_t r_after = t1 < arcs ? crow[t1] : -3;
+    constexpr int kC = kRunTile / 64;
+    int32_t rr[kC];
+    u32 aa[kC];
 #pragma unroll
-    for (int c = 0; c < kRunTile / 64; ++c) {
+    for (int c = 0; c < kC; ++c) {
+      const int64_t i = t0 + c * 64 + lane;
+      rr[c] = i < t1 ? __builtin_nontemporal_load(crow + i) : -2;
+      aa[c] = i < t1 ? (u32)__builtin_nontemporal_load(al + i) : kNone;
+    }
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
       const int64_t i = t0 + c * 64 + lane;
       const bool live = i < t1;  // every lane runs every shuffle
-      const int32_t r = live ? crow[i] : -2;
-      const u32 a = live ? (u32)al[i] : kNone;
-      int32_t rprev = __shfl_up(r, 1, 64);
-      u32 aprev = (u32)__shfl_up((int)a, 1, 64);
-      if (lane == 0) {
-        rprev = cr;
-        aprev = ca;
-      }
+      const int32_t r = rr[c];
+      const u32 a = aa[c];
+      // lane - 1's row and label (DPP wave_shr:1; lane 0 takes the carry)
+      const int32_t rprev = __builtin_amdgcn_update_dpp(cr, r, 0x138, 0xF, 0xF, false);
+      const u32 aprev = (u32)__builtin_amdgcn_update_dpp((int)ca, (int)a, 0x138, 0xF, 0xF, false);
       const u64 starts = __ballot(r != rprev || a != aprev);
       const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
       const u64 m = starts & upto;
       const u32 k = m ? (u32)(lane - (63 - __clzll((long long)m)) + 1) : (u32)lane + 1u + ck;
       u64 w = live ? (((u64)k << 32) | (u64)(~a)) : 0ull;
       if (r == cr && cw > w) w = cw;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const u64 wo = shfl_up_u64(w, off);
-        const int32_t ro = __shfl_up(r, off, 64);
-        if (lane >= off && ro == r && wo > w) w = wo;
+      seg_max_step<0x111, 0xF>(w, r);  // row_shr:1
+      seg_max_step<0x112, 0xF>(w, r);  // row_shr:2
+      seg_max_step<0x114, 0xF>(w, r);  // row_shr:4
+      seg_max_step<0x118, 0xF>(w, r);  // row_shr:8
+      seg_max_step<0x142, 0xA>(w, r);  // row_bcast:15 into rows 1, 3
+      seg_max_step<0x143, 0xC>(w, r);  // row_bcast:31 into rows 2, 3
+      // lane + 1's row (DPP wave_shl:1; lane 63: the next chunk's first row)
+      const int32_t r63 = c + 1 < kC ? __builtin_amdgcn_readlane(rr[c + 1 < kC ? c + 1 : c], 0) : r_after;
+      const int32_t rnext = __builtin_amdgcn_update_dpp(r63, r, 0x130, 0xF, 0xF, false);
+      if (live && rnext != r) {  // the row ends at i
+        if (r != r_before) Ln[r] = (int32_t)(~(u32)w);
+        else atomicMax(&best[r], w);
+      } else if (live && i + 1 == t1) {
+        atomicMax(&best[r], w);  // continues in the next tile
       }
-      const int32_t rnext = __shfl_down(r, 1, 64);
-      if (live && (lane == 63 || rnext != r)) {  // the row's last lane in this chunk
-        if (i + 1 == rp[r + 1]) {
-          if (rp[r] >= t0) Ln[r] = (int32_t)(~(u32)w);
-          else atomicMax(&best[r], w);
-        } else if (i + 1 == t1) {
-          atomicMax(&best[r], w);  // continues in the next tile
-        }
-      }
-      cr = __shfl(r, 63, 64);
-      ca = (u32)__shfl((int)a, 63, 64);
-      ck = (u32)__shfl((int)k, 63, 64);
-      cw = ((u64)(u32)__shfl((int)(u32)(w >> 32), 63, 64) << 32) | (u64)(u32)__shfl((int)(u32)w, 63, 64);
+      cr = __builtin_amdgcn_readlane(r, 63);
+      ca = (u32)__builtin_amdgcn_readlane((int)a, 63);
+      ck = (u32)__builtin_amdgcn_readlane((int)k, 63);
+      cw = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(w >> 32), 63) << 32) |
+           (u64)(u32)__builtin_amdgcn_readlane((int)(u32)w, 63);
     }
   }
 }
@@ -1606,7 +1626,7 @@ int launch_first(lpa_graph* g, int32_t* Lown) {
   hipStream_t s = g->stream;
   LPA_TRY(launch_frontier_lists(g));
   const int64_t ntiles = (g->arcs + kRunTile - 1) / kRunTile;
-  hipLaunchKernelGGL(k_first_runs, dim3(cap_grid((ntiles + 3) / 4, 8192)), dim3(256), 0, s, g->al, g->crow, g->rp,
+  hipLaunchKernelGGL(k_first_runs, dim3(cap_grid((ntiles + 3) / 4, 8192)), dim3(256), 0, s, g->al, g->crow,
                      g->arcs, Lown, g->first_best);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_first_final, dim3(cap_grid((g->slice + 255) / 256, 4096)), dim3(256), 0, s, g->rp,
