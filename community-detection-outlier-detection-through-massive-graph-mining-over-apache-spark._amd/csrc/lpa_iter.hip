@@ -1794,7 +1794,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   if (diff) {
     // inside the concurrent tally: no Lc sync here, the scatter refresh does it
     LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2], false, g->par, BIN_W16, BIN_W2));
-    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], g->vpad, false, g->par, BIN_W2, BIN_ISO));
+    // isolated slots (and the padding) never change: the diff stops at the isolated bin
+    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], bb[BIN_ISO], false, g->par, BIN_W2, BIN_ISO));
     LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par, BIN_SEG, BIN_W16));
   }
   if (!g->serial) {
@@ -1876,7 +1877,10 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   hipStream_t s = g->stream;
   // this superstep's counters (zeroed by the previous k_al_scatter or at build)
   unsigned long long* ctr = g->counters + 4 * par;
-  if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, g->vpad, true, par));
+  // one rank: its isolated slots (and the padding) never change; P > 1: the whole
+  // replicated vector (other ranks' slots change through the exchange)
+  if (!diff_done)
+    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, g->nranks == 1 ? g->bin_begin[BIN_ISO] : g->vpad, true, par));
   LPA_TRACE_POINT("diff");
   const int64_t thr = (int64_t)(g->rebuild_frac * (double)g->arcs);
   FrontierMarks fm;
