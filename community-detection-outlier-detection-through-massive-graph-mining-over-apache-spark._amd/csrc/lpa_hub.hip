@@ -335,7 +335,6 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
   u64* tab = tab_all[w];
   uint16_t* pre = aux_all[w];
   uint16_t* lst = aux_all[w];
-  for (int i = lane; i < kSmallSlots; i += 64) tab[i] = 0ull;
   // rows: [0, nd) directly, then list S (pre-classified by k_hub_classify), then
   // list W (from k_hub_lanes)
   // direct rows [0, nd): with the frontier, the listed dirty hub rows below nd
@@ -344,6 +343,8 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
   const int64_t nS = lcnt[7];
   const int64_t nq = nd_items + nS + lcnt[4];
   const int64_t stride = (int64_t)gridDim.x * 4;
+  if ((int64_t)blockIdx.x * 4 + w >= nq) return;  // no block-level barriers in this kernel
+  for (int i = lane; i < kSmallSlots; i += 64) tab[i] = 0ull;  // only waves with rows clear
   for (int64_t q = (int64_t)blockIdx.x * 4 + w; q < nq; q += stride) {
     const int64_t h = q < nd_items ? (all ? q : (int64_t)flist[q])
                                    : (q < nd_items + nS ? (int64_t)lists[5 * n_hub + (q - nd_items)]

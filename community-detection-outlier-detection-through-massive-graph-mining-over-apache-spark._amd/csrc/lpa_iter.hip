@@ -553,12 +553,12 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   u64* tab = tab_all[w];
   uint16_t* lst = lst_all[w];
-  for (int i = lane; i < kCap; i += 64) tab[i] = 0ull;
   const u64 lt = (1ull << lane) - 1ull;
   const int64_t stride = (int64_t)gridDim.x * 4;
   const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
   int64_t i = (int64_t)blockIdx.x * 4 + w;   // work item: row br.row(i)
   if (i >= br.n) return;  // no block-level barriers in this kernel
+  for (int k = lane; k < kCap; k += 64) tab[k] = 0ull;  // only waves with rows clear
   RowSpan s0 = row_span(rp, br, i), s1 = row_span(rp, br, i + stride), s2 = row_span(rp, br, i + 2 * stride);
   u32 ra[NC], rb[NC], rc[NC];
   row_load<NC>(ra, al, s0, lane);
@@ -884,7 +884,6 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   u64* tab = tab_all[w];
   uint16_t* lst = lst_all[w];
-  for (int i = lane; i < kCap; i += 64) tab[i] = 0ull;
   const u64 lt = (1ull << lane) - 1ull;
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t u = (int64_t)blockIdx.x * 4 + w;
@@ -895,6 +894,9 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
   ui.n = *fr_all ? nunits : (int64_t)*fcnt_u;
   ui.list = *fr_all ? nullptr : ulist;
   if (u >= ui.n) return;
+  // the wave's table is cleared only by waves with work (a frontier superstep lists
+  // few units: most of the grid leaves at once)
+  for (int i = lane; i < kCap; i += 64) tab[i] = 0ull;
   Segment d0 = load_unit(units, ui, u);
   Segment d1 = load_unit(units, ui, u + stride);
   Segment d2 = load_unit(units, ui, u + 2 * stride);
