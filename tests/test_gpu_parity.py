@@ -74,6 +74,47 @@ def test_edge_cases(gfa, oracle):
         assert g.run(2).tolist() == [0]
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_first_superstep_runs_cross_tiles(gfa, oracle, seed):
+    """Superstep 1 by column runs (k_first_runs): duplicate-edge runs of up to a few
+    thousand arcs that cross the 512-arc run tiles, ties between equal-length runs (the
+    smallest label wins), self-loop runs, rows of every length from 1 to ~20 K arcs
+    crossing tiles at every offset.  Bit-exact vs the oracle for supersteps 1-3, and
+    identical with the column-run path off (LPA_FIRST_RUNS=0)."""
+    rng = np.random.default_rng(seed)
+    V = 30_000
+    parts = []
+    hubs = rng.choice(V, 12, replace=False)
+    for h in hubs:
+        nb = rng.choice(V, int(rng.integers(50, 20_000)), replace=True)   # some repeats
+        parts.append(np.stack([np.full(nb.size, h), nb]))
+        for _ in range(4):                                              # long duplicate runs
+            u = int(rng.integers(0, V))
+            k = int(rng.integers(300, 3_000))
+            parts.append(np.stack([np.full(k, h), np.full(k, u)]))
+        parts.append(np.stack([np.full(700, h), np.full(700, h)]))      # self-loop run
+    # two equal-length runs: the smaller label must win
+    parts.append(np.stack([np.full(900, hubs[0]), np.full(900, 7)]))
+    parts.append(np.stack([np.full(900, hubs[0]), np.full(900, 5)]))
+    m_rand = 200_000
+    parts.append(rng.integers(0, V, size=(2, m_rand)))
+    e = np.concatenate(parts, axis=1).astype(np.int32)
+    s, d = e[0].copy(), e[1].copy()
+    _, hist, _ = oracle.lpa(V, s, d, 3, per_iter=True)
+    got = _per_step(gfa, V, s, d, 3)
+    for t in range(3):
+        assert np.array_equal(got[t], hist[t]), f"seed {seed} superstep {t + 1}"
+
+
+def test_first_runs_off_identical(gfa, monkeypatch):
+    s, d = gfa.gen_rmat(16, 16, seed=9)
+    V = 1 << 16
+    on = _per_step(gfa, V, s, d, 2)
+    monkeypatch.setenv("LPA_FIRST_RUNS", "0")
+    off = _per_step(gfa, V, s, d, 2)
+    assert np.array_equal(on, off)
+
+
 def test_bad_arguments(gfa):
     with gfa.Graph(np.array([0], np.int32), np.array([1], np.int32), 2) as g:
         with pytest.raises(ValueError, match="Maximum of steps must be greater than 0"):
