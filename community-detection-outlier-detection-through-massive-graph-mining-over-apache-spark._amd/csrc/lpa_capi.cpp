@@ -98,6 +98,7 @@ void destroy(lpa_graph* g) {
                          g->ev_join2[1], g->ev_join2[2]})
       if (e) (void)hipEventDestroy(e);
   }
+  if (g->host_pin) (void)hipHostFree(g->host_pin);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   if (g->own_stream) (void)hipStreamDestroy(g->own_stream);
   delete g;

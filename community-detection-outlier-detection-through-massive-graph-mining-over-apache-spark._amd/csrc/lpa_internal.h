@@ -247,6 +247,8 @@ struct lpa_graph {
   // and kept (label-independent topology, as GraphFrames' cachedTopologyGraphX)
   lpa::u64* de_keys = nullptr;
   int64_t de_n = -1;                        // -1: not built yet
+  void* host_pin = nullptr;                 // outlier stage: pinned staging of host labels in /
+  size_t host_pin_bytes = 0;                //   arrays out (kept with the handle)
 
   int64_t device_bytes = 0;
   bool pooled = false;                      // kFlagPooled: arrays from the stream-ordered pool

@@ -16,6 +16,11 @@
 // A sub-label L'[v] is the id of a vertex of v's own community (E' never
 // crosses communities), so the group (L[v], L'[v]) is identified by L'[v] alone
 // and its community is L[L'[v]].
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
 #include "lpa_device.h"
 
 namespace lpa {
@@ -302,6 +307,38 @@ int segmented_threshold(lpa_graph* g, Scratch& sc, const int32_t* size, const in
   return LPA_OK;
 }
 
+// Host side of the host-array interface: copies between the caller's (pageable)
+// arrays and a pinned staging area kept with the handle, split over threads (a
+// single-threaded copy of ~10^8 bytes is bound by the destination's first-touch page
+// faults; pageable hipMemcpy staged the same bytes through one thread).
+void par_copy(void* dst, const void* src, size_t n) {
+  const size_t kMin = size_t(8) << 20;
+  const int T = (int)std::min<size_t>(16, n / kMin);
+  if (T <= 1) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t step = (n + T - 1) / T;
+  for (int t = 0; t < T; ++t) {
+    const size_t a = (size_t)t * step;
+    if (a >= n) break;
+    const size_t b = std::min(n, a + step);
+    th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+  }
+  for (auto& x : th) x.join();
+}
+
+int ensure_pin(lpa_graph* g, size_t bytes) {
+  if (g->host_pin_bytes >= bytes) return LPA_OK;
+  if (g->host_pin) (void)hipHostFree(g->host_pin);
+  g->host_pin = nullptr;
+  g->host_pin_bytes = 0;
+  LPA_HIP(hipHostMalloc(&g->host_pin, bytes, hipHostMallocDefault));
+  g->host_pin_bytes = bytes;
+  return LPA_OK;
+}
+
 int bad_labels(unsigned long long n, int64_t V) {
   set_error("outlier: %llu labels outside [0, V=%lld)", n, (long long)V);
   return LPA_EINVAL;
@@ -345,8 +382,20 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     if (summary) *summary = sum;
     return LPA_OK;
   }
-  LPA_HIP(hipMemcpyAsync(L, labels, sizeof(int32_t) * V,
-                         labels_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  // pinned staging: [labels 4V | size 8V | incident 8V | sub-labels 4V | flags V]
+  LPA_TRY(ensure_pin(g, (size_t)25 * (size_t)V));
+  char* pin = (char*)g->host_pin;
+  int32_t* pin_lab = (int32_t*)pin;
+  int64_t* pin_size = (int64_t*)(pin + 4 * V);
+  int64_t* pin_inc = (int64_t*)(pin + 12 * V);
+  int32_t* pin_sub = (int32_t*)(pin + 20 * V);
+  uint8_t* pin_fl = (uint8_t*)(pin + 24 * V);
+  if (labels_on_device) {
+    LPA_HIP(hipMemcpyAsync(L, labels, sizeof(int32_t) * V, hipMemcpyDeviceToDevice, s));
+  } else {
+    par_copy(pin_lab, labels, sizeof(int32_t) * V);
+    LPA_HIP(hipMemcpyAsync(L, pin_lab, sizeof(int32_t) * V, hipMemcpyHostToDevice, s));
+  }
   LPA_HIP(hipMemsetAsync(size, 0, sizeof(int32_t) * V, s));
   LPA_HIP(hipMemsetAsync(inc, 0, sizeof(int32_t) * V, s));
   LPA_HIP(hipMemsetAsync(segflag, 0, sizeof(int32_t) * V, s));
@@ -430,7 +479,7 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     LPA_HIP(hipGetLastError());
     unsigned long long h_cnt[8];
     LPA_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
-    if (sub_labels) LPA_HIP(hipMemcpyAsync(sub_labels, sub, sizeof(int32_t) * V, hipMemcpyDeviceToHost, s));
+    if (sub_labels) LPA_HIP(hipMemcpyAsync(pin_sub, sub, sizeof(int32_t) * V, hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
     sum.n_groups = (int64_t)h_cnt[4];
     sum.k = -1;
@@ -441,20 +490,24 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     sum.distinct_edges = md;
   }
 
+  // every output into the pinned area in stream order (`wide` is reused: each copy is
+  // ordered before the next widening), one sync, then the threaded host copies
   if (size_hist) {
     hipLaunchKernelGGL(k_widen, dim3(grid_for(V)), dim3(256), 0, s, size, V, wide);
     LPA_HIP(hipGetLastError());
-    LPA_HIP(hipMemcpyAsync(size_hist, wide, sizeof(int64_t) * V, hipMemcpyDeviceToHost, s));
-    LPA_HIP(hipStreamSynchronize(s));
+    LPA_HIP(hipMemcpyAsync(pin_size, wide, sizeof(int64_t) * V, hipMemcpyDeviceToHost, s));
   }
   if (incident) {
     hipLaunchKernelGGL(k_widen, dim3(grid_for(V)), dim3(256), 0, s, inc, V, wide);
     LPA_HIP(hipGetLastError());
-    LPA_HIP(hipMemcpyAsync(incident, wide, sizeof(int64_t) * V, hipMemcpyDeviceToHost, s));
-    LPA_HIP(hipStreamSynchronize(s));
+    LPA_HIP(hipMemcpyAsync(pin_inc, wide, sizeof(int64_t) * V, hipMemcpyDeviceToHost, s));
   }
-  if (flags) LPA_HIP(hipMemcpyAsync(flags, fl, V, hipMemcpyDeviceToHost, s));
+  if (flags) LPA_HIP(hipMemcpyAsync(pin_fl, fl, V, hipMemcpyDeviceToHost, s));
   LPA_HIP(hipStreamSynchronize(s));
+  if (size_hist) par_copy(size_hist, pin_size, sizeof(int64_t) * V);
+  if (incident) par_copy(incident, pin_inc, sizeof(int64_t) * V);
+  if (mode == 2 && sub_labels) par_copy(sub_labels, pin_sub, sizeof(int32_t) * V);
+  if (flags) par_copy(flags, pin_fl, V);
   if (summary) *summary = sum;
   return LPA_OK;
 }
