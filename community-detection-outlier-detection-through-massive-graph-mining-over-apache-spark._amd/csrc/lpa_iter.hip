@@ -1765,7 +1765,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb)
   LPA_WAVE_LAUNCH(BIN_W2, 2, sc)
-  LPA_ROWS_LAUNCH(BIN_G64, 64)
+  if (g->g64_wave) LPA_WAVE_LAUNCH(BIN_G64, 1, sc) else LPA_ROWS_LAUNCH(BIN_G64, 64)
   LPA_ROWS_LAUNCH(BIN_G32, 32)
   LPA_ROWS_LAUNCH(BIN_G16, 16)
   LPA_ROWS_LAUNCH(BIN_G8, 8)
