@@ -89,6 +89,35 @@ __global__ __launch_bounds__(1024) void k_hot_nt(const int32_t* __restrict__ col
     for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
   }
 }
+// XCD-split rebuild: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8);
+// XCDs 0-3 gather the arcs whose column is < T (plus the LDS hot set), XCDs 4-7 the
+// rest, so each XCD's L2 caches half of the gathered label range.  Every block streams
+// col over its group's share of the arcs (col is read twice in all).
+__global__ __launch_bounds__(1024) void k_hot_xcd(const int32_t* __restrict__ col, int64_t arcs,
+                                                  const int32_t* __restrict__ L, int32_t* __restrict__ al, int32_t T) {
+  __shared__ int32_t hot[40960];
+  const bool ga = (blockIdx.x & 7) < 4;
+  if (ga) for (int i = threadIdx.x; i < 40960; i += 1024) hot[i] = L[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t gb = ((int64_t)(blockIdx.x >> 3) * 4 + ((blockIdx.x & 7) & 3));  // block index within its group
+  const int64_t ng = (int64_t)gridDim.x / 2;
+  const int64_t nw = ng * (blockDim.x >> 6);
+  for (int64_t base = (gb * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512; base + 512 <= arcs; base += nw * 512) {
+    int32_t c[8], r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + base + k * 64 + lane);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int32_t x = c[k];
+      const bool mine = ga ? x < T : x >= T;
+      r[k] = mine ? (ga && x < 40960 ? hot[x] : L[x]) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (ga ? c[k] < T : c[k] >= T) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
+  }
+}
 // cold list: al[cpos[j]] = L[ccol[j]] for the listed arcs (position-ordered or
 // column-ordered lists)
 __global__ __launch_bounds__(256) void k_cold_list(const uint32_t* __restrict__ cpos, const int32_t* __restrict__ ccol,
@@ -179,6 +208,15 @@ int main(int argc, char** argv) {
   timeit("floor: stream col -> al", [&] { hipLaunchKernelGGL(k_floor, dim3(cus), dim3(1024), 0, 0, col, arcs, al); });
   // MB_BASIC=1 (PMC calibration passes): the stream floor and the shipped kernel only
   const bool basic = getenv("MB_BASIC") != nullptr;
+  if (getenv("MB_XCD")) {
+    timeit("hot LDS 40960 (NT) [shipped]", [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
+    for (int32_t T : {131072, 262144, 524288, 1 << 20, 1 << 21}) {
+      char nm[80];
+      snprintf(nm, 80, "XCD split at %d", T);
+      timeit(nm, [&] { hipLaunchKernelGGL(k_hot_xcd, dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, T); });
+    }
+    return 0;
+  }
   if (basic) {
     timeit("hot LDS 40960 (NT) [shipped]", [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
     return 0;
