@@ -172,6 +172,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_HUB_FUSE")) g->hub_fuse = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FOLD_REBUILD")) g->fold_rebuild = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_BLOCK")) g->block_rows = atoi(f) ? 1 : 0;
+  if (const char* f = getenv("LPA_EARLY_SORT")) g->early_sort = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_G64_WAVE")) g->g64_wave = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_BLOCK_STEPS")) g->block_steps = atoi(f) < 0 ? 0 : (atoi(f) > 8 ? 8 : atoi(f));

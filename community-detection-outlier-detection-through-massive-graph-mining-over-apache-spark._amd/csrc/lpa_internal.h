@@ -166,6 +166,7 @@ struct lpa_graph {
   int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches
   int fold_rebuild = 1;           // LPA_FOLD_REBUILD=0: captured converged supersteps keep the rebuild launch
   int block_steps = 2;            // LPA_BLOCK_STEPS: supersteps after L0 in block mode (k_lpa_block rows)
+  int early_sort = 0;             // LPA_EARLY_SORT=1: row bins sort a chunk once a peel round finds no repeat
   int g64_wave = 0;               // LPA_G64_WAVE=1: rows of 32 < deg <= 64 by the wave-hash kernel
   int first_runs = 1;             // LPA_FIRST_RUNS=0: superstep 1 by the hash tallies, not column runs
   bool cols_sorted = true;        // columns ascending inside each row (false: row-only sorted build)

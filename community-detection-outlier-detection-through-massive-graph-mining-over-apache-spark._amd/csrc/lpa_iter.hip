@@ -719,7 +719,8 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend, const int32_t* __restrict__ flist,
                                                   const int32_t* __restrict__ fcnt_b,
-                                                  const int32_t* __restrict__ fr_all, int sort_after) {
+                                                  const int32_t* __restrict__ fr_all, int sort_after,
+                                                  int early_sort) {
   static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "lane width");
   constexpr int RB = 512 / G;  // rows per batch
   const int lane = threadIdx.x & 63;
@@ -764,8 +765,11 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       const u32 lb = lab[c];
       u64 act = __ballot(lb != kNone);
       u64 best = 0ull;
+      bool singles = false;  // the last round retired one vote in every group
       for (int round = 0; act; ++round) {
-        if (round == sort_after) {  // uniform: a label-dense chunk
+        // uniform: a label-dense chunk -- after sort_after rounds, or (early_sort) as soon
+        // as a round found no repeated label in any group
+        if (round == sort_after || (early_sort && singles)) {
           best = group_mode_sort<G>(lb, lane);
           break;
         }
@@ -775,6 +779,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
         const u64 mm = __ballot(((act >> lane) & 1ull) && lb == x);
         const u32 cn = (u32)__popcll((mm >> gbase) & gm);
         if (my) best = umax64(best, tally(cn, x));
+        singles = __ballot(my != 0ull && cn >= 2u) == 0ull;
         act &= ~mm;
         act &= ~decided_groups<G>(act, my, best, gbase, gm);
       }
@@ -1754,7 +1759,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
       hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
                          sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, \
-                         sort_after);                                                         \
+                         sort_after, g->early_sort);                                          \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
