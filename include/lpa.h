@@ -200,6 +200,9 @@ int lpa_run(lpa_graph* g, int32_t max_iter, int32_t* labels_out, int32_t out_is_
  *   incident[l]    distinct directed edges touching l  (Graphframes.py:107-118)
  *   sub_labels[v]  L2 only: second-level label         (Graphframes.py:121-128)
  *   flags[v]       1 = outlier                          (Graphframes.py:130-137)
+ * The first call on a handle builds its distinct directed edge set (topology) and a
+ * pinned host staging area of 25 bytes per vertex for the host copies; both are kept
+ * with the handle and released by lpa_graph_destroy.
  */
 int lpa_outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
                 int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
