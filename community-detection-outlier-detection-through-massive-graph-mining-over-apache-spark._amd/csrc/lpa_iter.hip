@@ -47,6 +47,7 @@
 #include <mutex>
 
 #include "lpa_internal.h"
+#include "lpa_lane.h"
 
 // LPA_TRACE (diagnostic build only): synchronise and log after every kernel
 #ifdef LPA_TRACE
@@ -357,31 +358,9 @@ __device__ __forceinline__ BinRows bin_rows(int64_t vbeg, int64_t vend, const in
   return br;
 }
 
-// v of lane ^ j for a compile-time j (every call is in a fully unrolled loop over a
-// full wave) without the LDS crossbar of ds_bpermute: DPP inside a 16-lane row (j = 1, 2
-// quad permutes; j = 8 one row rotation; j = 4 two rotations and a select), the gfx950
-// v_permlane16/32_swap across rows (j = 16, 32: each swap leaves one copy of the
-// partner row / half in one of its two results)
-__device__ __forceinline__ u32 lane_xor(u32 v, int j, int lane) {
-  if (j == 1) return dpp_u32<0xB1>(v);  // quad_perm [1,0,3,2]
-  if (j == 2) return dpp_u32<0x4E>(v);  // quad_perm [2,3,0,1]
-  if (j == 4) {
-    const u32 dn = dpp_u32<0x124>(v);  // row_ror:4  -> lane - 4
-    const u32 up = dpp_u32<0x12C>(v);  // row_ror:12 -> lane + 4
-    return (lane & 4) ? dn : up;
-  }
-  if (j == 8) return dpp_u32<0x128>(v);  // row_ror:8 -> lane ^ 8
-  if (j == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (lane & 16) ? (u32)r[0] : (u32)r[1];
-  }
-  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  return (lane & 32) ? (u32)r[0] : (u32)r[1];
-}
-
 // Mode of each G-lane group's labels (one label per lane, kNone = empty) by sorting:
 // a bitonic network across the group's lanes (log2 G (log2 G + 1) / 2 exchange
-// stages, each a lane_xor; a group's direction may come out descending, which leaves equal labels
+// stages, each a lane::lane_xor (lpa_lane.h); a group's direction may come out descending, which leaves equal labels
 // contiguous all the same), then run lengths from the ballot of run starts, then a
 // group max of the run tally words.  Every lane of a group returns its group's word.
 // The ballot peel costs one dependent round per distinct label; in the label-dense
@@ -394,14 +373,14 @@ __device__ __forceinline__ u64 group_mode_sort(u32 v, int lane) {
   for (int k = 2; k <= G; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      const u32 o = lane_xor(v, j, lane);
+      const u32 o = lane::lane_xor(v, j, lane);
       const bool up = (lane & k) == 0, low = (lane & j) == 0;
       v = (low == up) ? (v < o ? v : o) : (v > o ? v : o);
     }
   }
   const int gj = lane & (G - 1);
   const int gbase = lane - gj;
-  const u32 prev = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);  // wave_shr:1
+  const u32 prev = lane::lane_prev(v);
   const bool start = gj == 0 || v != prev;
   const u64 bm = __ballot(start);
   const u64 above = lane == 63 ? 0ull : (bm & ~((2ull << lane) - 1ull));
@@ -410,7 +389,7 @@ __device__ __forceinline__ u64 group_mode_sort(u32 v, int lane) {
   u64 w = (start && v != kNone) ? tally((u32)(nxt - lane), v) : 0ull;
 #pragma unroll
   for (int off = G >> 1; off > 0; off >>= 1) {
-    const u64 o = ((u64)lane_xor((u32)(w >> 32), off, lane) << 32) | (u64)lane_xor((u32)w, off, lane);
+    const u64 o = ((u64)lane::lane_xor((u32)(w >> 32), off, lane) << 32) | (u64)lane::lane_xor((u32)w, off, lane);
     w = umax64(w, o);
   }
   return w;
