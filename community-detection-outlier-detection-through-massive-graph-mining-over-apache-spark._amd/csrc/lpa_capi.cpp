@@ -168,6 +168,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_MID_MERGED")) g->mid_merged = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_DENSE_PEEL")) g->dense_peel = atoi(f) < 0 ? 0 : (atoi(f) > 8 ? 8 : atoi(f));
   if (const char* f = getenv("LPA_DENSE_SORT_AFTER")) g->dense_sort_after = atoi(f) < 0 ? 0 : (atoi(f) > 64 ? 64 : atoi(f));
+  if (const char* f = getenv("LPA_SORT_AFTER")) g->sort_after = atoi(f) < 0 ? 0 : (atoi(f) > 64 ? 64 : atoi(f));
   if (const char* f = getenv("LPA_BLOCK2")) g->block2 = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_HUB_FUSE")) g->hub_fuse = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FOLD_REBUILD")) g->fold_rebuild = atoi(f) ? 1 : 0;

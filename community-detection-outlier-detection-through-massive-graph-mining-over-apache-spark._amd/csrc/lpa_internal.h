@@ -161,6 +161,7 @@ struct lpa_graph {
   int dense_peel = 2;             // LPA_DENSE_PEEL: peel rounds of the tallies in the label-dense supersteps (2: measured
                                   // best of 0/2/4/8 at C3, superstep 2 5.82 -> 5.75 ms)
   int dense_sort_after = 0;       // LPA_DENSE_SORT_AFTER: row-bin peel rounds before the sort, label-dense supersteps
+  int sort_after = 3;             // LPA_SORT_AFTER: the same for the other supersteps' full tallies (kPeelSortAfter)
                                   // (0: measured best of 0/1/2/3 at C3, superstep 2 5.75 -> 5.62 ms)
   int block2 = 1;                 // LPA_BLOCK2=0: label-dense supersteps stage the rows of 4096 < deg <= 8192 by units
   int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches

@@ -1672,7 +1672,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // supersteps, where a round rarely retires more than a few votes)
   const int pmax = g->since_reset < kDenseSupersteps ? g->dense_peel : kPeelMax;
   // peel rounds of the row bins before a chunk is sorted (LPA_DENSE_SORT_AFTER)
-  const int sort_after = g->since_reset < kDenseSupersteps ? g->dense_sort_after : kPeelSortAfter;
+  const int sort_after = g->since_reset < kDenseSupersteps ? g->dense_sort_after : g->sort_after;
   // wide tier (rows 4096 < deg <= 8192: 16 waves, a 16K-slot table, one block per CU)
   auto launch_block_wide = [&](hipStream_t st) -> int {
     const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;

@@ -235,7 +235,8 @@ def test_schedules_identical(gfa, graph):
 
 @pytest.mark.parametrize("env", [{"LPA_BLOCK_STEPS": "3"}, {"LPA_BLOCK_STEPS": "0"}, {"LPA_BLOCK_AT": "3"},
                                  {"LPA_BLOCK_AT": "0"}, {"LPA_SERIAL": "1"}, {"LPA_FIRST_RUNS": "0"},
-                                 {"LPA_G64_WAVE": "1"}, {"LPA_EARLY_SORT": "1"}])
+                                 {"LPA_G64_WAVE": "1"}, {"LPA_EARLY_SORT": "1"},
+                                 {"LPA_SORT_AFTER": "1"}, {"LPA_SORT_AFTER": "0"}])
 def test_schedule_options_bit_exact(gfa, oracle, monkeypatch, env):
     """Schedule options read at graph creation (block-mode superstep count, where the
     block tiers run, the serialized profiling schedule): labels bit-exact per
