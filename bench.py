@@ -4,10 +4,15 @@
 
 Workloads (synthetic, generated in HBM; CSR construction not timed):
   C3  R-MAT scale 24, edgefactor 16 (16.7 M V / 268 M E)          default at N = 1
-  C4  R-MAT scale 26, edgefactor 16 (67 M V / 1.07 B E)            default at N > 1
-      (strong scaling: the same graph split over the N ranks)
+      N > 1 default: R-MAT scale 24 + log2 N (weak scaling, 268 M edges per GPU;
+      N = 4 is C4), every rank holding 1/N of the arcs
+  C4  R-MAT scale 26, edgefactor 16 (67 M V / 1.07 B E)            (--config C4, any N)
   C5  Chung-Lu gamma 2.1, 40 M V / 1.4 B E, max degree ~1.25 M (--config C5)
   C2  planted-partition SBM, 1 M V / 20 M E, 100 blocks            (--config C2)
+  A --config at N > 1 is strong scaling (the same graph split over the N ranks).
+
+--gpus N > 1 without a torch.distributed environment re-launches this script under
+torch.distributed.run (one rank per GPU) as a child process, before any GPU call.
 All run labelPropagation(maxIter=10) semantics (Graphframes.py:81).
 
 A "step" is ONE labelPropagation(maxIter=10) call as a user makes it, timed over
@@ -25,7 +30,9 @@ whole lpa_run(10) from reset (`run_maxiter10_ms`, supersteps 1..10 + label gathe
 the per-kernel breakdown of a serialized pass (`roofline` of the dominant kernel),
 `moved_bytes_frac` (bytes the replicated-label formulation actually moves in a
 converged superstep), the outlier stage (`outlier_l1_ms`, `outlier_l2_ms`) and the
-CPU baseline (OpenMP oracle on this host) at N = 1.
+CPU baseline (OpenMP oracle on this host) at N = 1, and `quality`: community count
+and modularity of the GPU labels for C1 (the reference's sample graph, maxIter=5),
+the bench graph and C2 (plus C2's NMI against its planted blocks).
 """
 import argparse
 import json
@@ -151,6 +158,91 @@ def cpu_baseline(src_np, dst_np, V, gpu_graph, budget_s=25.0):
                 parity_vs_gpu=ok)
 
 
+def self_launch(n):
+    """Run this script under torch.distributed.run with n ranks (one per GPU) as a
+    child process; returns its exit code.  Called before torch is imported."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def modularity(src, dst, lab):
+    """Newman modularity of the partition `lab` (device int32 labels, values in
+    [0, V)) on the symmetrised multigraph LPA votes on: every input edge is two arcs
+    (a self-loop two arcs at its vertex), Q = intra arcs / A - sum_c (D_c / A)^2."""
+    import torch
+
+    A = 2 * src.numel()
+    if A == 0:
+        return 0.0
+    V = lab.numel()
+    intra = 0
+    step = 1 << 27
+    for i in range(0, src.numel(), step):   # bounded temporaries
+        s, d = src[i:i + step].long(), dst[i:i + step].long()
+        intra += 2 * int((lab[s] == lab[d]).sum().item())
+    deg = torch.bincount(src.long(), minlength=V) + torch.bincount(dst.long(), minlength=V)
+    D = torch.zeros(V, dtype=torch.float64, device=lab.device)
+    D.index_add_(0, lab.long(), deg.double())
+    return intra / A - float(((D / A) ** 2).sum().item())
+
+
+def quality_entry(src, dst, lab, extra=None):
+    import torch
+
+    V = lab.numel()
+    present = torch.bincount(lab.long(), minlength=V) > 0
+    q = dict(communities=int(present.sum().item()), modularity=round(modularity(src, dst, lab), 6))
+    if extra:
+        q.update(extra)
+    return q
+
+
+def quality_report(gfa, device, bench_entry):
+    """C1 (the reference's sample graph, maxIter=5 as Graphframes.py:81), the bench
+    graph (maxIter=10) and C2 (maxIter=10, NMI vs the planted blocks): community
+    count + modularity of the GPU labels."""
+    import numpy as np
+    import torch
+
+    rep = {"agreement_note": "GraphFrames/GraphX itself cannot run here (no JVM, no pyspark): agreement "
+                             "with its own output is unpinned; labels are bit-exact vs the oracle's "
+                             "smallest-label tie-break (tests/)",
+           "bench_graph": bench_entry}
+    z = np.load(os.path.join(ROOT, "tests", "golden", "r9_golden.npz"), allow_pickle=False)
+    dev = torch.device("cuda", device)
+    s1 = torch.from_numpy(z["src"].astype(np.int32)).to(dev)
+    d1 = torch.from_numpy(z["dst"].astype(np.int32)).to(dev)
+    V1 = int(z["ids"].size)
+    with gfa.Graph(z["src"], z["dst"], V1, device=device) as g1:
+        out = torch.empty(V1, dtype=torch.int32, device=dev)
+        g1.run(5, out=out)
+    rep["C1"] = quality_entry(s1, d1, out, dict(max_iter=5, vertices=V1, edges=int(s1.numel())))
+    c2 = CONFIGS["C2"]
+    s2, d2 = gfa.gen_sbm(c2["V"], c2["blocks"], c2["m"], seed=c2["seed"], device=device)
+    with gfa.Graph(s2, d2, c2["V"], device=device) as g2:
+        out = torch.empty(c2["V"], dtype=torch.int32, device=dev)
+        g2.run(MAX_ITER, out=out)
+    extra = dict(max_iter=MAX_ITER)
+    try:
+        from sklearn.metrics import normalized_mutual_info_score as nmi
+        truth = np.minimum(np.arange(c2["V"]) // (c2["V"] // c2["blocks"]), c2["blocks"] - 1)
+        extra["nmi_vs_planted_blocks"] = round(float(nmi(truth, out.cpu().numpy())), 4)
+    except ImportError:
+        extra["nmi_vs_planted_blocks"] = None
+    rep["C2"] = quality_entry(s2, d2, out, extra)
+    del s2, d2
+    return rep
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,22 +253,35 @@ def main():
     ap.add_argument("--scale", type=int, default=None, help="R-MAT scale override (custom config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-outlier", action="store_true")
+    ap.add_argument("--no-quality", action="store_true", help="skip the community count / modularity report")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)  # tests: ranks + config only
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the driver's `bench.py --gpus N`: one rank process per GPU, started here
+        # before anything touches the GPU (a child process, never an exec)
+        sys.exit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-        args.gpus = world
-    config_id = args.config or ("C3" if world == 1 else "C4")
+    args.gpus = world
+    scaling = "strong"
+    if args.config is None and args.scale is None and world > 1:
+        # weak scaling from C3: 2^24 * N vertices, 268 M edges per GPU (N = 4: C4)
+        lg = world.bit_length() - 1
+        args.scale = 24 + lg
+        scaling = "weak"
+    config_id = args.config or "C3"
     cfg = dict(CONFIGS[config_id])
     if args.scale is not None:
         if cfg["kind"] != "rmat":
             raise SystemExit("--scale applies to the R-MAT configs")
         cfg["scale"] = args.scale
         config_id = {24: "C3", 26: "C4"}.get(args.scale, f"R-MAT-{args.scale}")
+    if args.launch_check:   # no GPU: what each rank would run (tests/test_bench_launch.py)
+        print(json.dumps(dict(rank=rank, world=world, local_rank=local_rank, config_id=config_id,
+                              scaling=scaling, cfg=cfg)), flush=True)
+        return
 
     import numpy as np
     import torch
@@ -214,7 +319,9 @@ def main():
     keep_host = world == 1 and not args.no_cpu_baseline
     if keep_host:
         src_np, dst_np = src.cpu().numpy(), dst.cpu().numpy()
-    del src, dst
+    if rank != 0 or args.no_quality:
+        del src, dst     # rank 0 keeps the edge list for the modularity report
+        src = dst = None
     torch.cuda.empty_cache()
 
     g.step(1)          # prime: code objects loaded, caches warm
@@ -272,6 +379,12 @@ def main():
         barrier()
         run_ms.append((time.perf_counter() - t0) * 1e3)
     run_ms = max_over_ranks(statistics.median(run_ms))
+    # partition quality of the labels of that call (rank 0: the full dense vector)
+    quality = None
+    if rank == 0 and not args.no_quality:
+        quality = dict(bench_graph=quality_entry(src, dst, out, dict(max_iter=MAX_ITER, config_id=config_id)))
+        del src, dst
+        torch.cuda.empty_cache()
 
     # ---- breakdown: supersteps 2..10 again with the tally kernels serialized on one
     # stream and HIP events around every kernel (standalone durations: the roofline
@@ -316,7 +429,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(t_sum * 1e3 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
@@ -326,6 +439,8 @@ def main():
             "config_id": config_id,
             "vertices": V, "edges": m, "arcs_rank0": info["arcs"],
             "parallelism": f"1D degree-ranked vertex partition x{world}, RCCL label allgather",
+            "scaling_note": ("weak: R-MAT scale 24 + log2 N, 268 M edges per GPU" if scaling == "weak" else
+                             "the same graph at every N"),
         },
         "timed_window": f"supersteps 2..{MAX_ITER} of each of {args.steps} labelPropagation(maxIter={MAX_ITER}) "
                         f"calls ({n_timed} supersteps); step = one call",
@@ -404,6 +519,8 @@ def main():
                                     "by its first outlier call and kept (outlier_l1_first_ms includes it)")
     if keep_host and rank == 0:
         out_json["cpu_baseline"] = cpu_baseline(src_np, dst_np, V, g)
+    if quality is not None:
+        out_json["quality"] = quality_report(gfa, device, quality["bench_graph"])
     if rank == 0:
         print(json.dumps(out_json), flush=True)
     g.close()

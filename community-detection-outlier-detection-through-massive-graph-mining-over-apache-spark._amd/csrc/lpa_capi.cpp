@@ -85,7 +85,8 @@ void destroy(lpa_graph* g) {
                   g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
-                  g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best};
+                  g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best,
+                  g->gbits};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
@@ -157,27 +158,12 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
     return LPA_ENOMEM;
   }
   g->device = device;
-  if (const char* f = getenv("LPA_REBUILD_FRAC")) g->rebuild_frac = atof(f);
   if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
   if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
   if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
-  if (const char* f = getenv("LPA_HUB_WAVES")) g->hub_waves = atoi(f) == 4 ? 4 : 8;
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_FRONTIER_FRAC")) g->frontier_frac = atof(f);
-  if (const char* f = getenv("LPA_MID_MERGED")) g->mid_merged = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_DENSE_PEEL")) g->dense_peel = atoi(f) < 0 ? 0 : (atoi(f) > 8 ? 8 : atoi(f));
-  if (const char* f = getenv("LPA_DENSE_SORT_AFTER")) g->dense_sort_after = atoi(f) < 0 ? 0 : (atoi(f) > 64 ? 64 : atoi(f));
-  if (const char* f = getenv("LPA_SORT_AFTER")) g->sort_after = atoi(f) < 0 ? 0 : (atoi(f) > 64 ? 64 : atoi(f));
-  if (const char* f = getenv("LPA_BLOCK2")) g->block2 = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_HUB_FUSE")) g->hub_fuse = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_FOLD_REBUILD")) g->fold_rebuild = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_BLOCK")) g->block_rows = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_EARLY_SORT")) g->early_sort = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_G64_WAVE")) g->g64_wave = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
-  if (const char* f = getenv("LPA_BLOCK_STEPS")) g->block_steps = atoi(f) < 0 ? 0 : (atoi(f) > 8 ? 8 : atoi(f));
-  if (const char* f = getenv("LPA_BLOCK_AT")) g->block_at = atoi(f) < 0 ? 0 : (atoi(f) > 4 ? 4 : atoi(f));
   // internal builds (the outlier stage's L2 sub-graph): the locality order is a
   // gather-locality heuristic worth its two atomic passes only on a graph that runs
   // many supersteps; labels do not depend on the vertex order
@@ -226,7 +212,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
       destroy(g);
       return rc;
     }
-  } else if (nranks > 1 && comm_id) {
+  } else if (comm_id) {
     ncclUniqueId id;
     memcpy(&id, comm_id, sizeof(id));
     ncclResult_t r = ncclCommInitRank(&g->comm, nranks, id, rank);

@@ -35,6 +35,9 @@ struct Loopback {
   std::vector<const void*> send;    // published send buffers (current collective)
   std::vector<size_t> bytes;        // published bytes per rank (must agree)
   int timeout_s = 300;
+  int attached = 0;                 // handles attached (rank_g non-null)
+  bool destroy_pending = false;     // lpa_loopback_destroy while handles were attached:
+                                    // the last detach frees the group
 
   // returns false on abort / timeout (the group is then poisoned: every later
   // collective fails fast instead of hanging the other ranks' threads)
@@ -78,7 +81,12 @@ int loopback_attach(lpa_graph* g, Loopback* lb) {
     return LPA_EINVAL;
   }
   for (auto& e : g->loop_ev) LPA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (lb->destroy_pending) {
+    set_error("loopback group is being destroyed");
+    return LPA_EINVAL;
+  }
   lb->rank_g[g->rank] = g;
+  ++lb->attached;
   g->loop = lb;
   return LPA_OK;
 }
@@ -86,13 +94,19 @@ int loopback_attach(lpa_graph* g, Loopback* lb) {
 void loopback_detach(lpa_graph* g) {
   Loopback* lb = g->loop;
   if (!lb) return;
+  bool last = false;
   {
     std::lock_guard<std::mutex> lk(lb->mu);
-    if (lb->rank_g[g->rank] == g) lb->rank_g[g->rank] = nullptr;
+    if (lb->rank_g[g->rank] == g) {
+      lb->rank_g[g->rank] = nullptr;
+      --lb->attached;
+    }
+    last = lb->destroy_pending && lb->attached == 0;
   }
   for (auto& e : g->loop_ev)
     if (e) (void)hipEventDestroy(e);
   g->loop = nullptr;
+  if (last) delete lb;  // the group was destroyed while this handle was attached
 }
 
 namespace {
@@ -181,6 +195,22 @@ void lpa_loopback_abort(lpa_loopback* group) {
   if (group) reinterpret_cast<Loopback*>(group)->abort();
 }
 
-void lpa_loopback_destroy(lpa_loopback* group) { delete reinterpret_cast<Loopback*>(group); }
+// A group destroyed while handles are still attached is poisoned (their collectives
+// fail fast) and freed by the last handle's detach (lpa_graph_destroy), so a handle
+// never locks a freed group.
+void lpa_loopback_destroy(lpa_loopback* group) {
+  Loopback* lb = reinterpret_cast<Loopback*>(group);
+  if (!lb) return;
+  {
+    std::lock_guard<std::mutex> lk(lb->mu);
+    if (lb->attached > 0) {
+      lb->destroy_pending = true;
+      lb->aborted = true;
+      lb->cv.notify_all();
+      return;
+    }
+  }
+  delete lb;
+}
 
 }  // extern "C"

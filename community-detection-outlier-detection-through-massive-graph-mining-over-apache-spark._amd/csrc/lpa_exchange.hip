@@ -140,7 +140,7 @@ inline unsigned grid_of(int64_t n, int64_t cap) {
 }  // namespace
 
 int exchange_alloc(lpa_graph* g) {
-  if (g->nranks <= 1) return LPA_OK;
+  if (!exchanges(g)) return LPA_OK;
   g->dcap = g->slice / 4;
   if (g->dcap < 1) g->dcap = 1;
   const int64_t P = g->nranks;

@@ -728,6 +728,12 @@ __global__ __launch_bounds__(64 * kW) void k_hub_mid_all(const int32_t* __restri
 // back / invalidate the whole L2 of the XCD, and 2048 blocks doing so cost ~90 us.
 // Tickets are two-level (kTicketGroups counters, one 64-B line each, then one for the
 // groups): returning atomics on ONE address serialise at ~88 M/s, 2048 of them ~23 us.
+// This hand-off leans on gfx950 behaviour the HIP memory model does not promise (device
+// atomics on hipMalloc memory complete at the memory side once vmcnt drains; agent-scope
+// relaxed loads read past the XCD's L2), so the library is built for gfx950 only:
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "lpa_hub.hip: the fused last-block hand-off is validated on gfx950 only"
+#endif
 constexpr int kTicketGroups = 16;
 constexpr int kTicketStride = 16;  // uint32 per ticket line
 constexpr int kTicketWords = (kTicketGroups + 1) * kTicketStride;
@@ -1129,22 +1135,17 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join) {
   const int64_t hc = block_mode_now(g) ? block_rows_begin(g) : hl;
   // fork (label-dense supersteps): classify the > 8-unit rows first and start the
   // bucket path on its own stream; the mid tiers follow k_hub_small on the main
-  // stream.  Otherwise everything runs in order on the main stream.
-  // (the fourth stream runs k_lpa_block when block_at == 2: the bucket path then
-  // follows the row bins on the third)
-  // (block_at == 3: the fourth stream runs the wide block tier, the third the narrow
-  // one after the row bins: the bucket path follows the wave bins on the second)
+  // stream.  Otherwise everything runs in order on the main stream.  In block mode the
+  // fourth stream runs the wide block tier, so the bucket path follows the wave bins
+  // on the second.
   const bool bm = block_mode_now(g) && !g->serial;
-  hipStream_t sd = !fork                         ? s
-                   : (bm && g->block_at == 2) ? g->aux_stream[1]
-                   : (bm && g->block_at >= 3) ? g->aux_stream[0]
-                                              : g->aux_stream[2];
+  hipStream_t sd = !fork ? s : bm ? g->aux_stream[0] : g->aux_stream[2];
   const unsigned ncl = grid_cap(g->n_hub_chunks, 2048);
   // fused (converged supersteps, few bucketed rows): the scan by the last block of
   // k_hub_count, the final pass by the last block of k_hub_bucket -- 5 dependent
   // launches -> 3; the label-dense supersteps, with ~10^2 bucketed rows of up to 4K
   // buckets each, keep the parallel k_hub_scan / k_hub_final
-  const bool fuse = g->hub_fuse && !fork;
+  const bool fuse = !fork;
   uint32_t* tickets = g->hub_tickets;
   int32_t* lcnt_next = g->hub_lcnt + 8 * (g->par ^ 1);
   auto bucket_path = [&]() -> int {
@@ -1164,12 +1165,7 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join) {
     LPA_HIP(hipGetLastError());
     uint32_t* tb = fuse ? tickets + kTicketWords : (uint32_t*)nullptr;
     const unsigned nbk = grid_cap(g->n_hub_buckets, fuse ? 512 : 2048);
-    if (g->hub_waves == 4)
-      hipLaunchKernelGGL(k_hub_bucket<4>, dim3(nbk), dim3(256), 0, sd,
-                         g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
-                         g->hub_best, g->dev_err, tb, listC, g->hub_wcount, g->ghist, Lown, lcnt_next);
-    else
-      hipLaunchKernelGGL(k_hub_bucket<8>, dim3(nbk), dim3(512), 0, sd,
+    hipLaunchKernelGGL(k_hub_bucket<8>, dim3(nbk), dim3(512), 0, sd,
                          g->items_cb, lcnt, g->rp, g->scat, g->hub_hoff, g->ghist, g->gcur,
                          g->hub_best, g->dev_err, tb, listC, g->hub_wcount, g->ghist, Lown, lcnt_next);
     LPA_HIP(hipGetLastError());
@@ -1208,17 +1204,12 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join) {
   // one launch in the converged supersteps (few queued rows: saves two dependent
   // launches); the label-dense ones keep the per-tier launches (the 4-wave blocks of
   // the small tiers measured faster there: 5.95 vs 6.2 ms at C3 superstep 2)
-  if (g->mid_merged && !fork) {
+  if (!fork) {
     hipLaunchKernelGGL((k_hub_mid_all<8>), dim3(grid_cap(n, 1024)), dim3(512), 0, s, lists, n, lcnt,
                        g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, g->dev_err);
     LPA_HIP(hipGetLastError());
   } else {
-    if (g->hub_waves == 4)
-      hipLaunchKernelGGL((k_hub_mid<13, 4>), dim3(grid_cap(n, 512)), dim3(256), 0, s, lists + 4 * n,
-                         lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
-                         g->dev_err);
-    else
-      hipLaunchKernelGGL((k_hub_mid<13, 8>), dim3(grid_cap(n, 512)), dim3(512), 0, s, lists + 4 * n,
+    hipLaunchKernelGGL((k_hub_mid<13, 8>), dim3(grid_cap(n, 512)), dim3(512), 0, s, lists + 4 * n,
                          lcnt, 6, g->rp, g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown,
                          g->dev_err);
     LPA_HIP(hipGetLastError());

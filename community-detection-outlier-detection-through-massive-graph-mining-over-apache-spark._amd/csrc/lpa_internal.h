@@ -53,7 +53,9 @@ constexpr int kChunkPos = 256;        // arc positions per scatter chunk of a ch
 // replicated-label refresh: scatter the changed vertices' labels while they touch at
 // most this fraction of the arcs, otherwise rebuild al[] with one gather pass
 constexpr double kRebuildFrac = 0.25;
-constexpr double kFrontierFrac = 0.005;  // default of lpa_graph::frontier_frac
+// the al[] scatter marks dirty rows while <= this fraction of the arcs changed; above
+// it the next superstep tallies every row
+constexpr double kFrontierFrac = 0.005;
 
 struct Segment {   // one unit of a seg-bin row
   int64_t begin;  // first arc (local CSR index)
@@ -157,27 +159,9 @@ struct lpa_graph {
                                   //   chunk items, wave path, mid2, mid3, small (list S)
   int64_t hub_lane_begin = 0;     // rows [hub_lane_begin, n_hub) have <= 8 units
   int64_t hub_block2_begin = 0;   // rows [hub_block2_begin, hub_lane_begin) have <= 16 units (wide block tier)
-  int block_rows = 1;             // LPA_BLOCK=0: label-dense supersteps also stage the rows above by units
-  int dense_peel = 2;             // LPA_DENSE_PEEL: peel rounds of the tallies in the label-dense supersteps (2: measured
-                                  // best of 0/2/4/8 at C3, superstep 2 5.82 -> 5.75 ms)
-  int dense_sort_after = 0;       // LPA_DENSE_SORT_AFTER: row-bin peel rounds before the sort, label-dense supersteps
-  int sort_after = 3;             // LPA_SORT_AFTER: the same for the other supersteps' full tallies (kPeelSortAfter)
-                                  // (0: measured best of 0/1/2/3 at C3, superstep 2 5.75 -> 5.62 ms)
-  int block2 = 1;                 // LPA_BLOCK2=0: label-dense supersteps stage the rows of 4096 < deg <= 8192 by units
-  int hub_fuse = 1;               // LPA_HUB_FUSE=0: converged supersteps keep k_hub_scan / k_hub_final launches
-  int fold_rebuild = 1;           // LPA_FOLD_REBUILD=0: captured converged supersteps keep the rebuild launch
-  int block_steps = 2;            // LPA_BLOCK_STEPS: supersteps after L0 in block mode (k_lpa_block rows)
-  int early_sort = 0;             // LPA_EARLY_SORT=1: row bins sort a chunk once a peel round finds no repeat
-  int g64_wave = 0;               // LPA_G64_WAVE=1: rows of 32 < deg <= 64 by the wave-hash kernel
   int first_runs = 1;             // LPA_FIRST_RUNS=0: superstep 1 by the hash tallies, not column runs
   bool cols_sorted = true;        // columns ascending inside each row (false: row-only sorted build)
   lpa::u64* first_best = nullptr; // [slice] superstep-1 best run word of rows spanning run tiles
-  int block_at = 4;               // LPA_BLOCK_AT: k_lpa_block before (0) / after (1) k_lpa_units on the
-                                  // main stream, or (2) on the fourth stream, concurrent with them,
-                                  // or (3) split: the wide tier on the fourth stream, the 8-wave
-                                  // tier after the row bins, the bucket path after the wave bins, or (4) as 3
-                                  // with the narrow tier on the main stream after the hub mid tiers
-                                  // (4: C3 293.8-295.4 -> 299.3-303.1 GTEPS over 0, same-box A/B)
   int64_t unit_lane_begin = 0;    // hub_uoff[hub_lane_begin]
   int64_t unit_block2_begin = 0;  // hub_uoff[hub_block2_begin]
   bool force_all_next = false;    // the next superstep tallies every row (after block mode)
@@ -203,13 +187,11 @@ struct lpa_graph {
   int32_t* ulist = nullptr;       // [n_segs] dirty hub units of this superstep
   int32_t* fcnt = nullptr;        // [2][16] per parity: list lengths (bins 0..12, units at 13)
   int frontier = 1;               // LPA_FRONTIER / lpa_set_frontier
-  // the al[] scatter marks dirty rows while <= this fraction of the arcs changed;
-  // above it the next superstep tallies every row (LPA_FRONTIER_FRAC overrides)
-  double frontier_frac = lpa::kFrontierFrac;
 
   // replicated neighbour labels (GraphX ReplicatedVertexView analogue):
   // al[i] = L_cur[col[i]]; kept current by scatter (few changes) or rebuild
   int32_t* al = nullptr;        // [arcs]
+  uint32_t* gbits = nullptr;    // [vpad / 32] rebuild: bit u = (L[u] == L[0]), the giant label
   int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
   uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])
   // per-superstep change bookkeeping (device)
@@ -221,14 +203,11 @@ struct lpa_graph {
   uint8_t* chflag = nullptr;    // [n_chunks, padded to 16] changed multi-chunk columns' flags
   int64_t n_chunk_scan = 0;     // chunks below this belong to every multi-chunk column
   int32_t* chlist = nullptr;    // [vpad] changed one-chunk columns (count: counters[par][0])
-  double rebuild_frac = lpa::kRebuildFrac;  // LPA_REBUILD_FRAC overrides (tuning experiments)
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   hipGraphExec_t gexec[4] = {};             // captured converged superstep per (cur, par)
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
-  int mid_merged = 1;                       // LPA_MID_MERGED=0: the three mid tiers as separate launches
-  int hub_waves = 8;                        // LPA_HUB_WAVES: waves per block of the 8K-slot hub combine (4 or 8)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
@@ -306,6 +285,10 @@ int gather_labels(lpa_graph* g, int32_t* out_dense_dev);
 // per rank in rank order (in place when send == recv + rank * count * elem),
 // stream-ordered on s, on the handle's RCCL communicator or loopback group
 inline bool has_collective(const lpa_graph* g) { return g->comm != nullptr || g->loop != nullptr; }
+// the superstep has a label-exchange step: P > 1, or an RCCL communicator at any P (a
+// one-rank job of the distributed path runs the same exchange code, ncclAllGather of
+// one rank included)
+inline bool exchanges(const lpa_graph* g) { return g->nranks > 1 || g->comm != nullptr; }
 int coll_allgather(lpa_graph* g, const void* send, void* recv, size_t count, int elem, hipStream_t s);
 int loopback_attach(lpa_graph* g, Loopback* lb);  // registers the handle's rank slot
 int loopback_ranks(const Loopback* lb);

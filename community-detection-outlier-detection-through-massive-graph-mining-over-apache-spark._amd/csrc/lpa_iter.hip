@@ -73,19 +73,21 @@ namespace {
 #define LPA_DIAG 0
 #endif
 
-// supersteps after L0 whose hub combine runs forked over two streams (see
-// launch_hub_combine)
+// supersteps after L0 that are label-dense: their hub combine runs forked over two
+// streams (launch_hub_combine) and the hub rows of <= kBlockMaxDeg2 arcs are tallied by
+// k_lpa_block (block mode)
 constexpr int kDenseSupersteps = 2;
+// peel rounds of the wave / unit / block tallies in the label-dense supersteps, where a
+// round rarely retires more than a few votes (measured best of 0/2/4/8 at C3)
+constexpr int kDensePeel = 2;
 
 }  // namespace
 
 // the label-dense supersteps tally the rows [hub_lane_begin, n_hub) with k_lpa_block
 // and skip their units; the superstep after them tallies every row (their units'
 // staged words are stale)
-bool block_mode_now(const lpa_graph* g) {
-  return g->block_rows && g->since_reset < g->block_steps && g->hub_lane_begin < g->n_hub;
-}
-int64_t block_rows_begin(const lpa_graph* g) { return g->block2 ? g->hub_block2_begin : g->hub_lane_begin; }
+bool block_mode_now(const lpa_graph* g) { return g->since_reset < kDenseSupersteps && g->hub_lane_begin < g->n_hub; }
+int64_t block_rows_begin(const lpa_graph* g) { return g->hub_block2_begin; }
 
 namespace {
 
@@ -719,8 +721,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend, const int32_t* __restrict__ flist,
                                                   const int32_t* __restrict__ fcnt_b,
-                                                  const int32_t* __restrict__ fr_all, int sort_after,
-                                                  int early_sort) {
+                                                  const int32_t* __restrict__ fr_all, int sort_after) {
   static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "lane width");
   constexpr int RB = 512 / G;  // rows per batch
   const int lane = threadIdx.x & 63;
@@ -765,11 +766,9 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       const u32 lb = lab[c];
       u64 act = __ballot(lb != kNone);
       u64 best = 0ull;
-      bool singles = false;  // the last round retired one vote in every group
       for (int round = 0; act; ++round) {
-        // uniform: a label-dense chunk -- after sort_after rounds, or (early_sort) as soon
-        // as a round found no repeated label in any group
-        if (round == sort_after || (early_sort && singles)) {
+        // uniform: a label-dense chunk after sort_after rounds
+        if (round == sort_after) {
           best = group_mode_sort<G>(lb, lane);
           break;
         }
@@ -779,7 +778,6 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
         const u64 mm = __ballot(((act >> lane) & 1ull) && lb == x);
         const u32 cn = (u32)__popcll((mm >> gbase) & gm);
         if (my) best = umax64(best, tally(cn, x));
-        singles = __ballot(my != 0ull && cn >= 2u) == 0ull;
         act &= ~mm;
         act &= ~decided_groups<G>(act, my, best, gbase, gm);
       }
@@ -812,6 +810,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
 // are unchanged since, so they are still exact)
 struct UnitIds {
   int64_t n;
+  int64_t lim;          // units >= lim are not this launch's (block-tier rows in block mode)
   const int32_t* list;  // nullptr: every unit
   __device__ __forceinline__ int64_t id(int64_t i) const { return list ? (int64_t)list[i] : i; }
 };
@@ -821,7 +820,10 @@ __device__ __forceinline__ Segment load_unit(const Segment* __restrict__ units, 
   d.begin = 0;
   d.len = 0;
   d.v = 0;
-  if (i < ui.n) d = units[ui.id(i)];
+  if (i < ui.n) {
+    const int64_t id = ui.id(i);
+    if (id < ui.lim) d = units[id];  // a listed unit of a block-tier row: len 0, skipped
+  }
   return d;
 }
 
@@ -897,6 +899,7 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
   // register with a load in flight would wait for it): labels two units ahead
   UnitIds ui;
   ui.n = *fr_all ? nunits : (int64_t)*fcnt_u;
+  ui.lim = nunits;
   ui.list = *fr_all ? nullptr : ulist;
   if (u >= ui.n) return;
   // the wave's table is cleared only by waves with work (a frontier superstep lists
@@ -1410,36 +1413,107 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
   rebuild_all(col, arcs, Ln, al);
 }
 
-// Same with the labels of the kHotLabels highest-degree vertices (slots
-// [0, kHotLabels) at P = 1: 30-40 % of all arc targets on R-MAT) served from LDS:
-// the rebuild is bound by the L2 request rate of its 4-B random gathers, and every
-// gather served by the block's LDS copy is one L2 request fewer.  One 1024-thread
-// block per CU, 128 KB of LDS.
-constexpr int kHotLabels = 32768;          // rank-strided set (P > 1: power-of-two shares)
-constexpr int kHotLabelsSingle = 40960;    // P = 1: the whole 160 KB of LDS
+// Giant-label bitmap of L (before a rebuild): bit u = (L[u] == G), G = L[0], the label
+// of the highest-degree vertex.  Once the labels concentrate (R-MAT, after superstep
+// 2: ~98.5 % of the arcs point at a column labelled G) the rebuild gathers one BIT per
+// arc -- the hot slots' bits from LDS, the rest from this 1-bit-per-slot array, which
+// stays in L2 (2 MB at C3 against the 64 MB label vector) -- and reads the label
+// vector only for the columns whose bit is clear.  One ballot per 64 slots; lanes
+// 0..7 store the wave's eight 64-bit words (64 contiguous bytes).
+template <bool kIfWanted>
+__global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __restrict__ counters, int64_t thr,
+                                                    const int32_t* __restrict__ L, int64_t n,
+                                                    unsigned long long* __restrict__ bits) {
+  if (kIfWanted && !rebuild_wanted(counters, thr)) return;
+  const int32_t G = L[0];
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t g0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 512; g0 < n; g0 += nw * 512) {
+    int32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = g0 + k * 64 + lane;
+      v[k] = i < n ? (int32_t)ld_stream(L + i) : ~G;
+    }
+    unsigned long long mine = 0ull;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const unsigned long long m = __ballot(v[k] == G);
+      if (lane == k) mine = m;
+    }
+    if (lane < 8 && g0 + lane * 64 < n) bits[(g0 >> 6) + lane] = mine;
+  }
+}
+
+// al[] rebuild with an LDS hot set (the slots of the highest-degree vertices: at P = 1
+// the first slots, 30-40 % of all arc targets on R-MAT).  The rebuild is bound by the
+// line traffic of its L2-missing 4-B gathers, and every gather served from LDS is one
+// L2 request fewer.  One 1024-thread block per CU, 160 KB of LDS, in one of two modes
+// that every block picks alike from the same data:
+//   bits    (most hot slots carry the giant label G): LDS holds the giant-label bits of
+//           the first 1.31 M slots, the other columns' bits come from gbits (L2); a
+//           set bit is G, a clear one reads L[c].
+//   labels  LDS holds the labels of the first 40,960 slots; the rest read L[c].
 // kRanked (P > 1, power-of-two slices and rank count): the hottest vertices of rank
 // r's slice are its first slots (degree rank k lives at slot (k mod P) S + k / P),
-// so the global top kHotLabels are the first H = kHotLabels / P slots of every
-// slice: slot c is hot iff (c mod S) < H, at LDS index (c / S) H + c mod S.
+// so the global top set is the first H slots of every slice: slot c is hot iff
+// (c mod S) < H, at LDS index (c / S) H + c mod S (H = 2^hot_lg labels or 2^hb_lg bits).
+constexpr int kHotLabels = 32768;          // rank-strided label set (P > 1: power-of-two shares)
+constexpr int kHotLabelsSingle = 40960;    // P = 1: the whole 160 KB of LDS
+// bits mode: 1,310,688 slots' bits (the last LDS word counts the set bits first)
+constexpr int64_t kHotBits = 32ll * (kHotLabelsSingle - 1);
 template <bool kIfWanted, bool kRanked>
 __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long long* __restrict__ counters,
                                                          int64_t thr, const int32_t* __restrict__ col,
                                                          int64_t arcs, const int32_t* __restrict__ Ln,
                                                          int32_t nhot, int32_t* __restrict__ al,
-                                                         int slice_lg, int hot_lg) {
+                                                         int slice_lg, int hot_lg, int hb_lg,
+                                                         const uint32_t* __restrict__ gbits, int64_t nbits) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
-  __shared__ int32_t hot[kHotLabelsSingle];
-  for (int i = threadIdx.x; i < nhot; i += 1024)
-    hot[i] = kRanked ? Ln[((int64_t)(i >> hot_lg) << slice_lg) + (i & ((1 << hot_lg) - 1))] : Ln[i];
+  __shared__ u32 hot[kHotLabelsSingle];
+  u32* s_cnt = &hot[kHotLabelsSingle - 1];   // beyond the bit words; labels mode refills it
+  // ---- the giant-label bits of the hot slots, and how many are set ----
+  const int64_t nhb = kRanked ? ((int64_t)(nbits >> slice_lg) << hb_lg) : (nbits < kHotBits ? nbits : kHotBits);
+  const int nhw = (int)((nhb + 31) >> 5);
+  if (threadIdx.x == 0) *s_cnt = 0u;
   __syncthreads();
+  int cnt = 0;
+  for (int q = threadIdx.x; q < nhw; q += 1024) {
+    int64_t gw = q;
+    if constexpr (kRanked) gw = ((int64_t)(q >> (hb_lg - 5)) << (slice_lg - 5)) + (q & ((1 << (hb_lg - 5)) - 1));
+    const u32 w = gbits[gw];
+    hot[q] = w;
+    cnt += __popc(w);
+  }
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(s_cnt, (u32)cnt);
+  __syncthreads();
+  const bool bits = 2 * (int64_t)*s_cnt >= nhb && nhb > 0;  // uniform: the same data in every block
+  const int32_t G = Ln[0];
+  if (!bits) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nhot; i += 1024)
+      hot[i] = (u32)(kRanked ? Ln[((int64_t)(i >> hot_lg) << slice_lg) + (i & ((1 << hot_lg) - 1))] : Ln[i]);
+    __syncthreads();
+  }
   const u32 nh = (u32)nhot;
-  const u32 smask = kRanked ? (1u << slice_lg) - 1u : 0u, hcap = 1u << hot_lg;
+  const u32 smask = kRanked ? (1u << slice_lg) - 1u : 0u, hcap = 1u << hot_lg, bcap = 1u << hb_lg;
   auto lab = [&](int c) -> int32_t {
+    if (bits) {
+      u32 w;
+      if constexpr (kRanked) {
+        const u32 j = (u32)c & smask;
+        w = j < bcap ? hot[((((u32)c >> slice_lg) << hb_lg) + j) >> 5] : gbits[(u32)c >> 5];
+      } else {
+        w = (u32)c < (u32)nhb ? hot[(u32)c >> 5] : gbits[(u32)c >> 5];
+      }
+      return ((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c];
+    }
     if constexpr (kRanked) {
       const u32 j = (u32)c & smask;
-      return j < hcap ? hot[(((u32)c >> slice_lg) << hot_lg) + j] : Ln[c];
+      return j < hcap ? (int32_t)hot[(((u32)c >> slice_lg) << hot_lg) + j] : Ln[c];
     } else {
-      return (u32)c < nh ? hot[c] : Ln[c];
+      return (u32)c < nh ? (int32_t)hot[c] : Ln[c];
     }
   };
   // lane-consecutive arcs: one gather instruction covers 64 consecutive arcs of
@@ -1670,13 +1744,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   const bool blk = block_mode_now(g);
   // peel rounds of the wave / unit / block tallies (LPA_DENSE_PEEL in the label-dense
   // supersteps, where a round rarely retires more than a few votes)
-  const int pmax = g->since_reset < kDenseSupersteps ? g->dense_peel : kPeelMax;
-  // peel rounds of the row bins before a chunk is sorted (LPA_DENSE_SORT_AFTER)
-  const int sort_after = g->since_reset < kDenseSupersteps ? g->dense_sort_after : g->sort_after;
+  const int pmax = g->since_reset < kDenseSupersteps ? kDensePeel : kPeelMax;
+  // peel rounds of the row bins before a chunk is sorted: none in the label-dense
+  // supersteps (measured best of 0/1/2/3 at C3), kPeelSortAfter otherwise
+  const int sort_after = g->since_reset < kDenseSupersteps ? 0 : kPeelSortAfter;
   // wide tier (rows 4096 < deg <= 8192: 16 waves, a 16K-slot table, one block per CU)
   auto launch_block_wide = [&](hipStream_t st) -> int {
     const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;
-    if (g->block2 && hl > h2) {
+    if (hl > h2) {
       hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, 1024)),
                          dim3(kBlockMaxDeg2 / kSegArcs * 64), 0, st, g->rp, g->al, Lown, h2, hl, g->flist, fcnt,
                          fr_all, pmax);
@@ -1700,10 +1775,11 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 7], st));
     return LPA_OK;
   };
-  // block_at 3 (split): the longest pole of a label-dense superstep is the main
-  // stream's block tiers + units + hub combine; the wide tier goes to the fourth
-  // stream, the narrow tier after the row bins (launched below)
-  const bool split = blk && g->block_at >= 3 && !g->serial;
+  // split (the concurrent schedule): the longest pole of a label-dense superstep is the
+  // main stream's block tiers + units + hub combine, so the wide tier goes to the
+  // fourth stream and the narrow tier follows the hub mid tiers on the main stream
+  // (C3 293.8-295.4 -> 299.3-303.1 GTEPS over the block tiers first on the main stream)
+  const bool split = blk && !g->serial;
   if (split) {
     LPA_HIP(hipStreamWaitEvent(g->aux_stream[2], g->ev_fork, 0));
     LPA_TRY(launch_block_wide(g->aux_stream[2]));
@@ -1711,16 +1787,9 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   }
   // serialized profiling: the block kernel bracketed on its own (stats kernel 16),
   // ahead of the seg units' marks
-  if (blk && (g->block_at == 0 || g->serial)) LPA_TRY(launch_block(s));
-  // block_at 2: on the fourth stream (idle until the hub combine forks its bucket path
-  // there, after this kernel in stream order; the combine's join then covers it)
-  if (blk && g->block_at == 2 && !g->serial) {
-    LPA_HIP(hipStreamWaitEvent(g->aux_stream[2], g->ev_fork, 0));
-    LPA_TRY(launch_block(g->aux_stream[2]));
-    LPA_HIP(hipEventRecord(g->ev_join2[1], g->aux_stream[2]));
-  }
+  if (blk && g->serial) LPA_TRY(launch_block(s));
   LPA_TRY(mark(0, s));
-  const int64_t n_units = blk ? (g->block2 ? g->unit_block2_begin : g->unit_lane_begin) : g->n_segs;
+  const int64_t n_units = blk ? g->unit_block2_begin : g->n_segs;
   if (n_units > 0) {
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
                        g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all, pmax);
@@ -1728,7 +1797,6 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRACE_POINT("seg");
   }
   LPA_TRY(mark(1, s));
-  if (blk && g->block_at == 1 && !g->serial) LPA_TRY(launch_block(s));
 #define LPA_WAVE_LAUNCH(BIN, NC, ST)                                                              \
   {                                                                                           \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                  \
@@ -1759,7 +1827,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
       hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
                          sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, \
-                         sort_after, g->early_sort);                                          \
+                         sort_after);                                                         \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
@@ -1770,17 +1838,13 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb)
   LPA_WAVE_LAUNCH(BIN_W2, 2, sc)
-  if (g->g64_wave) LPA_WAVE_LAUNCH(BIN_G64, 1, sc) else LPA_ROWS_LAUNCH(BIN_G64, 64)
+  LPA_ROWS_LAUNCH(BIN_G64, 64)
   LPA_ROWS_LAUNCH(BIN_G32, 32)
   LPA_ROWS_LAUNCH(BIN_G16, 16)
   LPA_ROWS_LAUNCH(BIN_G8, 8)
   LPA_GROUP_LAUNCH(BIN_G4, 4)
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
-  if (split && g->block_at == 3) {
-    LPA_TRY(launch_block_narrow(sc));
-    LPA_HIP(hipEventRecord(g->ev_join2[2], sc));
-  }
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
@@ -1788,15 +1852,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // run after those streams' bins
   LPA_TRY(mark(2, s));
   const bool hub_fork = !g->serial && g->since_reset < kDenseSupersteps;
-  LPA_TRY(launch_hub_combine(g, Lown, hub_fork, !(split && g->block_at == 4)));
-  if (split && g->block_at == 4) {
+  LPA_TRY(launch_hub_combine(g, Lown, hub_fork, !split));
+  if (split) {
     LPA_TRY(launch_block_narrow(s));
     if (hub_fork) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[0], 0));
   }
   LPA_TRACE_POINT("hub_combine");
   // the block rows' labels are seg-bin slots: joined before the main stream's diff
-  if (blk && g->block_at >= 2 && !g->serial) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[1], 0));
-  if (split && g->block_at == 3) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[2], 0));
+  if (split) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[1], 0));
   LPA_TRY(mark(3, s));
   if (diff) {
     // inside the concurrent tally: no Lc sync here, the scatter refresh does it
@@ -1825,16 +1888,32 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
   if (g->rebuild_hot && (g->nranks == 1 || ranked)) {
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
-    int slice_lg = 0, hot_lg = 0;
+    int slice_lg = 0, hot_lg = 0, hb_lg = 0;
     int32_t nhot = (int32_t)(g->vpad < kHotLabelsSingle ? g->vpad : kHotLabelsSingle);
     if (ranked) {
       while ((int64_t(1) << slice_lg) < g->slice) ++slice_lg;
       while ((int64_t(1) << hot_lg) < kHotLabels / g->nranks) ++hot_lg;
       nhot = (int32_t)(g->nranks << hot_lg);
+      // bits per slice: the largest power of two with P of them in the LDS bit budget,
+      // at least one word and at most the slice
+      while ((int64_t(2) << hb_lg) * g->nranks <= kHotBits && (int64_t(2) << hb_lg) <= g->slice) ++hb_lg;
+      if (hb_lg < 5 || slice_lg < 5) hb_lg = 0;
     }
+    // the giant-label bitmap of L first (same wanted-check: both return at once when
+    // the scatter refreshes instead)
+    const int64_t ngrp = (g->vpad + 511) / 512;
+    if (if_wanted)
+      hipLaunchKernelGGL(k_giant_bits<true>, dim3(cap_grid((ngrp + 3) / 4, 4096)), dim3(256), 0, s, ctr, thr, L,
+                         g->vpad, (unsigned long long*)g->gbits);
+    else
+      hipLaunchKernelGGL(k_giant_bits<false>, dim3(cap_grid((ngrp + 3) / 4, 4096)), dim3(256), 0, s, ctr, thr, L,
+                         g->vpad, (unsigned long long*)g->gbits);
+    LPA_HIP(hipGetLastError());
+    // ranked without a usable bit share: nbits 0 keeps every block in labels mode
+    const int64_t nbits = (ranked && hb_lg == 0) ? 0 : g->vpad;
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
-                     g->arcs, L, nhot, g->al, slice_lg, hot_lg)
+                     g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits)
     if (if_wanted) {
       if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
     } else {
@@ -1887,9 +1966,9 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   // one rank: its isolated slots (and the padding) never change; P > 1: the whole
   // replicated vector (other ranks' slots change through the exchange)
   if (!diff_done)
-    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, g->nranks == 1 ? g->bin_begin[BIN_ISO] : g->vpad, true, par));
+    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, !exchanges(g) ? g->bin_begin[BIN_ISO] : g->vpad, true, par));
   LPA_TRACE_POINT("diff");
-  const int64_t thr = (int64_t)(g->rebuild_frac * (double)g->arcs);
+  const int64_t thr = (int64_t)(kRebuildFrac * (double)g->arcs);
   FrontierMarks fm;
   fm.crow = g->crow;
   fm.rp = g->rp;
@@ -1901,7 +1980,7 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
                      (g->n_chunk_scan + 15) / 16, g->cowner, g->cch, ctr,
                      g->counters + 4 * (par ^ 1), g->cptr,
                      g->cpos, Ln, g->al, thr, fm, g->fr_all + (par ^ 1), g->frontier,
-                     (int64_t)(g->frontier_frac * (double)g->arcs), const_cast<int32_t*>(Lc),
+                     (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc),
                      fold_rebuild ? g->col : (const int32_t*)nullptr, g->arcs);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
@@ -1973,20 +2052,20 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
     // superstep 1 from L0: column runs, no hash tallies (its diff runs in the refresh)
     const bool first = first_runs_now(g);
-    const bool diff_in_tally = g->nranks == 1 && !g->serial && !first;
+    const bool diff_in_tally = !exchanges(g) && !g->serial && !first;
     // converged supersteps on one GPU replay a captured HIP graph of the whole
     // superstep (tally on four streams + diff + refresh; ~25 kernels and the
     // fork/join events): one launch instead of ~40 queue operations.  The graph bakes
     // the label / counter buffers, so there is one per (cur, par) state.
     // supersteps before `eager` are launched stream-ordered (their schedule differs
     // from the converged one a captured graph bakes)
-    const int eager = kDenseSupersteps > g->block_steps ? kDenseSupersteps : g->block_steps;
-    if (g->use_graphs && g->nranks == 1 && !g->serial && g->since_reset >= eager) {
+    const int eager = kDenseSupersteps;
+    if (g->use_graphs && !exchanges(g) && !g->serial && g->since_reset >= eager) {
       const int key = g->cur * 2 + g->par;
       if (!g->gexec[key])
         LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
           int rc = launch_tally(g, Lown, nullptr, Lc, Ln, true);
-          if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true, g->par, nullptr, g->fold_rebuild != 0);
+          if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true, g->par, nullptr, true);
           return rc;
         }));
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
@@ -1996,7 +2075,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       ++g->since_reset;
       continue;
     }
-    if (g->use_graphs && g->nranks > 1 && g->loop == nullptr && !g->serial &&
+    if (g->use_graphs && exchanges(g) && g->loop == nullptr && !g->serial &&
         g->since_reset >= eager) {
       // P > 1: the tally (no collective inside) replays a captured graph per
       // (cur, par); the exchange, whose delta size the host reads, and the refresh
@@ -2016,21 +2095,25 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     }
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
     bool changes_listed = false;
-    if (g->nranks > 1 && has_collective(g))
+    if (exchanges(g) && has_collective(g))
       LPA_TRY(exchange_collective(g, Lc, Ln, g->since_reset < kDenseSupersteps, &changes_listed));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
     // P > 1 without a communicator: the caller completes the superstep with
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
     // (changes + refresh); a refresh here would see a partial vector
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));  // stays if there is no refresh
-    if (g->nranks == 1 || has_collective(g))
+    if (!exchanges(g) || has_collective(g))
       LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par,
                              bev ? bev[kTallyEv + 2] : nullptr));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 3], s));
     // after the last block-mode superstep the next one tallies every row and unit:
     // the block rows' units staged nothing while k_lpa_block tallied them (set at the
     // next superstep's start, after any caller-driven refresh has written fr_all)
-    if (block_mode_now(g) && g->since_reset + 1 == g->block_steps) g->force_all_next = true;
+    if (block_mode_now(g) && g->since_reset + 1 == kDenseSupersteps) g->force_all_next = true;
+    // the column-run superstep staged no hub unit words: a frontier superstep after it
+    // would merge every unit of a dirty hub row with stale (or never written) words of
+    // its unlisted units, so the next superstep tallies every row and unit
+    if (first) g->force_all_next = true;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     g->cur ^= 1;
     g->par ^= 1;

@@ -318,13 +318,25 @@ void par_copy(void* dst, const void* src, size_t n) {
     memcpy(dst, src, n);
     return;
   }
+  // no exception crosses the C ABI: a piece whose thread cannot be started (or
+  // recorded) is copied by this thread
   std::vector<std::thread> th;
   const size_t step = (n + T - 1) / T;
+  try {
+    th.reserve((size_t)T);
+  } catch (...) {
+    memcpy(dst, src, n);
+    return;
+  }
   for (int t = 0; t < T; ++t) {
     const size_t a = (size_t)t * step;
     if (a >= n) break;
     const size_t b = std::min(n, a + step);
-    th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+    try {
+      th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+    } catch (...) {
+      memcpy((char*)dst + a, (const char*)src + a, b - a);
+    }
   }
   for (auto& x : th) x.join();
 }

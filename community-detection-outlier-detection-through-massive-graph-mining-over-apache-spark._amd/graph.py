@@ -66,7 +66,7 @@ class Graph:
             nranks = loopback.nranks
             rc = lib.lpa_graph_create_loopback(sp, dp, m, V, device, flags, rank, loopback._handle(),
                                                ctypes.byref(self._h))
-        elif nranks == 1:
+        elif nranks == 1 and comm_id is None:
             rc = lib.lpa_graph_create(sp, dp, m, V, device, flags, ctypes.byref(self._h))
         else:
             cid = None if comm_id is None else bytes(comm_id)

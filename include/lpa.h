@@ -111,7 +111,9 @@ int lpa_comm_unique_id(uint8_t id_out[128]);
  * 1D partition) and refreshes the replicated label vector with one RCCL
  * allgather per superstep.  Results are bit-identical to
  * the single-GPU build.  Replaces the Spark shuffle of aggregateMessages (U5).
- * comm_id == NULL with nranks > 1 selects the caller-driven exchange below.
+ * comm_id == NULL with nranks > 1 selects the caller-driven exchange below.  A
+ * comm_id with nranks == 1 builds a one-rank job of the same path (the exchange
+ * step and its ncclAllGather run every superstep; labels as lpa_graph_create).
  */
 int lpa_graph_create_dist(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
                           int32_t device, uint32_t flags, int32_t rank, int32_t nranks,
@@ -123,8 +125,9 @@ int lpa_graph_create_dist(const int32_t* src, const int32_t* dst, int64_t m, int
  * thread (lpa_run / lpa_step concurrently, as P processes would).  The library's
  * exchange runs unchanged -- full/delta switch, host count read, in-place
  * allgather, delta chain -- with the allgather done as stream-ordered D2D copies
- * between the handles instead of ncclAllGather.  The group must outlive its
- * handles.  lpa_loopback_abort releases every thread waiting in a collective
+ * between the handles instead of ncclAllGather.  lpa_loopback_destroy on a group
+ * that still has handles attached aborts it (their collectives fail) and leaves the
+ * free to the last handle's lpa_graph_destroy.  lpa_loopback_abort releases every thread waiting in a collective
  * (each then fails with LPA_ERCCL); a rank whose peers never arrive fails the
  * same way after 300 s.
  */

@@ -48,6 +48,33 @@ def degree_mix(seed=0, hubs=(600, 2100, 4500, 9000), n_low=3000, extra=20000):
     return V, perm[s], perm[d]
 
 
+def stale_units(leaves=10_000, leaf_loops=200):
+    """A hub of > 8192 arcs (above the block tiers: tallied by 512-arc units) whose
+    superstep-1 changes touch < 0.5 % of the arcs (leaves held by self-loops), so that
+    superstep 2 runs on the exact frontier right after the column-run superstep 1.
+    The hub row is dirty in superstep 2 only through x (a late unit); b sits in the
+    hub row's first unit, keeps its label in superstep 1 and changes in superstep 2
+    (to its cluster's label), so a unit word staged by an earlier run differs from the
+    superstep-2 truth.  (the column-run path staged no unit words.)"""
+    hub, b, c0, y = 0, 1, 2, 3
+    nclu = 350
+    clu = np.arange(4, 4 + nclu)
+    lv = np.arange(4 + nclu, 4 + nclu + leaves)
+    x = 4 + nclu + leaves
+    V = x + 1
+    e = []
+    e.append(np.stack([np.full(leaves, hub), lv]))                      # hub - leaves
+    e.append(np.stack([np.repeat(lv, leaf_loops), np.repeat(lv, leaf_loops)]))  # leaf self-loops
+    e.append(np.stack([np.full(3, hub), np.full(3, b)]))                # b: 3 votes at the hub
+    e.append(np.stack([np.full(300, b), np.full(300, b)]))              # b: 600 own votes
+    e.append(np.stack([np.repeat(np.full(nclu, b), 2), np.repeat(clu, 2)]))  # b: 700 cluster votes
+    e.append(np.stack([np.repeat(clu, 3), np.full(3 * nclu, c0)]))      # cluster -> c0 in superstep 1
+    e.append(np.stack([np.full(200, x), np.full(200, y)]))              # x -> y in superstep 1
+    e.append(np.stack([np.array([x]), np.array([hub])]))                # x dirties the hub row
+    a = np.concatenate(e, axis=1).astype(np.int32)
+    return V, a[0].copy(), a[1].copy()
+
+
 def random_multigraph(V, m, seed):
     rng = np.random.default_rng(seed)
     return V, rng.integers(0, V, size=m).astype(np.int32), rng.integers(0, V, size=m).astype(np.int32)

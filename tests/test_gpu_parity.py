@@ -4,7 +4,8 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from graphs import adversarial_hub, degree_mix, giant_hub, random_multigraph, settled_hubs, star, two_cliques
+from graphs import (adversarial_hub, degree_mix, giant_hub, random_multigraph, settled_hubs, stale_units, star,
+                    two_cliques)
 
 pytestmark = pytest.mark.gpu
 
@@ -104,6 +105,23 @@ def test_first_superstep_runs_cross_tiles(gfa, oracle, seed):
     got = _per_step(gfa, V, s, d, 3)
     for t in range(3):
         assert np.array_equal(got[t], hist[t]), f"seed {seed} superstep {t + 1}"
+
+
+def test_frontier_after_column_runs(gfa, oracle):
+    """Superstep 1 by column runs stages no hub unit words; when it changes < 0.5 % of
+    the arcs, superstep 2 must still tally every unit of a dirty hub row.
+    Fresh handle per superstep, then lpa_run twice on one handle (the second run would
+    otherwise merge the first run's stale unit words)."""
+    V, s, d = stale_units()
+    _, hist, _ = oracle.lpa(V, s, d, 5, per_iter=True)
+    got = _per_step(gfa, V, s, d, 5)
+    for t in range(5):
+        assert np.array_equal(got[t], hist[t]), f"superstep {t + 1}"
+    with gfa.Graph(s, d, V) as g:
+        assert g.info()["max_degree"] > 8192
+        for _ in range(2):
+            for it in (2, 5):
+                assert np.array_equal(g.run(it), hist[it - 1]), f"run({it})"
 
 
 def test_first_runs_off_identical(gfa, monkeypatch):
@@ -233,14 +251,13 @@ def test_schedules_identical(gfa, graph):
         assert np.array_equal(conc[t], ser[t]), f"superstep {t + 1}"
 
 
-@pytest.mark.parametrize("env", [{"LPA_BLOCK_STEPS": "3"}, {"LPA_BLOCK_STEPS": "0"}, {"LPA_BLOCK_AT": "3"},
-                                 {"LPA_BLOCK_AT": "0"}, {"LPA_SERIAL": "1"}, {"LPA_FIRST_RUNS": "0"},
-                                 {"LPA_G64_WAVE": "1"}, {"LPA_EARLY_SORT": "1"},
-                                 {"LPA_SORT_AFTER": "1"}, {"LPA_SORT_AFTER": "0"}])
+@pytest.mark.parametrize("env", [{"LPA_SERIAL": "1"}, {"LPA_FIRST_RUNS": "0"}, {"LPA_GRAPHS": "0"},
+                                 {"LPA_REBUILD_HOT": "0"}, {"LPA_FRONTIER": "0"}, {"LPA_LOCALITY": "0"}])
 def test_schedule_options_bit_exact(gfa, oracle, monkeypatch, env):
-    """Schedule options read at graph creation (block-mode superstep count, where the
-    block tiers run, the serialized profiling schedule): labels bit-exact per
-    superstep on the degree mix (both block tiers + a bucketed hub) and R-MAT-16."""
+    """The switches read at graph creation (the serialized profiling
+    schedule, superstep 1 by hash tallies, no captured graphs, the plain rebuild, no
+    frontier, plain degree order): labels bit-exact per superstep on the degree mix
+    (both block tiers + a bucketed hub) and R-MAT-16."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     V, s, d = degree_mix(1)
