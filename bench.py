@@ -158,6 +158,14 @@ def cpu_baseline(src_np, dst_np, V, gpu_graph, budget_s=25.0):
                 parity_vs_gpu=ok)
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A stderr progress line per phase (the JSON result is the only stdout line)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def self_launch(n):
     """Run this script under torch.distributed.run with n ranks (one per GPU) as a
     child process; returns its exit code.  Called before torch is imported."""
@@ -324,11 +332,13 @@ def main():
         src = dst = None
     torch.cuda.empty_cache()
 
+    progress(f"{config_id}: built (arcs {info['arcs']}), warm-up")
     g.step(1)          # prime: code objects loaded, caches warm
     for _ in range(args.warmup):
         g.reset()
         g.step(MAX_ITER)
 
+    progress("timed calls")
     # ---- timed: K labelPropagation(10) calls, supersteps 2..10 of each ----
     t_sum = 0.0
     for _ in range(args.steps):
@@ -345,6 +355,7 @@ def main():
     n_timed = (MAX_ITER - 1) * args.steps
     value = m * n_timed / t_sum / 1e9
 
+    progress(f"timed: {value:.1f} GTEPS; per-superstep method")
     # ---- BASELINE.md:48 method: median superstep time of iterations 2..10 over >= 5
     # runs (HIP events around each superstep, concurrent schedule, graphs replayed) ----
     runs = max(5, args.steps)
@@ -367,6 +378,7 @@ def main():
     g.set_frontier(True)
     conv_ms = max_over_ranks(statistics.median(x for r in off_ms for x in r[2:]))  # supersteps 4..10
 
+    progress("lpa_run(10) wall time")
     # ---- whole call: lpa_run(10) from reset, labels gathered into a device tensor ----
     out = torch.empty(V, dtype=torch.int32, device=f"cuda:{device}")
     run_ms = []
@@ -386,6 +398,7 @@ def main():
         del src, dst
         torch.cuda.empty_cache()
 
+    progress("serialized breakdown")
     # ---- breakdown: supersteps 2..10 again with the tally kernels serialized on one
     # stream and HIP events around every kernel (standalone durations: the roofline
     # of that kernel, not of its co-runners; not used for `value`) ----
@@ -501,6 +514,7 @@ def main():
         "exchange_ms_per_superstep": round(exch_ms / (MAX_ITER - 1), 4),
     }
     if world == 1 and not args.no_outlier:
+        progress("outlier stage")
         lab = g.run(MAX_ITER)
         for mode, key in (("L1", "outlier_l1_ms"), ("L2", "outlier_l2_ms")):
             ts = []
@@ -508,6 +522,7 @@ def main():
                 t0 = time.perf_counter()
                 res = g.outlier(lab, mode, sub_iter=5)
                 ts.append((time.perf_counter() - t0) * 1e3)
+                progress(f"outlier {mode}: {ts[-1]:.1f} ms")
             out_json[key] = round(statistics.median(ts), 2)
             if mode == "L1":   # the first call also builds the handle's distinct edge set
                 out_json["outlier_l1_first_ms"] = round(ts[0], 2)
@@ -518,8 +533,10 @@ def main():
                                     "distinct edges; the handle's distinct directed edge set (topology) is built "
                                     "by its first outlier call and kept (outlier_l1_first_ms includes it)")
     if keep_host and rank == 0:
+        progress("CPU baseline")
         out_json["cpu_baseline"] = cpu_baseline(src_np, dst_np, V, g)
     if quality is not None:
+        progress("quality report")
         out_json["quality"] = quality_report(gfa, device, quality["bench_graph"])
     if rank == 0:
         print(json.dumps(out_json), flush=True)

@@ -587,6 +587,11 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     LPA_TRY(build_hub_tables(g, deg_own));
     scratch_free(g, nseg);
     LPA_TRY(dev_alloc(g, (void**)&g->ucnt, sizeof(int32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
+    LPA_TRY(dev_alloc(g, (void**)&g->ugc, sizeof(uint32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
+    LPA_TRY(dev_alloc(g, (void**)&g->umx, sizeof(uint32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
+    LPA_TRY(dev_alloc(g, (void**)&g->ulist2, sizeof(int32_t) * (g->n_segs > 0 ? g->n_segs : 1)));
+    LPA_TRY(dev_alloc(g, (void**)&g->gdec, sizeof(int32_t) * 2));
+    LPA_HIP(hipMemsetAsync(g->gdec, 0, sizeof(int32_t) * 2, s));
     g->hub_uoff = seg_off;  // the seg bin is exactly the hub rows (deg > kSegArcs)
     // first unit of the k_lpa_block rows
     LPA_HIP(hipMemcpyAsync(&g->unit_lane_begin, seg_off + g->hub_lane_begin, sizeof(int64_t),

@@ -86,7 +86,7 @@ void destroy(lpa_graph* g) {
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
                   g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best,
-                  g->gbits};
+                  g->gbits, g->ugc, g->umx, g->ulist2, g->gdec};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);

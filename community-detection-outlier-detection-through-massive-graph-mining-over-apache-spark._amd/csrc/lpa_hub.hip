@@ -191,6 +191,51 @@ __device__ __forceinline__ void queue_row(int64_t h, int T, int nu, int lane,
   }
 }
 
+// Superstep 2's giant-label decision for the unit-tallied rows [0, h_end) (after
+// k_lpa_units_giant): row h's G votes S_g = sum of its units' ugc, and any other
+// label's row count is at most S_m = sum of its units' umx (each unit's fullest
+// bucket).  S_g > S_m: G is the strict mode -- written, wcount[h] = -1 (the combine's
+// classify / enqueue skip the row).  Otherwise wcount[h] = 0 and the row's units are
+// appended to ulist2 (count *ndec) for the exact unit tally.  One wave per row.
+__global__ __launch_bounds__(256) void k_hub_decide(int64_t h_end, const int64_t* __restrict__ uoff,
+                                                    const uint32_t* __restrict__ ugc,
+                                                    const uint32_t* __restrict__ umx,
+                                                    const int32_t* __restrict__ gsel,
+                                                    int32_t* __restrict__ Ln, int32_t* __restrict__ wcount,
+                                                    int32_t* __restrict__ ulist2, int32_t* __restrict__ ndec) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  const int32_t G = gsel[0];
+  for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < h_end; h += stride) {
+    const int64_t u0 = uoff[h];
+    const int nu = (int)(uoff[h + 1] - u0);
+    u64 sg = 0, sm = 0;
+    for (int j = lane; j < nu; j += 64) {
+      sg += ugc[u0 + j];
+      sm += umx[u0 + j];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      sg += __shfl_xor(sg, off, 64);
+      sm += __shfl_xor(sm, off, 64);
+    }
+    if (sg > sm) {
+      if (lane == 0) {
+        Ln[h] = G;
+        wcount[h] = -1;
+      }
+    } else {
+      int base = 0;
+      if (lane == 0) {
+        wcount[h] = 0;
+        base = atomicAdd(ndec, nu);
+      }
+      base = __shfl(base, 0, 64);
+      for (int j = lane; j < nu; j += 64) ulist2[base + j] = (int32_t)(u0 + j);
+    }
+  }
+}
+
 // Label-dense supersteps: classify the rows of > kLaneUnits units right after the
 // unit tallies, so the bucket path (count / scan / scatter / bucket, complete once
 // these rows are queued: rows of <= kLaneUnits units never exceed kCombDirect words)
@@ -206,11 +251,12 @@ __global__ __launch_bounds__(256) void k_hub_classify(int64_t h_lane, int64_t n_
                                                       int32_t* __restrict__ lists,
                                                       int32_t* __restrict__ lcnt,
                                                       u64* __restrict__ itemsCB,
-                                                      u64* __restrict__ itemsCC) {
+                                                      u64* __restrict__ itemsCC, int giant) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t stride = (int64_t)gridDim.x * 4;
   for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < h_lane; h += stride) {
+    if (giant && wcount[h] < 0) continue;  // settled by k_hub_decide (uniform)
     const RowUnits ru = row_units(rp, uoff, h);
     const int nu = ru.nu;
     const int32_t* uc = ucnt + ru.u0;
@@ -249,11 +295,15 @@ __global__ __launch_bounds__(256) void k_hub_enqueue(int64_t h_lane, int64_t n_h
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t h0 = (int64_t)blockIdx.x * blockDim.x; h0 < h_lane; h0 += stride) {
     const int64_t h = h0 + threadIdx.x;
-    const bool live = h < h_lane;
+    bool live = h < h_lane;
     int T = 0, nu = 0;
     if (live) {
       T = wcount[h];
       nu = (int)(uoff[h + 1] - uoff[h]);
+      if (T < 0) {  // settled by k_hub_decide: not queued
+        wcount[h] = 0;
+        live = false;
+      }
     }
     const bool sm = live && nu <= kSmallWords && T <= kSmallWords;
     const bool q = live && !sm;
@@ -350,6 +400,10 @@ __global__ __launch_bounds__(256) void k_hub_small(int64_t nd, int64_t n_hub,
                                    : (q < nd_items + nS ? (int64_t)lists[5 * n_hub + (q - nd_items)]
                                                         : (int64_t)lists[2 * n_hub + (q - nd_items - nS)]);
     if (h >= nd && q < nd_items) continue;  // a lane-path row (k_hub_lanes); uniform
+    if (q < nd_items && wcount[h] < 0) {     // settled by k_hub_decide (serialized schedule)
+      if (lane == 0) wcount[h] = 0;
+      continue;
+    }
     const RowUnits ru = row_units(rp, uoff, h);
     const int nu = ru.nu;
     const int32_t* uc = ucnt + ru.u0;
@@ -1121,7 +1175,18 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
   return LPA_OK;
 }
 
-int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join) {
+// the giant-label decision of superstep 2 (before the combine, on the main stream):
+// k_hub_decide over the unit-tallied rows [0, h_end), then the exact unit tally of the
+// units it listed (k_lpa_units in list mode, launched by the caller's lambda)
+int launch_hub_decide(lpa_graph* g, int32_t* Lown, int64_t h_end, const int32_t* gsel) {
+  if (h_end <= 0) return LPA_OK;
+  hipLaunchKernelGGL(k_hub_decide, dim3(grid_cap((h_end + 3) / 4, 2048)), dim3(256), 0, g->stream, h_end,
+                     g->hub_uoff, g->ugc, g->umx, gsel, Lown, g->hub_wcount, g->ulist2, g->gdec);
+  LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
+
+int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join, bool giant) {
   const int64_t n = g->n_hub;
   if (n == 0) return LPA_OK;
   hipStream_t s = g->stream;
@@ -1180,7 +1245,7 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join) {
     if (hc > 0) {
       hipLaunchKernelGGL(k_hub_classify, dim3(grid_cap((hc + 3) / 4, 2048)), dim3(256), 0, s, hc, n,
                          g->rp, g->hub_uoff, g->ucnt, g->hub_wcount, lists, lcnt, g->items_cb,
-                         g->items_cc);
+                         g->items_cc, giant ? 1 : 0);
       LPA_HIP(hipGetLastError());
       hipLaunchKernelGGL(k_hub_enqueue, dim3(grid_cap((hc + 255) / 256, 2048)), dim3(256), 0, s, hc, n,
                          g->hub_uoff, g->hub_wcount, lists, lcnt);

@@ -146,6 +146,10 @@ struct lpa_graph {
                                   //  stage[rp[h] + j*kSegArcs ...), ucnt[hub_uoff[h] + j] words)
   int64_t* hub_uoff = nullptr;    // [n_hub + 1] first unit of each row (units = segs[])
   int32_t* ucnt = nullptr;        // [n_segs] staged words of each unit
+  uint32_t* ugc = nullptr;        // [n_segs] superstep 2: the unit's giant-label votes ...
+  uint32_t* umx = nullptr;        // [n_segs] ... and its fullest other-label bucket (k_lpa_units_giant)
+  int32_t* ulist2 = nullptr;      // [n_segs] units of the rows k_hub_decide could not settle
+  int32_t* gdec = nullptr;        // [2] their count, then a constant 0 (the list-mode "fr_all")
   lpa::u64* scat = nullptr;       // [hub arcs] bucket-partitioned words
   int32_t* hub_wcount = nullptr;  // [n_hub] staged words of a queued row (0 otherwise)
   lpa::u64* hub_best = nullptr;   // [n_hub] reduced tally word (bucketed hubs)
@@ -271,7 +275,9 @@ int init_labels(lpa_graph* g);
 int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
 // join = false: the forked bucket path's end is recorded in ev_join2[0] and the caller
 // joins it (main-stream work can be queued behind the mid tiers first)
-int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join = true);  // lpa_hub.hip
+int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join = true,
+                       bool giant = false);  // lpa_hub.hip
+int launch_hub_decide(lpa_graph* g, int32_t* Lown, int64_t h_end, const int32_t* gsel);  // lpa_hub.hip
 bool block_mode_now(const lpa_graph* g);  // lpa_iter.hip
 int64_t block_rows_begin(const lpa_graph* g);  // first row of the block tiers (lpa_iter.hip)
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]

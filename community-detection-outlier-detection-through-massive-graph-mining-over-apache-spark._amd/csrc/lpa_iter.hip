@@ -142,6 +142,15 @@ __device__ __forceinline__ u32 wave_sum_u32(u32 v) {
          (u32)__builtin_amdgcn_readlane((int)v, 32) + (u32)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+__device__ __forceinline__ u32 wave_max_u32(u32 v) {
+  v = max(v, dpp_u32<0xB1>(v));
+  v = max(v, dpp_u32<0x4E>(v));
+  v = max(v, dpp_u32<0x141>(v));
+  v = max(v, dpp_u32<0x140>(v));
+  return max(max((u32)__builtin_amdgcn_readlane((int)v, 0), (u32)__builtin_amdgcn_readlane((int)v, 16)),
+             max((u32)__builtin_amdgcn_readlane((int)v, 32), (u32)__builtin_amdgcn_readlane((int)v, 48)));
+}
+
 __device__ __forceinline__ u32 hash_slot(u32 label, int shift) {
   return (label * 0x9E3779B1u) >> shift;
 }
@@ -335,6 +344,44 @@ __device__ __forceinline__ void load_labels(u32 (&lab)[NC], const int32_t* __res
 }
 
 // ---------------------------------------------------------------------------
+// The giant label of the label-dense supersteps.  One label G -- the current label of
+// the top hub, L[slot 0] -- is the STRICT mode of nearly every row of more than 64
+// arcs in superstep 2 (R-MAT, oracle at scale 22: G holds ~36 % of the votes of every
+// degree band, a median 10-13x the next label's count).  giant_count counts G's votes
+// exactly and adds every other vote to a bucket of a small label-hash histogram: a
+// label's count is at most its bucket's, so G's count above every bucket decides the
+// row -- no hash table, no probe chains, no table scan.  A row it cannot decide (G not
+// the strict mode, or a bucket too full) takes the exact tally.
+// ---------------------------------------------------------------------------
+constexpr int kGiantLg = 6;   // wave histogram: 64 buckets, one per lane
+
+// this lane's G votes among its labels; the others into hist (bucket = label hash >>
+// (32 - lg)); no-return LDS adds
+template <int NC>
+__device__ __forceinline__ u32 giant_count(const u32 (&lab)[NC], int nch, u32 G, u32* hist, int lg) {
+  u32 c = 0;
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    if (u >= nch) break;  // uniform
+    const u32 x = lab[u];
+    if (x == G) ++c;
+    else if (x != kNone) atomicAdd(&hist[hash_slot(x, 32 - lg)], 1u);
+  }
+  return c;
+}
+
+// one wave, one row in registers: true when G is decided (its count above every
+// bucket); the histogram (kGiantLg buckets at hist) is left zeroed either way
+template <int NC>
+__device__ __forceinline__ bool giant_decide(const u32 (&lab)[NC], int nch, u32 G, u32* hist, int lane) {
+  const u32 cg = wave_sum_u32(giant_count<NC>(lab, nch, G, hist, kGiantLg));
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const u32 b = hist[lane];
+  hist[lane] = 0u;
+  return cg > wave_max_u32(b);
+}
+
+// ---------------------------------------------------------------------------
 // bins g1 / g2 / g4 / g8 / g16
 // ---------------------------------------------------------------------------
 // Frontier row lists (k_frontier_lists): with *fr_all == 0 a bin kernel tallies only
@@ -509,7 +556,7 @@ __device__ __forceinline__ void row_load(u32 (&raw)[NC], const int32_t* __restri
 template <int NC>
 __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r, int64_t v,
                                           int32_t* __restrict__ Ln, u64* tab, uint16_t* lst, int lane,
-                                          u64 lt, int pmax) {
+                                          u64 lt, int pmax, bool giant, u32 G) {
   const int d = span_len(r);
   if (d == 0) return;
   u32 lab[NC];
@@ -518,6 +565,11 @@ __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r
   int lg = ceil_log2(2u * (u32)d);
   lg = lg < 6 ? 6 : lg;
   const int nch = (d + 63) >> 6;
+  // label-dense supersteps: the giant label first (the table's first 64 words, zero)
+  if (giant && giant_decide<NC>(lab, nch, G, reinterpret_cast<u32*>(tab), lane)) {
+    if (lane == 0) Ln[v] = (int32_t)G;
+    return;
+  }
   Batch<NC> bt;
   peel_batch<NC>(bt, lab, nch, lane, pmax, true);
   if (!bt.any) {
@@ -547,7 +599,8 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend, const int32_t* __restrict__ flist,
                                                   const int32_t* __restrict__ fcnt_b,
-                                                  const int32_t* __restrict__ fr_all, int pmax) {
+                                                  const int32_t* __restrict__ fr_all, int pmax,
+                                                  const int32_t* __restrict__ gsel) {
   constexpr int kCap = 2 * 64 * NC;
   __shared__ u64 tab_all[4][kCap];
   __shared__ uint16_t lst_all[4][64 * NC];
@@ -561,6 +614,10 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   int64_t i = (int64_t)blockIdx.x * 4 + w;   // work item: row br.row(i)
   if (i >= br.n) return;  // no block-level barriers in this kernel
   for (int k = lane; k < kCap; k += 64) tab[k] = 0ull;  // only waves with rows clear
+  // gsel (label-dense supersteps): the label vector this superstep reads; its slot 0
+  // is the top hub, whose label is the giant label
+  const bool giant = gsel != nullptr;
+  const u32 G = giant ? (u32)gsel[0] : 0u;
   RowSpan s0 = row_span(rp, br, i), s1 = row_span(rp, br, i + stride), s2 = row_span(rp, br, i + 2 * stride);
   u32 ra[NC], rb[NC], rc[NC];
   row_load<NC>(ra, al, s0, lane);
@@ -568,17 +625,17 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   while (true) {
     row_load<NC>(rc, al, s2, lane);
     RowSpan s3 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(ra, s0, br.row(i), Ln, tab, lst, lane, lt, pmax);
+    row_tally<NC>(ra, s0, br.row(i), Ln, tab, lst, lane, lt, pmax, giant, G);
     i += stride;
     if (i >= br.n) break;
     row_load<NC>(ra, al, s3, lane);
     RowSpan s4 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(rb, s1, br.row(i), Ln, tab, lst, lane, lt, pmax);
+    row_tally<NC>(rb, s1, br.row(i), Ln, tab, lst, lane, lt, pmax, giant, G);
     i += stride;
     if (i >= br.n) break;
     row_load<NC>(rb, al, s4, lane);
     RowSpan s5 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(rc, s2, br.row(i), Ln, tab, lst, lane, lt, pmax);
+    row_tally<NC>(rc, s2, br.row(i), Ln, tab, lst, lane, lt, pmax, giant, G);
     i += stride;
     if (i >= br.n) break;
     s0 = s3;
@@ -606,12 +663,17 @@ __global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* _
                                                                int64_t h1,
                                                                const int32_t* __restrict__ flist,
                                                                const int32_t* __restrict__ fcnt0,
-                                                               const int32_t* __restrict__ fr_all, int pmax) {
+                                                               const int32_t* __restrict__ fr_all, int pmax,
+                                                               const int32_t* __restrict__ gsel) {
   static_assert((1 << kLg) >= 2 * kBlockWaves * kSegArcs, "table load <= 1/2");
   constexpr int kSlots = 1 << kLg;
   constexpr int kT = 64 * kBlockWaves;
+  constexpr int kGB = 256;   // giant-label histogram buckets of a block row
+  static_assert(kT >= kGB, "one bucket per thread");
   __shared__ u64 tab[kSlots];
   __shared__ u64 redw[kBlockWaves];
+  __shared__ u32 ghist[kGB];
+  __shared__ u32 gcnt[2], gmax[2];   // by row parity (two barriers per decided row)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u64 lt = (1ull << lane) - 1ull;
@@ -619,7 +681,13 @@ __global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* _
   const int64_t n = all ? h1 - h0 : (int64_t)*fcnt0;
   if ((int64_t)blockIdx.x >= n) return;  // uniform
   for (int i = threadIdx.x; i < kSlots; i += kT) tab[i] = 0ull;
+  if (threadIdx.x < kGB) ghist[threadIdx.x] = 0u;
+  if (threadIdx.x < 2) gcnt[threadIdx.x] = gmax[threadIdx.x] = 0u;
+  // gsel (label-dense supersteps): G = the top hub's current label (giant_count)
+  const bool giant = gsel != nullptr;
+  const u32 G = giant ? (u32)gsel[0] : 0u;
   __syncthreads();
+  int rpar = 0;  // parity of the rows this block has tallied
   for (int64_t q = blockIdx.x; q < n; q += gridDim.x) {
     const int64_t h = all ? h0 + q : (int64_t)flist[q];
     if (h < h0 || h >= h1) continue;  // uniform over the block
@@ -628,10 +696,37 @@ __global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* _
     int lg = ceil_log2(2u * (u32)d);
     lg = lg < 6 ? 6 : lg;
     const int64_t c0 = b + (int64_t)w * kSegArcs;
+    u32 lab[kChunks];
+    int nch = 0;
     if (c0 < e) {
-      u32 lab[kChunks];
       load_labels<kChunks>(lab, al, c0, e, lane);
-      const int nch = (int)min<int64_t>(kChunks, (e - c0 + 63) >> 6);
+      nch = (int)min<int64_t>(kChunks, (e - c0 + 63) >> 6);
+    }
+    if (giant) {
+      // G's votes (block total) and the other votes' bucket histogram; decided when
+      // G's count exceeds every bucket (uniform: read after the barrier)
+      // (the counters of parity rpar: the other parity's, read by the previous row
+      // before this row's first barrier, are reset before its second)
+      if (c0 < e) {
+        const u32 cg = wave_sum_u32(giant_count<kChunks>(lab, nch, G, ghist, 8));
+        if (lane == 0 && cg) atomicAdd(&gcnt[rpar], cg);
+      }
+      __syncthreads();
+      if (threadIdx.x < kGB) {
+        const u32 m = ghist[threadIdx.x];
+        ghist[threadIdx.x] = 0u;
+        if (m) atomicMax(&gmax[rpar], m);
+      }
+      if (threadIdx.x == 0) gcnt[rpar ^ 1] = gmax[rpar ^ 1] = 0u;
+      __syncthreads();
+      const bool decided = gcnt[rpar] > gmax[rpar];
+      rpar ^= 1;
+      if (decided) {  // uniform
+        if (threadIdx.x == 0) Ln[h] = (int32_t)G;
+        continue;
+      }
+    }
+    if (c0 < e) {
       Batch<kChunks> bt;
       peel_batch<kChunks>(bt, lab, nch, lane, pmax);
       int unused = 0;
@@ -721,9 +816,12 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend, const int32_t* __restrict__ flist,
                                                   const int32_t* __restrict__ fcnt_b,
-                                                  const int32_t* __restrict__ fr_all, int sort_after) {
+                                                  const int32_t* __restrict__ fr_all, int sort_after,
+                                                  const int32_t* __restrict__ gsel) {
   static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "lane width");
   constexpr int RB = 512 / G;  // rows per batch
+  constexpr int kGB = 16;      // giant-label histogram buckets per row (group)
+  __shared__ u32 ghist_all[4][64 / G * kGB];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (!*fr_all) {
@@ -742,6 +840,14 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t bi = (int64_t)blockIdx.x * 4 + w;
   if (bi >= nb) return;  // no block-level barriers in this kernel
+  // gsel (superstep 2, rows of > 8 arcs): a chunk whose every row is decided for the
+  // giant label (its exact count above each of the row's kGB label-hash buckets of
+  // other votes, as giant_decide) skips the peel / sort
+  const bool giant = G >= 16 && gsel != nullptr;
+  const u32 Gl = giant ? (u32)gsel[0] : 0u;
+  u32* hg = &ghist_all[w][(lane / G) * kGB];
+  const int gj = lane & (G - 1);   // G >= kGB when giant: lane gj < kGB owns bucket gj
+  if (gj < kGB) hg[gj] = 0u;
   int64_t rpl0, rpe0, rpl1 = 0, rpe1 = 0;
   rows_rp<G>(rp, vbeg + bi * RB, vend, lane, rpl0, rpe0);
   if (bi + stride < nb) rows_rp<G>(rp, vbeg + (bi + stride) * RB, vend, lane, rpl1, rpe1);
@@ -766,6 +872,23 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       const u32 lb = lab[c];
       u64 act = __ballot(lb != kNone);
       u64 best = 0ull;
+      if constexpr (G >= kGB) if (giant) {
+        const u64 gb = __ballot(lb == Gl);
+        const u32 cg = (u32)__popcll((gb >> gbase) & gm);
+        if (lb != Gl && lb != kNone) atomicAdd(&hg[hash_slot(lb, 28)], 1u);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        u32 mx = 0u;
+        if (gj < kGB) {
+          mx = hg[gj];
+          hg[gj] = 0u;
+        }
+        for (int off = G >> 1; off > 0; off >>= 1) mx = max(mx, (u32)lane::lane_xor(mx, off, lane));
+        const bool dec = cg > mx;
+        if (__ballot(lb != kNone && !dec) == 0ull) {  // uniform: every row decided
+          best = dec ? tally(cg, Gl) : 0ull;
+          act = 0ull;
+        }
+      }
       for (int round = 0; act; ++round) {
         // uniform: a label-dense chunk after sort_after rounds
         if (round == sort_after) {
@@ -930,6 +1053,66 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
     d0 = d3;
     d1 = d4;
     d2 = d5;
+  }
+}
+
+// Superstep 2, the unit-tallied hub rows (deg > kBlockMaxDeg2): each unit only counts
+// the giant label's votes exactly (ugc[u]) and bounds every other label's count in the
+// unit by its fullest label-hash bucket (umx[u]; giant_count, 64 buckets).  A label's
+// row count is at most the sum of the units' bounds, so k_hub_decide settles a row
+// whose G votes exceed that sum without staging or merging a single word; only the
+// units of the rows it cannot settle are then tallied exactly (k_lpa_units, list mode).
+// Block 0 also zeroes the undecided-unit list count (*ndec) for k_hub_decide.
+__global__ __launch_bounds__(256) void k_lpa_units_giant(const int32_t* __restrict__ al,
+                                                         const Segment* __restrict__ units, int64_t nunits,
+                                                         const int32_t* __restrict__ gsel,
+                                                         uint32_t* __restrict__ ugc, uint32_t* __restrict__ umx,
+                                                         int32_t* __restrict__ ndec) {
+  __shared__ u32 hist_all[4][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ndec = 0;
+  u32* hist = hist_all[w];
+  hist[lane] = 0u;
+  const u32 G = (u32)gsel[0];
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t u = (int64_t)blockIdx.x * 4 + w;
+  if (u >= nunits) return;  // no block-level barriers in this kernel
+  UnitIds ui;
+  ui.n = nunits;
+  ui.lim = nunits;
+  ui.list = nullptr;
+  Segment d0 = load_unit(units, ui, u), d1 = load_unit(units, ui, u + stride);
+  u32 ra[kChunks], rb[kChunks];
+  unit_load(ra, al, d0, lane);
+  auto one = [&](const u32 (&raw)[kChunks], const Segment& d, int64_t id) {
+    const int len = d.len & 1023;
+    u32 lab[kChunks];
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) lab[c] = c * 64 + lane < len ? raw[c] : kNone;
+    const u32 cg = wave_sum_u32(giant_count<kChunks>(lab, kChunks, G, hist, kGiantLg));
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const u32 b = hist[lane];
+    hist[lane] = 0u;
+    const u32 hm = wave_max_u32(b);
+    if (lane == 0) {
+      ugc[id] = cg;
+      umx[id] = hm;
+    }
+  };
+  while (true) {
+    unit_load(rb, al, d1, lane);
+    Segment d2 = load_unit(units, ui, u + 2 * stride);
+    one(ra, d0, u);
+    u += stride;
+    if (u >= nunits) break;
+    unit_load(ra, al, d2, lane);
+    Segment d3 = load_unit(units, ui, u + 2 * stride);
+    one(rb, d1, u);
+    u += stride;
+    if (u >= nunits) break;
+    d0 = d2;
+    d1 = d3;
   }
 }
 
@@ -1748,13 +1931,17 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // peel rounds of the row bins before a chunk is sorted: none in the label-dense
   // supersteps (measured best of 0/1/2/3 at C3), kPeelSortAfter otherwise
   const int sort_after = g->since_reset < kDenseSupersteps ? 0 : kPeelSortAfter;
+  // superstep 2 (the label-dense one after the column-run superstep 1): the wave and
+  // block tallies try the giant label first (giant_decide); gsel = the label vector
+  // the tally reads (its slot 0 is the top hub)
+  const int32_t* gsel = g->since_reset == 1 ? Lc : nullptr;
   // wide tier (rows 4096 < deg <= 8192: 16 waves, a 16K-slot table, one block per CU)
   auto launch_block_wide = [&](hipStream_t st) -> int {
     const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;
     if (hl > h2) {
       hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, 1024)),
                          dim3(kBlockMaxDeg2 / kSegArcs * 64), 0, st, g->rp, g->al, Lown, h2, hl, g->flist, fcnt,
-                         fr_all, pmax);
+                         fr_all, pmax, gsel);
       LPA_HIP(hipGetLastError());
     }
     return LPA_OK;
@@ -1764,7 +1951,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     const int64_t nb = g->n_hub - g->hub_lane_begin;
     hipLaunchKernelGGL((k_lpa_block<13, kBlockMaxDeg / kSegArcs>), dim3(cap_grid(nb, 2048)),
                        dim3(kBlockMaxDeg / kSegArcs * 64), 0, st, g->rp, g->al, Lown, g->hub_lane_begin, g->n_hub,
-                       g->flist, fcnt, fr_all, pmax);
+                       g->flist, fcnt, fr_all, pmax, gsel);
     LPA_HIP(hipGetLastError());
     return LPA_OK;
   };
@@ -1790,7 +1977,18 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   if (blk && g->serial) LPA_TRY(launch_block(s));
   LPA_TRY(mark(0, s));
   const int64_t n_units = blk ? g->unit_block2_begin : g->n_segs;
-  if (n_units > 0) {
+  // superstep 2 in block mode: the unit-tallied rows by giant counts first, the exact
+  // unit tally only for the rows k_hub_decide cannot settle
+  const bool giant_units = gsel != nullptr && blk;
+  if (n_units > 0 && giant_units) {
+    hipLaunchKernelGGL(k_lpa_units_giant, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s, g->al,
+                       g->segs, n_units, gsel, g->ugc, g->umx, g->gdec);
+    LPA_HIP(hipGetLastError());
+    LPA_TRY(launch_hub_decide(g, Lown, block_rows_begin(g), gsel));
+    hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
+                       g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist2, g->gdec, g->gdec + 1, pmax);
+    LPA_HIP(hipGetLastError());
+  } else if (n_units > 0) {
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
                        g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all, pmax);
     LPA_HIP(hipGetLastError());
@@ -1803,7 +2001,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(mark(2 * (BIN + 1), ST));                                                         \
     if (n > 0) {                                                                              \
       hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, ST,  \
-                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, pmax); \
+                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, pmax, gsel); \
       LPA_HIP(hipGetLastError());                                                             \
     }                                                                                         \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                     \
@@ -1827,7 +2025,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
       hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
                          sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, \
-                         sort_after);                                                         \
+                         sort_after, gsel);                                                   \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
@@ -1852,7 +2050,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // run after those streams' bins
   LPA_TRY(mark(2, s));
   const bool hub_fork = !g->serial && g->since_reset < kDenseSupersteps;
-  LPA_TRY(launch_hub_combine(g, Lown, hub_fork, !split));
+  LPA_TRY(launch_hub_combine(g, Lown, hub_fork, !split, giant_units));
   if (split) {
     LPA_TRY(launch_block_narrow(s));
     if (hub_fork) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[0], 0));
