@@ -182,36 +182,15 @@ def self_launch(n):
     return subprocess.run(cmd, env=env).returncode
 
 
-def modularity(src, dst, lab):
-    """Newman modularity of the partition `lab` (device int32 labels, values in
-    [0, V)) on the symmetrised multigraph LPA votes on: every input edge is two arcs
-    (a self-loop two arcs at its vertex), Q = intra arcs / A - sum_c (D_c / A)^2."""
-    import torch
-
-    A = 2 * src.numel()
-    if A == 0:
-        return 0.0
-    V = lab.numel()
-    intra = 0
-    step = 1 << 27
-    for i in range(0, src.numel(), step):   # bounded temporaries
-        s, d = src[i:i + step].long(), dst[i:i + step].long()
-        intra += 2 * int((lab[s] == lab[d]).sum().item())
-    deg = torch.bincount(src.long(), minlength=V) + torch.bincount(dst.long(), minlength=V)
-    D = torch.zeros(V, dtype=torch.float64, device=lab.device)
-    D.index_add_(0, lab.long(), deg.double())
-    return intra / A - float(((D / A) ** 2).sum().item())
-
-
-def quality_entry(src, dst, lab, extra=None):
-    import torch
-
-    V = lab.numel()
-    present = torch.bincount(lab.long(), minlength=V) > 0
-    q = dict(communities=int(present.sum().item()), modularity=round(modularity(src, dst, lab), 6))
+def quality_entry(g, lab, extra=None):
+    """Community count + modularity of labels `lab` on handle g's graph (lpa_quality:
+    exact integer sums on the GPU; the symmetrised multigraph LPA votes on)."""
+    q = g.quality(lab)
+    out = dict(communities=q["n_communities"], modularity=round(q["modularity"], 6),
+               intra_arc_fraction=round(q["intra_arcs"] / q["arcs"], 6) if q["arcs"] else 0.0)
     if extra:
-        q.update(extra)
-    return q
+        out.update(extra)
+    return out
 
 
 def quality_report(gfa, device, bench_entry):
@@ -219,35 +198,29 @@ def quality_report(gfa, device, bench_entry):
     graph (maxIter=10) and C2 (maxIter=10, NMI vs the planted blocks): community
     count + modularity of the GPU labels."""
     import numpy as np
-    import torch
 
     rep = {"agreement_note": "GraphFrames/GraphX itself cannot run here (no JVM, no pyspark): agreement "
                              "with its own output is unpinned; labels are bit-exact vs the oracle's "
                              "smallest-label tie-break (tests/)",
            "bench_graph": bench_entry}
     z = np.load(os.path.join(ROOT, "tests", "golden", "r9_golden.npz"), allow_pickle=False)
-    dev = torch.device("cuda", device)
-    s1 = torch.from_numpy(z["src"].astype(np.int32)).to(dev)
-    d1 = torch.from_numpy(z["dst"].astype(np.int32)).to(dev)
     V1 = int(z["ids"].size)
     with gfa.Graph(z["src"], z["dst"], V1, device=device) as g1:
-        out = torch.empty(V1, dtype=torch.int32, device=dev)
-        g1.run(5, out=out)
-    rep["C1"] = quality_entry(s1, d1, out, dict(max_iter=5, vertices=V1, edges=int(s1.numel())))
+        lab1 = g1.run(5)
+        rep["C1"] = quality_entry(g1, lab1, dict(max_iter=5, vertices=V1, edges=int(z["src"].size)))
     c2 = CONFIGS["C2"]
     s2, d2 = gfa.gen_sbm(c2["V"], c2["blocks"], c2["m"], seed=c2["seed"], device=device)
     with gfa.Graph(s2, d2, c2["V"], device=device) as g2:
-        out = torch.empty(c2["V"], dtype=torch.int32, device=dev)
-        g2.run(MAX_ITER, out=out)
-    extra = dict(max_iter=MAX_ITER)
-    try:
-        from sklearn.metrics import normalized_mutual_info_score as nmi
-        truth = np.minimum(np.arange(c2["V"]) // (c2["V"] // c2["blocks"]), c2["blocks"] - 1)
-        extra["nmi_vs_planted_blocks"] = round(float(nmi(truth, out.cpu().numpy())), 4)
-    except ImportError:
-        extra["nmi_vs_planted_blocks"] = None
-    rep["C2"] = quality_entry(s2, d2, out, extra)
-    del s2, d2
+        del s2, d2
+        lab2 = g2.run(MAX_ITER)
+        extra = dict(max_iter=MAX_ITER)
+        try:
+            from sklearn.metrics import normalized_mutual_info_score as nmi
+            truth = np.minimum(np.arange(c2["V"]) // (c2["V"] // c2["blocks"]), c2["blocks"] - 1)
+            extra["nmi_vs_planted_blocks"] = round(float(nmi(truth, lab2)), 4)
+        except ImportError:
+            extra["nmi_vs_planted_blocks"] = None
+        rep["C2"] = quality_entry(g2, lab2, extra)
     return rep
 
 
@@ -327,9 +300,7 @@ def main():
     keep_host = world == 1 and not args.no_cpu_baseline
     if keep_host:
         src_np, dst_np = src.cpu().numpy(), dst.cpu().numpy()
-    if rank != 0 or args.no_quality:
-        del src, dst     # rank 0 keeps the edge list for the modularity report
-        src = dst = None
+    del src, dst
     torch.cuda.empty_cache()
 
     progress(f"{config_id}: built (arcs {info['arcs']}), warm-up")
@@ -394,9 +365,7 @@ def main():
     # partition quality of the labels of that call (rank 0: the full dense vector)
     quality = None
     if rank == 0 and not args.no_quality:
-        quality = dict(bench_graph=quality_entry(src, dst, out, dict(max_iter=MAX_ITER, config_id=config_id)))
-        del src, dst
-        torch.cuda.empty_cache()
+        quality = dict(bench_graph=quality_entry(g, out, dict(max_iter=MAX_ITER, config_id=config_id)))
 
     progress("serialized breakdown")
     # ---- breakdown: supersteps 2..10 again with the tally kernels serialized on one

@@ -70,6 +70,14 @@ class LpaGraphInfo(ctypes.Structure):
         return d
 
 
+class LpaQualitySummary(ctypes.Structure):
+    _fields_ = [("n_communities", ctypes.c_int64), ("intra_arcs", ctypes.c_int64), ("arcs", ctypes.c_int64),
+                ("degree_term", ctypes.c_double), ("modularity", ctypes.c_double)]
+
+    def to_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class LpaOutlierSummary(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int64) for k in (
         "n_groups", "k", "threshold", "n_flagged", "n_communities", "n_communities_flagged",
@@ -101,6 +109,7 @@ SIGNATURES = {
     "lpa_outlier": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                    _i64p, _i64p, _i32p, _u8p, ctypes.POINTER(LpaOutlierSummary)]),
     "lpa_degrees": (ctypes.c_int, [_vp, _i32p]),
+    "lpa_quality": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, _vp]),
     "lpa_loopback_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_vp)]),
     "lpa_loopback_abort": (None, [_vp]),
     "lpa_loopback_destroy": (None, [_vp]),
@@ -147,7 +156,8 @@ def load():
         import torch  # noqa: F401
     except ImportError:
         pass
-    lib = ctypes.CDLL(LIB_PATH)
+    # LPA_LIB_PATH: a diagnostic build of the same library (csrc/Makefile `trace`)
+    lib = ctypes.CDLL(os.environ.get("LPA_LIB_PATH") or LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

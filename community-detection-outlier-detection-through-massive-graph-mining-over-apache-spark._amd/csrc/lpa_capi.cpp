@@ -86,7 +86,7 @@ void destroy(lpa_graph* g) {
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
                   g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best,
-                  g->gbits, g->ugc, g->umx, g->ulist2, g->gdec};
+                  g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
@@ -491,6 +491,15 @@ int lpa_outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, i
   LPA_HIP(hipSetDevice(g->device));
   return outlier(g, labels, labels_on_device, mode, sub_iter, size_hist, incident, sub_labels, flags,
                  summary);
+}
+
+int lpa_quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, lpa_quality_summary* out) {
+  if (!g || !out || (!labels && g->V > 0)) {
+    set_error("null handle, labels or output");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  return quality(g, labels, labels_on_device, out);
 }
 
 int lpa_degrees(lpa_graph* g, int32_t* deg_out) {

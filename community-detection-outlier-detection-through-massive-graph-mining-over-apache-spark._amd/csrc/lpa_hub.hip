@@ -207,6 +207,7 @@ __global__ __launch_bounds__(256) void k_hub_decide(int64_t h_end, const int64_t
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t stride = (int64_t)gridDim.x * 4;
   const int32_t G = gsel[0];
+  const bool on = gsel[1] != 0;  // off: k_lpa_units_giant counted nothing, every row is listed
   for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < h_end; h += stride) {
     const int64_t u0 = uoff[h];
     const int nu = (int)(uoff[h + 1] - u0);
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(256) void k_hub_decide(int64_t h_end, const int64_t
       sg += __shfl_xor(sg, off, 64);
       sm += __shfl_xor(sm, off, 64);
     }
-    if (sg > sm) {
+    if (on && sg > sm) {
       if (lane == 0) {
         Ln[h] = G;
         wcount[h] = -1;

@@ -195,7 +195,8 @@ struct lpa_graph {
   // replicated neighbour labels (GraphX ReplicatedVertexView analogue):
   // al[i] = L_cur[col[i]]; kept current by scatter (few changes) or rebuild
   int32_t* al = nullptr;        // [arcs]
-  uint32_t* gbits = nullptr;    // [vpad / 32] rebuild: bit u = (L[u] == L[0]), the giant label
+  uint32_t* gbits = nullptr;    // [vpad / 32] rebuild: bit u = (L[u] == G), the giant label
+  int32_t* gword = nullptr;     // [2] G of the last refreshed vector (k_giant_pick), worth-trying flag
   int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
   uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])
   // per-superstep change bookkeeping (device)
@@ -314,5 +315,6 @@ int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool 
 int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
             int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
             uint8_t* flags, lpa_outlier_summary* summary);
+int quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, lpa_quality_summary* out);
 
 }  // namespace lpa

@@ -614,9 +614,9 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   int64_t i = (int64_t)blockIdx.x * 4 + w;   // work item: row br.row(i)
   if (i >= br.n) return;  // no block-level barriers in this kernel
   for (int k = lane; k < kCap; k += 64) tab[k] = 0ull;  // only waves with rows clear
-  // gsel (label-dense supersteps): the label vector this superstep reads; its slot 0
-  // is the top hub, whose label is the giant label
-  const bool giant = gsel != nullptr;
+  // gsel (label-dense supersteps): the giant-label word of the labels this superstep
+  // reads (k_giant_pick: label, worth trying)
+  const bool giant = gsel != nullptr && gsel[1] != 0;
   const u32 G = giant ? (u32)gsel[0] : 0u;
   RowSpan s0 = row_span(rp, br, i), s1 = row_span(rp, br, i + stride), s2 = row_span(rp, br, i + 2 * stride);
   u32 ra[NC], rb[NC], rc[NC];
@@ -683,8 +683,8 @@ __global__ __launch_bounds__(64 * kBlockWaves) void k_lpa_block(const int64_t* _
   for (int i = threadIdx.x; i < kSlots; i += kT) tab[i] = 0ull;
   if (threadIdx.x < kGB) ghist[threadIdx.x] = 0u;
   if (threadIdx.x < 2) gcnt[threadIdx.x] = gmax[threadIdx.x] = 0u;
-  // gsel (label-dense supersteps): G = the top hub's current label (giant_count)
-  const bool giant = gsel != nullptr;
+  // gsel (label-dense supersteps): the giant-label word (k_giant_pick; giant_count)
+  const bool giant = gsel != nullptr && gsel[1] != 0;
   const u32 G = giant ? (u32)gsel[0] : 0u;
   __syncthreads();
   int rpar = 0;  // parity of the rows this block has tallied
@@ -843,7 +843,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
   // gsel (superstep 2, rows of > 8 arcs): a chunk whose every row is decided for the
   // giant label (its exact count above each of the row's kGB label-hash buckets of
   // other votes, as giant_decide) skips the peel / sort
-  const bool giant = G >= 16 && gsel != nullptr;
+  const bool giant = G >= 16 && gsel != nullptr && gsel[1] != 0;
   const u32 Gl = giant ? (u32)gsel[0] : 0u;
   u32* hg = &ghist_all[w][(lane / G) * kGB];
   const int gj = lane & (G - 1);   // G >= kGB when giant: lane gj < kGB owns bucket gj
@@ -1072,6 +1072,7 @@ __global__ __launch_bounds__(256) void k_lpa_units_giant(const int32_t* __restri
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0) *ndec = 0;
+  if (gsel[1] == 0) return;  // no giant label worth trying: k_hub_decide lists every unit
   u32* hist = hist_all[w];
   hist[lane] = 0u;
   const u32 G = (u32)gsel[0];
@@ -1603,12 +1604,45 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
 // stays in L2 (2 MB at C3 against the 64 MB label vector) -- and reads the label
 // vector only for the columns whose bit is clear.  One ballot per 64 slots; lanes
 // 0..7 store the wave's eight 64-bit words (64 contiguous bytes).
+// The giant-label candidate of a label vector: the most frequent label among the
+// kPickK highest-degree vertices (degree ranks k < kPickK; at P > 1 rank k lives at slot
+// (k mod P) S + k / P), and whether it holds >= 1/5 of them (gword[1]: the tallies'
+// giant step is worth trying).  On R-MAT and Chung-Lu (oracle, scale 21-22) that label
+// is the degree-weighted mode of the whole vector in every superstep -- the top hub's
+// own label is not (Chung-Lu superstep 2: the mode holds 43 % of the arcs' columns, the
+// top hub's label 0.3 %).  One block, a 2K-slot LDS table.  The choice of G only
+// affects speed: every use of it is exact for any G.
+constexpr int kPickK = 1024;
+__global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__ L, int64_t n_real, int64_t S,
+                                                     int P, int32_t* __restrict__ gword) {
+  __shared__ u64 tab[2 * kPickK];
+  __shared__ u64 wbest[kPickK / 64];
+  const int t = threadIdx.x;
+  tab[t] = 0ull;
+  tab[t + kPickK] = 0ull;
+  __syncthreads();
+  const int64_t n = n_real < kPickK ? n_real : kPickK;
+  if (t < n) lds_insert(tab, 32 - 11, 2 * kPickK - 1, (u32)L[(int64_t)(t % P) * S + t / P], 1u);
+  __syncthreads();
+  const u64 b = wave_max_u64(umax64(tab[t], tab[t + kPickK]));
+  if ((t & 63) == 0) wbest[t >> 6] = b;
+  __syncthreads();
+  if (t == 0) {
+    u64 m = 0ull;
+#pragma unroll
+    for (int k = 0; k < kPickK / 64; ++k) m = umax64(m, wbest[k]);
+    gword[0] = (int32_t)(~(u32)m);
+    gword[1] = n > 0 && 5 * (int64_t)(m >> 32) >= n ? 1 : 0;
+  }
+}
+
 template <bool kIfWanted>
 __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __restrict__ counters, int64_t thr,
                                                     const int32_t* __restrict__ L, int64_t n,
+                                                    const int32_t* __restrict__ gword,
                                                     unsigned long long* __restrict__ bits) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
-  const int32_t G = L[0];
+  const int32_t G = gword[0];
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t g0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 512; g0 < n; g0 += nw * 512) {
@@ -1651,7 +1685,8 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
                                                          int64_t arcs, const int32_t* __restrict__ Ln,
                                                          int32_t nhot, int32_t* __restrict__ al,
                                                          int slice_lg, int hot_lg, int hb_lg,
-                                                         const uint32_t* __restrict__ gbits, int64_t nbits) {
+                                                         const uint32_t* __restrict__ gbits, int64_t nbits,
+                                                         const int32_t* __restrict__ gword) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   __shared__ u32 hot[kHotLabelsSingle];
   u32* s_cnt = &hot[kHotLabelsSingle - 1];   // beyond the bit words; labels mode refills it
@@ -1672,7 +1707,7 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
   if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(s_cnt, (u32)cnt);
   __syncthreads();
   const bool bits = 2 * (int64_t)*s_cnt >= nhb && nhb > 0;  // uniform: the same data in every block
-  const int32_t G = Ln[0];
+  const int32_t G = gword[0];
   if (!bits) {
     __syncthreads();
     for (int i = threadIdx.x; i < nhot; i += 1024)
@@ -1931,10 +1966,10 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // peel rounds of the row bins before a chunk is sorted: none in the label-dense
   // supersteps (measured best of 0/1/2/3 at C3), kPeelSortAfter otherwise
   const int sort_after = g->since_reset < kDenseSupersteps ? 0 : kPeelSortAfter;
-  // superstep 2 (the label-dense one after the column-run superstep 1): the wave and
-  // block tallies try the giant label first (giant_decide); gsel = the label vector
-  // the tally reads (its slot 0 is the top hub)
-  const int32_t* gsel = g->since_reset == 1 ? Lc : nullptr;
+  // supersteps 2 and 3 (the label-dense ones after the column-run superstep 1): the
+  // tallies try the giant label first (giant_decide); gsel = its word, picked by the
+  // previous superstep's refresh from the labels this one reads
+  const int32_t* gsel = (g->since_reset == 1 || g->since_reset == 2) ? g->gword : nullptr;
   // wide tier (rows 4096 < deg <= 8192: 16 waves, a 16K-slot table, one block per CU)
   auto launch_block_wide = [&](hipStream_t st) -> int {
     const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;
@@ -2080,6 +2115,12 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
 int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
                    const unsigned long long* ctr) {
   hipStream_t s = g->stream;
+  // the giant label of the refreshed vector: the rebuild's bits below and the next
+  // superstep's tallies (launch_tally's gsel) read it
+  if (g->V > 0) {
+    hipLaunchKernelGGL(k_giant_pick, dim3(1), dim3(kPickK), 0, s, L, g->V, g->slice, g->nranks, g->gword);
+    LPA_HIP(hipGetLastError());
+  }
   const auto pow2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
   const bool ranked = g->nranks > 1 && pow2(g->nranks) && pow2(g->slice) && g->nranks <= kHotLabels &&
                       g->slice >= kHotLabels / g->nranks;
@@ -2102,16 +2143,16 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     const int64_t ngrp = (g->vpad + 511) / 512;
     if (if_wanted)
       hipLaunchKernelGGL(k_giant_bits<true>, dim3(cap_grid((ngrp + 3) / 4, 4096)), dim3(256), 0, s, ctr, thr, L,
-                         g->vpad, (unsigned long long*)g->gbits);
+                         g->vpad, g->gword, (unsigned long long*)g->gbits);
     else
       hipLaunchKernelGGL(k_giant_bits<false>, dim3(cap_grid((ngrp + 3) / 4, 4096)), dim3(256), 0, s, ctr, thr, L,
-                         g->vpad, (unsigned long long*)g->gbits);
+                         g->vpad, g->gword, (unsigned long long*)g->gbits);
     LPA_HIP(hipGetLastError());
     // ranked without a usable bit share: nbits 0 keeps every block in labels mode
     const int64_t nbits = (ranked && hb_lg == 0) ? 0 : g->vpad;
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
-                     g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits)
+                     g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword)
     if (if_wanted) {
       if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
     } else {

@@ -356,7 +356,115 @@ int bad_labels(unsigned long long n, int64_t V) {
   return LPA_EINVAL;
 }
 
+// ---- partition quality (lpa_quality): modularity on the symmetrised multigraph ----
+// arcs inside a community: 2 per input edge with L[s] == L[d] (a self-loop's two arcs)
+__global__ __launch_bounds__(256) void k_q_intra(const int32_t* __restrict__ s, const int32_t* __restrict__ d,
+                                                 int64_t m, const int32_t* __restrict__ L, int64_t V,
+                                                 unsigned long long* __restrict__ acc) {
+  unsigned long long c = 0;
+  GRID_STRIDE(e, m) {
+    const u32 a = (u32)L[s[e]], b = (u32)L[d[e]];
+    c += (a == b && a < (u32)V) ? 2ull : 0ull;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(acc, c);
+}
+// D[l] += deg(v) for L[v] = l (out-of-range labels counted in *bad)
+__global__ __launch_bounds__(256) void k_q_degsum(const int32_t* __restrict__ L, const int32_t* __restrict__ deg,
+                                                  int64_t V, unsigned long long* __restrict__ D,
+                                                  unsigned long long* __restrict__ bad) {
+  GRID_STRIDE(v, V) {
+    const u32 l = (u32)L[v];
+    if (l < (u32)V) {
+      if (deg[v]) atomicAdd(&D[l], (unsigned long long)deg[v]);
+    } else {
+      atomicAdd(bad, 1ull);
+    }
+  }
+}
+// communities (labels held by >= 1 vertex: size from k_histogram) and sum_c D_c^2
+// (exact: D_c <= 2m < 2^33, sum <= (2m)^2 < 2^66 -- kept as two 64-bit halves)
+__global__ __launch_bounds__(256) void k_q_sum(const int32_t* __restrict__ size, const unsigned long long* __restrict__ D,
+                                               int64_t V, unsigned long long* __restrict__ acc) {
+  unsigned long long n = 0, lo = 0, hi = 0;
+  GRID_STRIDE(l, V) {
+    n += size[l] > 0 ? 1ull : 0ull;
+    const unsigned long long x = D[l];
+    const unsigned long long sq_lo = x * x, sq_hi = __umul64hi(x, x);
+    const unsigned long long t = lo + sq_lo;
+    hi += sq_hi + (t < lo ? 1ull : 0ull);
+    lo = t;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    n += __shfl_xor(n, off, 64);
+    const unsigned long long olo = __shfl_xor(lo, off, 64), ohi = __shfl_xor(hi, off, 64);
+    const unsigned long long t = lo + olo;
+    hi += ohi + (t < lo ? 1ull : 0ull);
+    lo = t;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (n) atomicAdd(&acc[0], n);
+    // 128-bit accumulate: low half with carry into the high half
+    const unsigned long long old = atomicAdd(&acc[1], lo);
+    const unsigned long long carry = (old + lo < old) ? 1ull : 0ull;
+    if (hi + carry) atomicAdd(&acc[2], hi + carry);
+  }
+}
+
 }  // namespace
+
+// Community count and Newman modularity of a labelling (dense ids) on the handle's
+// symmetrised multigraph: A = 2m arcs, Q = intra / A - sum_c (D_c / A)^2 with D_c the
+// degree sum of community c -- integer sums on the device, one host round trip.
+int quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, lpa_quality_summary* out) {
+  hipStream_t s = g->stream;
+  const int64_t V = g->V, m = g->m;
+  lpa_quality_summary q = {};
+  q.arcs = 2 * m;
+  if (V == 0) {
+    *out = q;
+    return LPA_OK;
+  }
+  Scratch sc(s);
+  int32_t *L = nullptr, *size = nullptr;
+  unsigned long long *D = nullptr, *acc = nullptr;
+  LPA_TRY(sc.get(&L, V));
+  LPA_TRY(sc.get(&size, V));
+  LPA_TRY(sc.get(&D, V));
+  LPA_TRY(sc.get(&acc, 8));
+  if (labels_on_device) {
+    LPA_HIP(hipMemcpyAsync(L, labels, sizeof(int32_t) * V, hipMemcpyDeviceToDevice, s));
+  } else {
+    LPA_TRY(ensure_pin(g, (size_t)4 * (size_t)V));
+    par_copy(g->host_pin, labels, sizeof(int32_t) * V);
+    LPA_HIP(hipMemcpyAsync(L, g->host_pin, sizeof(int32_t) * V, hipMemcpyHostToDevice, s));
+  }
+  LPA_HIP(hipMemsetAsync(size, 0, sizeof(int32_t) * V, s));
+  LPA_HIP(hipMemsetAsync(D, 0, sizeof(unsigned long long) * V, s));
+  LPA_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long) * 8, s));
+  hipLaunchKernelGGL(k_histogram, dim3(grid_bh(V)), dim3(256), 0, s, L, V, size, acc + 4);
+  LPA_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_q_degsum, dim3(grid_bh(V)), dim3(256), 0, s, L, g->deg, V, D, acc + 5);
+  LPA_HIP(hipGetLastError());
+  if (m > 0) {
+    hipLaunchKernelGGL(k_q_intra, dim3(grid_bh(m)), dim3(256), 0, s, g->e_src, g->e_dst, m, L, V, acc + 3);
+    LPA_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_q_sum, dim3(grid_bh(V)), dim3(256), 0, s, size, D, V, acc);
+  LPA_HIP(hipGetLastError());
+  unsigned long long h[8];
+  LPA_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  if (h[4] || h[5]) return bad_labels(h[4] ? h[4] : h[5], V);
+  q.n_communities = (int64_t)h[0];
+  q.intra_arcs = (int64_t)h[3];
+  const double A = (double)q.arcs;
+  const double s2 = ((double)h[2] * 18446744073709551616.0 + (double)h[1]) / (A * A);
+  q.degree_term = A > 0 ? s2 : 0.0;
+  q.modularity = A > 0 ? (double)q.intra_arcs / A - s2 : 0.0;
+  *out = q;
+  return LPA_OK;
+}
 
 // Host round trips: the first call on a handle builds its distinct edge set (one);
 // then none in L1 before the results are copied out, one in L2 (the size of E',

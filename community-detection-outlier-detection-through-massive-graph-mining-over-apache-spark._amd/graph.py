@@ -212,6 +212,24 @@ class Graph:
                     summary=summ.to_dict())
 
 
+    def quality(self, labels) -> dict:
+        """Community count and modularity of a labelling (host array or device tensor of
+        dense-id labels) on this graph's symmetrised multigraph (lpa_quality)."""
+        q = _lib.LpaQualitySummary()
+        if _is_device_tensor(labels):
+            if labels.numel() != self.num_vertices:
+                raise ValueError(f"labels must hold {self.num_vertices} entries")
+            lab, ptr, on_dev = labels.contiguous(), None, 1
+            ptr = lab.data_ptr()
+        else:
+            lab = np.ascontiguousarray(labels, dtype=np.int32)
+            if lab.shape != (self.num_vertices,):
+                raise ValueError(f"labels must have shape ({self.num_vertices},)")
+            ptr, on_dev = lab.ctypes.data, 0
+        _lib.check(self._lib.lpa_quality(self._handle(), ptr, on_dev, ctypes.byref(q)))
+        return q.to_dict()
+
+
 class Loopback:
     """In-process collective group of ``nranks`` handles on one device (the
     multi-GPU exchange rehearsed on one GPU).  Drive each rank's Graph from its own

@@ -211,6 +211,22 @@ int lpa_outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, i
                 int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
                 uint8_t* flags, lpa_outlier_summary* summary);
 
+/* Partition quality of a labelling (dense ids, values in [0, V)) on the handle's
+ * symmetrised multigraph, the graph labelPropagation votes on (A = 2m arcs: every
+ * input edge both ways, a self-loop as two arcs at its vertex):
+ *   modularity = intra_arcs / A - degree_term,  degree_term = sum_c (D_c / A)^2,
+ * D_c the degree sum of community c, plus the community count (the distinct-label
+ * count of Graphframes.py:85).  Exact integer sums on the device.  North-star
+ * "community-count / modularity agreement" report; not a GraphFrames call. */
+typedef struct lpa_quality_summary {
+  int64_t n_communities;
+  int64_t intra_arcs;
+  int64_t arcs;
+  double degree_term;
+  double modularity;
+} lpa_quality_summary;
+int lpa_quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, lpa_quality_summary* out);
+
 /* Symmetrised degree of every vertex (dense ids), host output. */
 int lpa_degrees(lpa_graph* g, int32_t* deg_out);
 

@@ -540,3 +540,34 @@ def test_frontier_from_superstep_2_with_block_rows(gfa, oracle, seed):
         assert bad.size == 0, f"superstep {t + 1}: {bad.size} differ, first {bad[:5]}"
     with gfa.Graph(s, d, V) as g:
         assert np.array_equal(g.run(8), hist[7])
+
+
+def _modularity_np(V, s, d, lab):
+    """Newman modularity on the symmetrised multigraph (numpy restatement)."""
+    A = 2 * s.size
+    intra = 2 * int((lab[s] == lab[d]).sum())
+    deg = np.bincount(s, minlength=V) + np.bincount(d, minlength=V)
+    D = np.bincount(lab, weights=deg, minlength=V)
+    return intra / A - float(((D / A) ** 2).sum()), intra
+
+
+@pytest.mark.parametrize("graph", ["r9", "rmat16", "mix"])
+def test_quality_matches_numpy(gfa, golden, graph):
+    """lpa_quality (community count, intra arcs, modularity) against a numpy
+    restatement, on the labels the GPU computes (maxIter 5) and on L0."""
+    if graph == "r9":
+        V, s, d = golden["ids"].size, golden["src"], golden["dst"]
+    elif graph == "rmat16":
+        ts, td = gfa.gen_rmat(16, 16, seed=2)
+        V, s, d = 1 << 16, ts.cpu().numpy(), td.cpu().numpy()
+    else:
+        V, s, d = degree_mix(4)
+    with gfa.Graph(s, d, V) as g:
+        for lab in (g.run(5), np.arange(V, dtype=np.int32)):
+            q = g.quality(lab)
+            Q, intra = _modularity_np(V, s.astype(np.int64), d.astype(np.int64), lab.astype(np.int64))
+            assert q["n_communities"] == np.unique(lab).size
+            assert q["intra_arcs"] == intra and q["arcs"] == 2 * s.size
+            assert abs(q["modularity"] - Q) < 1e-9
+        with pytest.raises(ValueError, match="outside"):
+            g.quality(np.full(V, V, dtype=np.int32))
