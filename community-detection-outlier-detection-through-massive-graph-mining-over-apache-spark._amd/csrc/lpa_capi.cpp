@@ -86,7 +86,8 @@ void destroy(lpa_graph* g) {
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
                   g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best,
-                  g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword};
+                  g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword, g->al0, g->abits,
+                  g->glist};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
@@ -307,6 +308,7 @@ int lpa_exchange_put(lpa_graph* g, const int32_t* full_in) {
                          g->stream));
   g->prev_delta_ok = false;
   LPA_TRY(rebuild_arc_labels(g));
+  g->al_pending = false;
   LPA_TRY(frontier_all(g, g->par));
   LPA_HIP(hipStreamSynchronize(g->stream));
   return LPA_OK;
@@ -359,6 +361,7 @@ int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t*
   // parity): its counters (zeroed here -- the caller-driven path runs no scatter of
   // its own), its arc mode, and the next superstep's flags / mode
   const int pp = g->par ^ 1;
+  LPA_TRY(ensure_al(g));   // the scatter below updates al in place
   LPA_HIP(hipMemsetAsync(g->counters + 4 * pp, 0, sizeof(unsigned long long) * 2, s));
   const int32_t* Lc = g->lab[g->cur ^ 1];
   int32_t* Ln = g->lab[g->cur];

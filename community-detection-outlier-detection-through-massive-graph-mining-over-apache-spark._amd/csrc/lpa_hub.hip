@@ -191,24 +191,33 @@ __device__ __forceinline__ void queue_row(int64_t h, int T, int nu, int lane,
   }
 }
 
-// Superstep 2's giant-label decision for the unit-tallied rows [0, h_end) (after
+// Superstep 2's giant-label decision for the hub rows [0, h_end) (after
 // k_lpa_units_giant): row h's G votes S_g = sum of its units' ugc, and any other
 // label's row count is at most S_m = sum of its units' umx (each unit's fullest
-// bucket).  S_g > S_m: G is the strict mode -- written, wcount[h] = -1 (the combine's
-// classify / enqueue skip the row).  Otherwise wcount[h] = 0 and the row's units are
-// appended to ulist2 (count *ndec) for the exact unit tally.  One wave per row.
+// bucket).  S_g > S_m: G is the strict mode and is written.  Otherwise the row is
+// tallied exactly: a unit-tallied row (h < hb2) gets wcount[h] = 0 and its units in
+// ulist2 (count ndec[0]), a block-tier row (h >= hb2, <= 16 units) goes to
+// glist (count ndec[2]); settled unit-tallied rows get wcount[h] = -1 (the combine's
+// classify / enqueue skip them).  ndec[3] = 1 when G is not worth trying: nothing is
+// decided and the exact kernels take their whole ranges (ndec[3] is their "fr_all").
+// Unit-tallied rows: a wave per row; block-tier rows: a lane per row, one list atomic
+// per wave.
 __global__ __launch_bounds__(256) void k_hub_decide(int64_t h_end, const int64_t* __restrict__ uoff,
                                                     const uint32_t* __restrict__ ugc,
                                                     const uint32_t* __restrict__ umx,
                                                     const int32_t* __restrict__ gsel,
                                                     int32_t* __restrict__ Ln, int32_t* __restrict__ wcount,
-                                                    int32_t* __restrict__ ulist2, int32_t* __restrict__ ndec) {
+                                                    int32_t* __restrict__ ulist2, int32_t* __restrict__ ndec,
+                                                    int64_t hb2, int32_t* __restrict__ glist) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t stride = (int64_t)gridDim.x * 4;
   const int32_t G = gsel[0];
-  const bool on = gsel[1] != 0;  // off: k_lpa_units_giant counted nothing, every row is listed
-  for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < h_end; h += stride) {
+  const bool on = gsel[1] != 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) ndec[3] = on ? 0 : 1;
+  if (!on) return;  // uniform: k_lpa_units_giant counted nothing
+  const int64_t ha = hb2 < h_end ? hb2 : h_end;
+  for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < ha; h += stride) {
     const int64_t u0 = uoff[h];
     const int nu = (int)(uoff[h + 1] - u0);
     u64 sg = 0, sm = 0;
@@ -220,7 +229,7 @@ __global__ __launch_bounds__(256) void k_hub_decide(int64_t h_end, const int64_t
       sg += __shfl_xor(sg, off, 64);
       sm += __shfl_xor(sm, off, 64);
     }
-    if (on && sg > sm) {
+    if (sg > sm) {
       if (lane == 0) {
         Ln[h] = G;
         wcount[h] = -1;
@@ -229,11 +238,28 @@ __global__ __launch_bounds__(256) void k_hub_decide(int64_t h_end, const int64_t
       int base = 0;
       if (lane == 0) {
         wcount[h] = 0;
-        base = atomicAdd(ndec, nu);
+        base = atomicAdd(&ndec[0], nu);
       }
       base = __shfl(base, 0, 64);
       for (int j = lane; j < nu; j += 64) ulist2[base + j] = (int32_t)(u0 + j);
     }
+  }
+  // block-tier rows: a lane per row
+  for (int64_t h0 = ha + ((int64_t)blockIdx.x * 4 + w) * 64; h0 < h_end; h0 += stride * 64) {
+    const int64_t h = h0 + lane;
+    bool open = false;
+    if (h < h_end) {
+      const int64_t u0 = uoff[h];
+      const int nu = (int)(uoff[h + 1] - u0);
+      u32 sg = 0, sm = 0;
+      for (int j = 0; j < nu; ++j) {
+        sg += ugc[u0 + j];
+        sm += umx[u0 + j];
+      }
+      if (sg > sm) Ln[h] = G;
+      else open = true;
+    }
+    wave_append(open, glist, &ndec[2], (int32_t)h, lane);
   }
 }
 
@@ -1182,7 +1208,8 @@ int build_hub_tables(lpa_graph* g, const int32_t* deg_own) {
 int launch_hub_decide(lpa_graph* g, int32_t* Lown, int64_t h_end, const int32_t* gsel) {
   if (h_end <= 0) return LPA_OK;
   hipLaunchKernelGGL(k_hub_decide, dim3(grid_cap((h_end + 3) / 4, 2048)), dim3(256), 0, g->stream, h_end,
-                     g->hub_uoff, g->ugc, g->umx, gsel, Lown, g->hub_wcount, g->ulist2, g->gdec);
+                     g->hub_uoff, g->ugc, g->umx, gsel, Lown, g->hub_wcount, g->ulist2, g->gdec,
+                     block_rows_begin(g), g->glist);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }

@@ -102,7 +102,9 @@ struct lpa_graph {
   // bucket path (2); 4 streams = the 4 hardware queues of a process
   hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
-  hipEvent_t ev_fork2 = nullptr, ev_join2[3] = {nullptr, nullptr, nullptr};  // hub combine tail, block tiers
+  // hub combine tail, block tiers; ev_join2[2]: superstep 2's giant decision is done (the
+  // block tiers on the fourth stream wait for it)
+  hipEvent_t ev_fork2 = nullptr, ev_join2[3] = {nullptr, nullptr, nullptr};
   int32_t rank = 0, nranks = 1;
   // label-exchange collective backend (P > 1): RCCL communicator (one process per
   // GPU) or the in-process loopback group (P handles on one device, one host thread
@@ -149,7 +151,8 @@ struct lpa_graph {
   uint32_t* ugc = nullptr;        // [n_segs] superstep 2: the unit's giant-label votes ...
   uint32_t* umx = nullptr;        // [n_segs] ... and its fullest other-label bucket (k_lpa_units_giant)
   int32_t* ulist2 = nullptr;      // [n_segs] units of the rows k_hub_decide could not settle
-  int32_t* gdec = nullptr;        // [2] their count, then a constant 0 (the list-mode "fr_all")
+  int32_t* gdec = nullptr;        // [4] their count, a constant 0 (the list-mode "fr_all"), the count of glist
+  int32_t* glist = nullptr;       // [n_hub] block-tier rows k_hub_decide could not settle (k_lpa_block's list)
   lpa::u64* scat = nullptr;       // [hub arcs] bucket-partitioned words
   int32_t* hub_wcount = nullptr;  // [n_hub] staged words of a queued row (0 otherwise)
   lpa::u64* hub_best = nullptr;   // [n_hub] reduced tally word (bucketed hubs)
@@ -195,8 +198,16 @@ struct lpa_graph {
   // replicated neighbour labels (GraphX ReplicatedVertexView analogue):
   // al[i] = L_cur[col[i]]; kept current by scatter (few changes) or rebuild
   int32_t* al = nullptr;        // [arcs]
+  // al0[i] = L0[col[i]] (label-independent: the dense id of the column), kept when
+  // superstep 1 runs by column runs.  A reset then leaves al stale (al_pending): the
+  // column-run superstep reads al0 and its refresh rebuilds al, or fills it from al0
+  // when it only scatters; any other first use copies al0 first (ensure_al).
+  int32_t* al0 = nullptr;       // [arcs] or nullptr
+  bool al_pending = false;
   uint32_t* gbits = nullptr;    // [vpad / 32] rebuild: bit u = (L[u] == G), the giant label
-  int32_t* gword = nullptr;     // [2] G of the last refreshed vector (k_giant_pick), worth-trying flag
+  int32_t* gword = nullptr;     // [4] G of the last refreshed vector (k_giant_pick), worth-trying flag,
+                                //     abits valid (bits-mode rebuild, no scatter since)
+  unsigned long long* abits = nullptr;  // [arcs / 64] bit i = (al[i] == G): the bits-mode rebuild's by-product
   int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
   uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])
   // per-superstep change bookkeeping (device)
@@ -282,6 +293,7 @@ int launch_hub_decide(lpa_graph* g, int32_t* Lown, int64_t h_end, const int32_t*
 bool block_mode_now(const lpa_graph* g);  // lpa_iter.hip
 int64_t block_rows_begin(const lpa_graph* g);  // first row of the block tiers (lpa_iter.hip)
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
+int ensure_al(lpa_graph* g);           // al valid (copies al0 after a lazy reset)
 int frontier_all(lpa_graph* g, int par);  // next tally of parity `par` takes every row
 
 // iteration (lpa_iter.hip)

@@ -1071,8 +1071,8 @@ __global__ __launch_bounds__(256) void k_lpa_units_giant(const int32_t* __restri
   __shared__ u32 hist_all[4][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ndec = 0;
-  if (gsel[1] == 0) return;  // no giant label worth trying: k_hub_decide lists every unit
+  if (blockIdx.x == 0 && threadIdx.x == 0) ndec[0] = ndec[2] = 0;  // unit list, block-row list
+  if (gsel[1] == 0) return;  // no giant label worth trying: k_hub_decide lists every row
   u32* hist = hist_all[w];
   hist[lane] = 0u;
   const u32 G = (u32)gsel[0];
@@ -1151,6 +1151,11 @@ struct BinBounds {
   int64_t b[LPA_NBINS + 1];
 };
 constexpr int kDiffQuads = 2048;
+// fcnt[] slot set by the row settle of a giant superstep (k_settle_*): the bin kernels
+// walk lists of the unsettled rows, but the diff scans every slot (settled rows may
+// have changed label)
+constexpr int kFcntSettled = LPA_NBINS + 1;
+static_assert(kFcntSettled < 16, "fcnt: 16 slots per parity");
 __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
                                               const int4* __restrict__ Ln4, int32_t* __restrict__ Lsync,
                                               int64_t s0, int64_t s1,
@@ -1177,7 +1182,7 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
     if (nch == 1) q_col[atomicAdd(&qn, 1)] = (int32_t)u;
     else if (nch > 1) flag_chunks(chflag, cch, u);
   };
-  if (flist != nullptr && *fr_all == 0) {
+  if (flist != nullptr && *fr_all == 0 && fcnt[kFcntSettled] == 0) {
     // a list holds at most its bin's rows, so the grid (sized for the slot range)
     // gives each thread <= 32 entries, inside the block's queue
     int64_t total = 0;
@@ -1274,7 +1279,7 @@ __global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rd
   __shared__ int32_t lpos[LPA_NBINS + 1];
   __shared__ int32_t gbase[LPA_NBINS + 1];
   __shared__ int64_t sbb[LPA_NBINS + 1];
-  if (blockIdx.x == 0 && threadIdx.x < LPA_NBINS + 1) fcnt_next[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 16) fcnt_next[threadIdx.x] = 0;  // + kFcntSettled
   if (*fr_all) return;  // uniform
   const bool units = (int64_t)blockIdx.x >= nblk_rows;
   const int64_t n = units ? nunits : S;   // flag arrays are padded to 16 bytes
@@ -1390,6 +1395,82 @@ __global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rd
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row settle from the arc giant bits (superstep 3: the full tally right after the
+// bits-mode rebuild of superstep 2).  A row's exact count of G votes is the popcount of
+// its abits range (bit i = al[i] == G); a strict majority makes G the row's mode
+// without reading one label.  Every row's dirty flag is WRITTEN (1: unsettled, a hub
+// row's units alike, so no stale flag survives), k_settle_commit switches the
+// superstep to list mode, and k_frontier_lists turns the flags into the bin lists
+// (block scans, no per-row atomics).  It applies only while *fr_all (every row due),
+// gword[1] (G worth trying) and gword[2] (abits match al), checked alike by every
+// block before k_settle_commit changes fr_all.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool settle_on(const int32_t* fr_all, const int32_t* gword) {
+  return *fr_all != 0 && gword[1] != 0 && gword[2] != 0;
+}
+
+__device__ __forceinline__ unsigned long long range_mask(int64_t x, int64_t w0, int64_t w1, int64_t a, int64_t b) {
+  unsigned long long m = ~0ull;
+  if (x == w0) m &= ~0ull << (a & 63);
+  if (x == w1) m &= ~0ull >> (63 - ((b - 1) & 63));
+  return m;
+}
+
+// hub rows [0, n_hub) (> 1024 arcs): one wave per row
+__global__ __launch_bounds__(256) void k_settle_big(const int64_t* __restrict__ rp,
+                                                    const unsigned long long* __restrict__ abits, int64_t n_hub,
+                                                    const int32_t* __restrict__ fr_all,
+                                                    const int32_t* __restrict__ gword, int32_t* __restrict__ Ln,
+                                                    uint8_t* __restrict__ rdirty, uint8_t* __restrict__ udirty,
+                                                    const int64_t* __restrict__ uoff) {
+  if (!settle_on(fr_all, gword)) return;  // uniform
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int32_t G = gword[0];
+  for (int64_t v = (int64_t)blockIdx.x * 4 + w; v < n_hub; v += (int64_t)gridDim.x * 4) {
+    const int64_t a = rp[v], b = rp[v + 1];
+    const int64_t w0 = a >> 6, w1 = (b - 1) >> 6;
+    u32 c = 0;
+    for (int64_t x = w0 + lane; x <= w1; x += 64) c += (u32)__popcll(abits[x] & range_mask(x, w0, w1, a, b));
+    c = wave_sum_u32(c);
+    const bool settled = 2 * (int64_t)c > b - a;
+    if (lane == 0) {
+      if (settled) Ln[v] = G;
+      rdirty[v] = settled ? 0 : 1;
+    }
+    const uint8_t f = settled ? 0 : 1;
+    for (int64_t u = uoff[v] + lane; u < uoff[v + 1]; u += 64) udirty[u] = f;
+  }
+}
+
+// rows [r0, r1) (<= 1024 arcs, not isolated): a thread per row
+__global__ __launch_bounds__(256) void k_settle_rows(const int64_t* __restrict__ rp,
+                                                     const unsigned long long* __restrict__ abits, int64_t r0,
+                                                     int64_t r1, const int32_t* __restrict__ fr_all,
+                                                     const int32_t* __restrict__ gword, int32_t* __restrict__ Ln,
+                                                     uint8_t* __restrict__ rdirty) {
+  if (!settle_on(fr_all, gword)) return;  // uniform
+  const int32_t G = gword[0];
+  for (int64_t v = r0 + (int64_t)blockIdx.x * 256 + threadIdx.x; v < r1; v += (int64_t)gridDim.x * 256) {
+    const int64_t a = rp[v], b = rp[v + 1];
+    const int64_t w0 = a >> 6, w1 = (b - 1) >> 6;
+    u32 c = 0;
+    for (int64_t x = w0; x <= w1; ++x) c += (u32)__popcll(abits[x] & range_mask(x, w0, w1, a, b));
+    const bool settled = 2 * (int64_t)c > b - a;
+    if (settled) Ln[v] = G;
+    rdirty[v] = settled ? 0 : 1;
+  }
+}
+
+// the settled superstep runs in list mode over the unsettled rows; the diff scans all
+__global__ void k_settle_commit(int32_t* __restrict__ fr_all, const int32_t* __restrict__ gword,
+                                int32_t* __restrict__ fcnt) {
+  if (!settle_on(fr_all, gword)) return;
+  *fr_all = 0;
+  fcnt[kFcntSettled] = 1;
+}
+
 // rebuild al[] when the changed vertices touch more than `thr` arcs (host-set)
 __device__ __forceinline__ bool rebuild_wanted(const unsigned long long* counters, int64_t thr) {
   return (int64_t)counters[1] > thr;
@@ -1422,9 +1503,11 @@ static_assert(kSegArcs == 512, "unit of a position: (p - rp[row]) >> 9");
 // lanes (lane -> piece by a binary search over the inclusive piece prefix), so a
 // wave whose lanes hold runs of 17..256 positions writes them in parallel instead of
 // run after run with the whole wave.  Every lane of the wave must call it.
+// ab != nullptr: the arc giant bits are kept in step (bit p = (lab == G); no-return
+// 64-bit atomics, the positions of other columns share the words)
 __device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, const uint32_t* __restrict__ cpos,
                                              int32_t* __restrict__ al, bool all, const FrontierMarks& fm,
-                                             int lane) {
+                                             int lane, unsigned long long* __restrict__ ab, int32_t G) {
   const int k = (n + 15) >> 4;
   int incl = k;
 #pragma unroll
@@ -1459,6 +1542,11 @@ __device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, cons
           if (q + u < cnt) {
             al[p[u]] = lv;
             if (!all) fm.mark(p[u]);
+            if (ab) {
+              const unsigned long long bit = 1ull << (p[u] & 63);
+              if (lv == G) atomicOr(&ab[p[u] >> 6], bit);
+              else atomicAnd(&ab[p[u] >> 6], ~bit);
+            }
           }
       }
     }
@@ -1509,10 +1597,21 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
                                                     FrontierMarks fm, int32_t* __restrict__ fr_all_next,
                                                     int frontier, int64_t fr_thr,
                                                     int32_t* __restrict__ Lold,
-                                                    const int32_t* __restrict__ col_fold, int64_t arcs) {
+                                                    const int32_t* __restrict__ col_fold, int64_t arcs,
+                                                    int32_t* __restrict__ gword,
+                                                    unsigned long long* __restrict__ abits) {
   // the next superstep's counters (the other parity; no memset launch)
   if (blockIdx.x == 0 && threadIdx.x < 2) counters_next[threadIdx.x] = 0ull;
   const bool rebuild = rebuild_wanted(counters, thr);
+  // the arc giant bits: kept in step by the scatter while valid (read before any block
+  // can clear the flag: the clear below only follows a plain folded rebuild)
+  // al changes here (scatter, or the plain folded rebuild): the arc giant bits go stale
+  // (keeping them in step cost 0.25 ms of 64-bit atomics in superstep 3, more than a
+  // settled superstep 4 would save)
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (!rebuild || col_fold)) gword[2] = 0;
+  unsigned long long* ab = nullptr;
+  const int32_t G = 0;
+  (void)abits;
   // The next superstep tallies every row after a rebuild, with the frontier off, or
   // when more than fr_thr arcs changed: then nearly every row has a changed neighbour
   // anyway (R-MAT superstep 3 -> 4: 1.5 % of arcs dirty, 88 % of the arcs in dirty
@@ -1541,7 +1640,7 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
         lab = Ln[u];
         Lold[u] = lab;  // frontier sync (after the join)
       }
-      scatter_runs(b, n, lab, cpos, al, all, fm, lane);
+      scatter_runs(b, n, lab, cpos, al, all, fm, lane, ab, G);
     }
   }
   uint4* __restrict__ flw = const_cast<uint4*>(chflag16);
@@ -1580,8 +1679,23 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
         // (after the join; every changed vertex with local arcs has a chunk 0)
         if (kk == 0) Lold[u] = lab;
       }
-      scatter_runs(b, n, lab, cpos, al, all, fm, lane);
+      scatter_runs(b, n, lab, cpos, al, all, fm, lane, ab, G);
     }
+  }
+}
+
+// After a lazy reset (al0) the first refresh that only scatters needs the L0 arc
+// labels in al first: copied here unless the rebuild that follows rewrites every arc.
+__global__ __launch_bounds__(256) void k_al_fill_unless_rebuild(const unsigned long long* __restrict__ counters,
+                                                                int64_t thr, const v4i* __restrict__ src,
+                                                                v4i* __restrict__ dst, int64_t arcs) {
+  if (rebuild_wanted(counters, thr)) return;
+  const int64_t n4 = arcs >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + q), dst + q);
+  if (blockIdx.x == 0 && threadIdx.x < (arcs & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    reinterpret_cast<int32_t*>(dst)[i] = reinterpret_cast<const int32_t*>(src)[i];
   }
 }
 
@@ -1592,8 +1706,9 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
                                                     int64_t thr, const int32_t* __restrict__ col,
                                                     int64_t arcs,
                                                     const int32_t* __restrict__ Ln,
-                                                    int32_t* __restrict__ al) {
+                                                    int32_t* __restrict__ al, int32_t* __restrict__ gword) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[2] = 0;  // no arc giant bits from this form
   rebuild_all(col, arcs, Ln, al);
 }
 
@@ -1631,7 +1746,9 @@ __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__
     u64 m = 0ull;
 #pragma unroll
     for (int k = 0; k < kPickK / 64; ++k) m = umax64(m, wbest[k]);
-    gword[0] = (int32_t)(~(u32)m);
+    const int32_t G = (int32_t)(~(u32)m);
+    if (G != gword[0]) gword[2] = 0;  // the arc giant bits are relative to the old G
+    gword[0] = G;
     gword[1] = n > 0 && 5 * (int64_t)(m >> 32) >= n ? 1 : 0;
   }
 }
@@ -1686,7 +1803,8 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
                                                          int32_t nhot, int32_t* __restrict__ al,
                                                          int slice_lg, int hot_lg, int hb_lg,
                                                          const uint32_t* __restrict__ gbits, int64_t nbits,
-                                                         const int32_t* __restrict__ gword) {
+                                                         int32_t* __restrict__ gword,
+                                                         unsigned long long* __restrict__ abits) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   __shared__ u32 hot[kHotLabelsSingle];
   u32* s_cnt = &hot[kHotLabelsSingle - 1];   // beyond the bit words; labels mode refills it
@@ -1708,6 +1826,9 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
   __syncthreads();
   const bool bits = 2 * (int64_t)*s_cnt >= nhb && nhb > 0;  // uniform: the same data in every block
   const int32_t G = gword[0];
+  // bits mode also writes the arc giant bits (abits: bit i = al[i] == G, one ballot per
+  // 64 arcs), which the next superstep's full tally settles rows from (k_settle_*)
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[2] = bits ? 1 : 0;
   if (!bits) {
     __syncthreads();
     for (int i = threadIdx.x; i < nhot; i += 1024)
@@ -1748,10 +1869,23 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
       for (int k = 0; k < 8; ++k) r[k] = lab(c[k]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
+      if (bits) {
+        unsigned long long mine = 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const unsigned long long m = __ballot(r[k] == G);
+          if (lane == k) mine = m;
+        }
+        if (lane < 8) abits[(base >> 6) + lane] = mine;
+      }
     } else {
       for (int k = 0; k < 8; ++k) {
         const int64_t i = base + k * 64 + lane;
-        if (i < arcs) al[i] = lab(col[i]);
+        const bool v = i < arcs;
+        const int32_t x = v ? lab(col[i]) : 0;
+        if (v) al[i] = x;
+        const unsigned long long m = __ballot(v && x == G);
+        if (bits && lane == 0 && base + k * 64 < arcs) abits[(base >> 6) + k] = m;
       }
     }
   }
@@ -1925,8 +2059,9 @@ int launch_first(lpa_graph* g, int32_t* Lown) {
   hipStream_t s = g->stream;
   LPA_TRY(launch_frontier_lists(g));
   const int64_t ntiles = (g->arcs + kRunTile - 1) / kRunTile;
-  hipLaunchKernelGGL(k_first_runs, dim3(cap_grid((ntiles + 3) / 4, 8192)), dim3(256), 0, s, g->al, g->crow,
-                     g->arcs, Lown, g->first_best);
+  // after a lazy reset the L0 arc labels are in al0 (al is rebuilt by the refresh)
+  hipLaunchKernelGGL(k_first_runs, dim3(cap_grid((ntiles + 3) / 4, 8192)), dim3(256), 0, s,
+                     g->al_pending ? g->al0 : g->al, g->crow, g->arcs, Lown, g->first_best);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_first_final, dim3(cap_grid((g->slice + 255) / 256, 4096)), dim3(256), 0, s, g->rp,
                      g->slice, g->first_best, Lown, g->hub_lcnt);
@@ -1943,8 +2078,26 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   const int64_t* bb = g->bin_begin;
   const int32_t* fr_all = g->fr_all + g->par;
   int32_t* fcnt = g->fcnt + 16 * g->par;
-  // frontier lists of this superstep (no-op when every row is tallied)
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 4], s));
+  // superstep 3: rows settled from the arc giant bits of superstep 2's rebuild (each
+  // kernel returns at once unless they are valid): the others' dirty flags, then the
+  // lists of this superstep are built from them in list mode
+  if (g->since_reset == 2 && g->abits && !block_mode_now(g)) {
+    if (g->n_hub > 0) {
+      hipLaunchKernelGGL(k_settle_big, dim3(cap_grid((g->n_hub + 3) / 4, 2048)), dim3(256), 0, s, g->rp, g->abits,
+                         g->n_hub, fr_all, g->gword, Lown, g->rdirty[g->par], g->udirty[g->par], g->hub_uoff);
+      LPA_HIP(hipGetLastError());
+    }
+    const int64_t r0 = g->n_hub, r1 = g->bin_begin[BIN_ISO];
+    if (r1 > r0) {
+      hipLaunchKernelGGL(k_settle_rows, dim3(cap_grid((r1 - r0 + 255) / 256, 8192)), dim3(256), 0, s, g->rp,
+                         g->abits, r0, r1, fr_all, g->gword, Lown, g->rdirty[g->par]);
+      LPA_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_settle_commit, dim3(1), dim3(1), 0, s, const_cast<int32_t*>(fr_all), g->gword, fcnt);
+    LPA_HIP(hipGetLastError());
+  }
+  // frontier lists of this superstep (no-op when every row is tallied)
   LPA_TRY(launch_frontier_lists(g));
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (!g->serial) {
@@ -1969,14 +2122,26 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // supersteps 2 and 3 (the label-dense ones after the column-run superstep 1): the
   // tallies try the giant label first (giant_decide); gsel = its word, picked by the
   // previous superstep's refresh from the labels this one reads
-  const int32_t* gsel = (g->since_reset == 1 || g->since_reset == 2) ? g->gword : nullptr;
+  const int32_t* gsel = (g->since_reset >= 1 && g->since_reset <= 3) ? g->gword : nullptr;
+  // superstep 2 in block mode: every hub row by giant counts first (k_lpa_units_giant
+  // over all units, k_hub_decide); only the rows it cannot settle are tallied exactly --
+  // block-tier rows by k_lpa_block from glist, the longer ones by their units
+  const bool giant_units = gsel != nullptr && block_mode_now(g);
+  // the block tiers' rows: in giant mode the undecided ones (glist, count gdec[2]; all
+  // of them when G was not worth trying: gdec[3] as "fr_all"), else the superstep's
+  // rows or frontier list
+  const int32_t* blist = giant_units ? g->glist : g->flist;
+  const int32_t* bcnt = giant_units ? g->gdec + 2 : fcnt;
+  const int32_t* ball = giant_units ? g->gdec + 3 : fr_all;
+  // (the block tiers' giant step is then done: no gsel for them)
+  const int32_t* bsel = giant_units ? nullptr : gsel;
   // wide tier (rows 4096 < deg <= 8192: 16 waves, a 16K-slot table, one block per CU)
   auto launch_block_wide = [&](hipStream_t st) -> int {
     const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;
     if (hl > h2) {
       hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, 1024)),
-                         dim3(kBlockMaxDeg2 / kSegArcs * 64), 0, st, g->rp, g->al, Lown, h2, hl, g->flist, fcnt,
-                         fr_all, pmax, gsel);
+                         dim3(kBlockMaxDeg2 / kSegArcs * 64), 0, st, g->rp, g->al, Lown, h2, hl, blist, bcnt,
+                         ball, pmax, bsel);
       LPA_HIP(hipGetLastError());
     }
     return LPA_OK;
@@ -1986,7 +2151,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     const int64_t nb = g->n_hub - g->hub_lane_begin;
     hipLaunchKernelGGL((k_lpa_block<13, kBlockMaxDeg / kSegArcs>), dim3(cap_grid(nb, 2048)),
                        dim3(kBlockMaxDeg / kSegArcs * 64), 0, st, g->rp, g->al, Lown, g->hub_lane_begin, g->n_hub,
-                       g->flist, fcnt, fr_all, pmax, gsel);
+                       blist, bcnt, ball, pmax, bsel);
     LPA_HIP(hipGetLastError());
     return LPA_OK;
   };
@@ -2002,26 +2167,31 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // fourth stream and the narrow tier follows the hub mid tiers on the main stream
   // (C3 293.8-295.4 -> 299.3-303.1 GTEPS over the block tiers first on the main stream)
   const bool split = blk && !g->serial;
-  if (split) {
+  if (split && !giant_units) {
     LPA_HIP(hipStreamWaitEvent(g->aux_stream[2], g->ev_fork, 0));
     LPA_TRY(launch_block_wide(g->aux_stream[2]));
     LPA_HIP(hipEventRecord(g->ev_join2[1], g->aux_stream[2]));
+  }
+  const int64_t n_units = blk ? g->unit_block2_begin : g->n_segs;
+  if (giant_units && g->n_segs > 0) {
+    hipLaunchKernelGGL(k_lpa_units_giant, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s, g->al,
+                       g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
+    LPA_HIP(hipGetLastError());
+    LPA_TRY(launch_hub_decide(g, Lown, g->n_hub, gsel));
+    if (split) {  // the wide tier's undecided rows on the fourth stream
+      LPA_HIP(hipEventRecord(g->ev_join2[2], s));
+      LPA_HIP(hipStreamWaitEvent(g->aux_stream[2], g->ev_join2[2], 0));
+      LPA_TRY(launch_block_wide(g->aux_stream[2]));
+      LPA_HIP(hipEventRecord(g->ev_join2[1], g->aux_stream[2]));
+    }
   }
   // serialized profiling: the block kernel bracketed on its own (stats kernel 16),
   // ahead of the seg units' marks
   if (blk && g->serial) LPA_TRY(launch_block(s));
   LPA_TRY(mark(0, s));
-  const int64_t n_units = blk ? g->unit_block2_begin : g->n_segs;
-  // superstep 2 in block mode: the unit-tallied rows by giant counts first, the exact
-  // unit tally only for the rows k_hub_decide cannot settle
-  const bool giant_units = gsel != nullptr && blk;
   if (n_units > 0 && giant_units) {
-    hipLaunchKernelGGL(k_lpa_units_giant, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s, g->al,
-                       g->segs, n_units, gsel, g->ugc, g->umx, g->gdec);
-    LPA_HIP(hipGetLastError());
-    LPA_TRY(launch_hub_decide(g, Lown, block_rows_begin(g), gsel));
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
-                       g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist2, g->gdec, g->gdec + 1, pmax);
+                       g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist2, g->gdec, g->gdec + 3, pmax);
     LPA_HIP(hipGetLastError());
   } else if (n_units > 0) {
     hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
@@ -2152,7 +2322,7 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     const int64_t nbits = (ranked && hb_lg == 0) ? 0 : g->vpad;
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
-                     g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword)
+                     g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits)
     if (if_wanted) {
       if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
     } else {
@@ -2163,10 +2333,10 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
     if (if_wanted)
       hipLaunchKernelGGL(k_al_rebuild<true>, dim3(grid), dim3(256), 0, s, ctr, thr, g->col,
-                         g->arcs, L, g->al);
+                         g->arcs, L, g->al, g->gword);
     else
       hipLaunchKernelGGL(k_al_rebuild<false>, dim3(grid), dim3(256), 0, s, ctr, thr, g->col,
-                         g->arcs, L, g->al);
+                         g->arcs, L, g->al, g->gword);
   }
   LPA_HIP(hipGetLastError());
   return LPA_OK;
@@ -2215,12 +2385,18 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   fm.n_hub = g->n_hub;
   fm.rdirty = g->rdirty[par ^ 1];
   fm.udirty = g->udirty[par ^ 1];
+  if (g->al_pending) {  // the column-run superstep after a lazy reset (al holds nothing)
+    hipLaunchKernelGGL(k_al_fill_unless_rebuild, dim3(cap_grid((g->arcs / 4 + 255) / 256, 8192)), dim3(256), 0, s,
+                       ctr, thr, (const v4i*)g->al0, (v4i*)g->al, g->arcs);
+    LPA_HIP(hipGetLastError());
+    g->al_pending = false;  // the rebuild below (or this fill + the scatter) makes al valid
+  }
   hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chlist, (const uint4*)g->chflag,
                      (g->n_chunk_scan + 15) / 16, g->cowner, g->cch, ctr,
                      g->counters + 4 * (par ^ 1), g->cptr,
                      g->cpos, Ln, g->al, thr, fm, g->fr_all + (par ^ 1), g->frontier,
                      (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc),
-                     fold_rebuild ? g->col : (const int32_t*)nullptr, g->arcs);
+                     fold_rebuild ? g->col : (const int32_t*)nullptr, g->arcs, g->gword, g->abits);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   if (ev_scatter) LPA_HIP(hipEventRecord(ev_scatter, s));  // profiling: scatter | rebuild
@@ -2291,6 +2467,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
     // superstep 1 from L0: column runs, no hash tallies (its diff runs in the refresh)
     const bool first = first_runs_now(g);
+    if (!first) LPA_TRY(ensure_al(g));  // a lazy reset's al is needed by the hash tallies
     const bool diff_in_tally = !exchanges(g) && !g->serial && !first;
     // converged supersteps on one GPU replay a captured HIP graph of the whole
     // superstep (tally on four streams + diff + refresh; ~25 kernels and the
@@ -2298,7 +2475,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // the label / counter buffers, so there is one per (cur, par) state.
     // supersteps before `eager` are launched stream-ordered (their schedule differs
     // from the converged one a captured graph bakes)
-    const int eager = kDenseSupersteps;
+    // (superstep 3 too: its row settle is launched only then)
+    const int eager = kDenseSupersteps + 1;
     if (g->use_graphs && !exchanges(g) && !g->serial && g->since_reset >= eager) {
       const int key = g->cur * 2 + g->par;
       if (!g->gexec[key])
@@ -2353,6 +2531,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // would merge every unit of a dirty hub row with stale (or never written) words of
     // its unlisted units, so the next superstep tallies every row and unit
     if (first) g->force_all_next = true;
+    // a settled superstep 3 (k_settle_*) re-tallies no unit of a settled hub row: their
+    // staged words are stale for a frontier superstep 4
+    if (g->since_reset == 2 && g->abits) g->force_all_next = true;
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
     g->cur ^= 1;
     g->par ^= 1;
@@ -2411,6 +2592,13 @@ int frontier_all(lpa_graph* g, int par) {
 int rebuild_arc_labels(lpa_graph* g) {
   if (g->arcs == 0) return LPA_OK;
   return launch_rebuild(g, false, 0, g->lab[g->cur], g->counters);
+}
+
+int ensure_al(lpa_graph* g) {
+  if (!g->al_pending) return LPA_OK;
+  LPA_HIP(hipMemcpyAsync(g->al, g->al0, sizeof(int32_t) * g->arcs, hipMemcpyDeviceToDevice, g->stream));
+  g->al_pending = false;
+  return LPA_OK;
 }
 
 int gather_labels(lpa_graph* g, int32_t* out_dense_dev) {
