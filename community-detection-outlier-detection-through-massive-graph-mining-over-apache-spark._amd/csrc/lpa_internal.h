@@ -102,9 +102,7 @@ struct lpa_graph {
   // bucket path (2); 4 streams = the 4 hardware queues of a process
   hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
-  // hub combine tail, block tiers; ev_join2[2]: superstep 2's giant decision is done (the
-  // block tiers on the fourth stream wait for it)
-  hipEvent_t ev_fork2 = nullptr, ev_join2[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_fork2 = nullptr, ev_join2[3] = {nullptr, nullptr, nullptr};  // hub combine tail, block tiers
   int32_t rank = 0, nranks = 1;
   // label-exchange collective backend (P > 1): RCCL communicator (one process per
   // GPU) or the in-process loopback group (P handles on one device, one host thread

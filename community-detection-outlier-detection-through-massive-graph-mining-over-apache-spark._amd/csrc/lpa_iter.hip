@@ -375,7 +375,7 @@ __device__ __forceinline__ u32 giant_count(const u32 (&lab)[NC], int nch, u32 G,
 template <int NC>
 __device__ __forceinline__ bool giant_decide(const u32 (&lab)[NC], int nch, u32 G, u32* hist, int lane) {
   const u32 cg = wave_sum_u32(giant_count<NC>(lab, nch, G, hist, kGiantLg));
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();  // no reordering across (LDS ops of a wave complete in order)
   const u32 b = hist[lane];
   hist[lane] = 0u;
   return cg > wave_max_u32(b);
@@ -876,7 +876,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
         const u64 gb = __ballot(lb == Gl);
         const u32 cg = (u32)__popcll((gb >> gbase) & gm);
         if (lb != Gl && lb != kNone) atomicAdd(&hg[hash_slot(lb, 28)], 1u);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // no reordering across (LDS ops of a wave complete in order)
         u32 mx = 0u;
         if (gj < kGB) {
           mx = hg[gj];
@@ -1092,7 +1092,7 @@ __global__ __launch_bounds__(256) void k_lpa_units_giant(const int32_t* __restri
 #pragma unroll
     for (int c = 0; c < kChunks; ++c) lab[c] = c * 64 + lane < len ? raw[c] : kNone;
     const u32 cg = wave_sum_u32(giant_count<kChunks>(lab, kChunks, G, hist, kGiantLg));
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // no reordering across (LDS ops of a wave complete in order)
     const u32 b = hist[lane];
     hist[lane] = 0u;
     const u32 hm = wave_max_u32(b);
@@ -1151,6 +1151,15 @@ struct BinBounds {
   int64_t b[LPA_NBINS + 1];
 };
 constexpr int kDiffQuads = 2048;
+// counters[1] value that makes the refresh rebuild al[] (k_dense_decide)
+constexpr unsigned long long kForcedRebuild = 1ull << 62;
+
+// Label-dense supersteps (P = 1): the per-stream diffs only counted the changed slots.
+// More than 1/10 of the slots changed: the refresh rebuilds al[] (counters[1] forced),
+// so no position chunk is ever emitted; otherwise the full diff (mode 2) runs next.
+__global__ void k_dense_decide(unsigned long long* __restrict__ counters, int64_t n_slots) {
+  if (threadIdx.x == 0 && (int64_t)counters[2] * 10 > n_slots) counters[1] = kForcedRebuild;
+}
 // fcnt[] slot set by the row settle of a giant superstep (k_settle_*): the bin kernels
 // walk lists of the unsettled rows, but the diff scans every slot (settled rows may
 // have changed label)
@@ -1167,7 +1176,28 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
                                               BinBounds bb, int b0, int b1,
                                               const int32_t* __restrict__ flist,
                                               const int32_t* __restrict__ fcnt,
-                                              const int32_t* __restrict__ fr_all) {
+                                              const int32_t* __restrict__ fr_all, int mode) {
+  // mode 1 (label-dense supersteps): only count the changed slots (counters[2]); mode 2:
+  // the full diff unless k_dense_decide already chose the rebuild (counters[1] forced)
+  if (mode == 2 && counters[1] >= kForcedRebuild) return;
+  if (mode == 1) {
+    unsigned long long c = 0;
+    const int64_t q0 = s0 / 4 + (int64_t)blockIdx.x * kDiffQuads;
+    const int64_t q1 = min((s1 + 3) / 4, q0 + kDiffQuads);
+    for (int64_t q = q0 + threadIdx.x; q < q1; q += 256) {
+      const int4 a = Lc4[q], b = Ln4[q];
+      int chg = (a.x != b.x) | ((a.y != b.y) << 1) | ((a.z != b.z) << 2) | ((a.w != b.w) << 3);
+      if (q * 4 < s0 || q * 4 + 4 > s1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (q * 4 + k < s0 || q * 4 + k >= s1) chg &= ~(1 << k);
+      }
+      c += (unsigned long long)__popc(chg);
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&counters[2], c);
+    return;
+  }
   __shared__ int32_t q_col[kDiffQuads * 4];
   __shared__ int qn;
   __shared__ unsigned long long base_s;
@@ -1274,13 +1304,15 @@ __global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rd
                                                         int32_t* __restrict__ ulist,
                                                         int32_t* __restrict__ fcnt,
                                                         int32_t* __restrict__ fcnt_next,
-                                                        int64_t nblk_rows) {
+                                                        int64_t nblk_rows, const int32_t* __restrict__ build) {
   __shared__ int32_t lcnt[LPA_NBINS + 1];
   __shared__ int32_t lpos[LPA_NBINS + 1];
   __shared__ int32_t gbase[LPA_NBINS + 1];
   __shared__ int64_t sbb[LPA_NBINS + 1];
   if (blockIdx.x == 0 && threadIdx.x < 16) fcnt_next[threadIdx.x] = 0;  // + kFcntSettled
-  if (*fr_all) return;  // uniform
+  // build (nullable) == 0: the lists are built in a full-tally superstep too (the
+  // lane-giant rows k_giant_lane could not settle; the other bins take their ranges)
+  if (*fr_all && !(build && *build == 0)) return;  // uniform
   const bool units = (int64_t)blockIdx.x >= nblk_rows;
   const int64_t n = units ? nunits : S;   // flag arrays are padded to 16 bytes
   uint8_t* flags = units ? udirty : rdirty;
@@ -1463,6 +1495,49 @@ __global__ __launch_bounds__(256) void k_settle_rows(const int64_t* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// Giant supersteps (2 and 4), rows of 8 < deg <= 128 (bins w2, g64 .. g8): one LANE
+// per row.  The lane streams its row, counts G's votes and keeps 16 label-hash bucket
+// counts (8 bits each, in two registers: at most 128 votes); G above every bucket
+// settles the row (giant_decide's bound).  A row it cannot settle gets its dirty flag,
+// and those bins then walk the flagged rows' lists (k_frontier_lists with `build`)
+// while the rest of the superstep takes its ranges.  The per-group ballot / sort
+// kernels spent ~100 scalar + vector instructions per row here (scalar-issue bound:
+// SQ_INSTS_SALU 2x SQ_INSTS_VALU in k_lpa_rows<32>, profiles/r03/c_pmc).
+// mode_out (gword[3]) = 0: list mode for those bins; 1 (G not worth trying): ranges.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_giant_lane(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
+                                                    int64_t r0, int64_t r1, int32_t* __restrict__ gword,
+                                                    int32_t* __restrict__ Ln, uint8_t* __restrict__ rdirty) {
+  const bool on = gword[1] != 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[3] = on ? 0 : 1;
+  if (!on) return;  // uniform
+  const u32 G = (u32)gword[0];
+  for (int64_t v = r0 + (int64_t)blockIdx.x * 256 + threadIdx.x; v < r1; v += (int64_t)gridDim.x * 256) {
+    const int64_t b = rp[v], e = rp[v + 1];
+    u32 cg = 0;
+    unsigned long long h0 = 0ull, h1 = 0ull;
+#pragma unroll 8
+    for (int64_t i = b; i < e; ++i) {
+      const u32 x = ld_stream(al + i);
+      if (x == G) {
+        ++cg;
+      } else {
+        const u32 hb = hash_slot(x, 28);
+        const unsigned long long inc = 1ull << (8 * (hb & 7u));
+        if (hb & 8u) h1 += inc;
+        else h0 += inc;
+      }
+    }
+    u32 mx = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx = max(mx, max((u32)(h0 >> (8 * k)) & 0xFFu, (u32)(h1 >> (8 * k)) & 0xFFu));
+    const bool settled = cg > mx;
+    if (settled) Ln[v] = (int32_t)G;
+    rdirty[v] = settled ? 0 : 1;
+  }
+}
+
 // the settled superstep runs in list mode over the unsettled rows; the diff scans all
 __global__ void k_settle_commit(int32_t* __restrict__ fr_all, const int32_t* __restrict__ gword,
                                 int32_t* __restrict__ fcnt) {
@@ -1601,7 +1676,7 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
                                                     int32_t* __restrict__ gword,
                                                     unsigned long long* __restrict__ abits) {
   // the next superstep's counters (the other parity; no memset launch)
-  if (blockIdx.x == 0 && threadIdx.x < 2) counters_next[threadIdx.x] = 0ull;
+  if (blockIdx.x == 0 && threadIdx.x < 3) counters_next[threadIdx.x] = 0ull;
   const bool rebuild = rebuild_wanted(counters, thr);
   // the arc giant bits: kept in step by the scatter while valid (read before any block
   // can clear the flag: the clear below only follows a plain folded rebuild)
@@ -1856,37 +1931,51 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
     }
   };
   // lane-consecutive arcs: one gather instruction covers 64 consecutive arcs of
-  // a row, whose sorted columns often share lines (hub rows) -> fewer L2 requests
+  // a row, whose sorted columns often share lines (hub rows) -> fewer L2 requests.
+  // Full 512-arc batches are software-pipelined: the next batch's column loads are in
+  // flight while this batch's labels are looked up and stored.
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512;
-       base < arcs; base += nw * 512) {
-    int32_t c[8], r[8];
-    if (base + 512 <= arcs) {
+  const int64_t step = nw * 512;
+  const int64_t nfull = arcs & ~(int64_t)511;  // arcs of the full batches
+  int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512;
+  int32_t c[8];
+  if (base < nfull) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + base + k * 64 + lane);
+    for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + base + k * 64 + lane);
+  }
+  for (; base < nfull; base += step) {
+    int32_t cn[8], r[8];
+    const int64_t nb = base + step;
+    if (nb < nfull) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) r[k] = lab(c[k]);
+      for (int k = 0; k < 8; ++k) cn[k] = __builtin_nontemporal_load(col + nb + k * 64 + lane);
+    }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
-      if (bits) {
-        unsigned long long mine = 0ull;
+    for (int k = 0; k < 8; ++k) r[k] = lab(c[k]);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const unsigned long long m = __ballot(r[k] == G);
-          if (lane == k) mine = m;
-        }
-        if (lane < 8) abits[(base >> 6) + lane] = mine;
-      }
-    } else {
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
+    if (bits) {
+      unsigned long long mine = 0ull;
+#pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const int64_t i = base + k * 64 + lane;
-        const bool v = i < arcs;
-        const int32_t x = v ? lab(col[i]) : 0;
-        if (v) al[i] = x;
-        const unsigned long long m = __ballot(v && x == G);
-        if (bits && lane == 0 && base + k * 64 < arcs) abits[(base >> 6) + k] = m;
+        const unsigned long long m = __ballot(r[k] == G);
+        if (lane == k) mine = m;
       }
+      if (lane < 8) abits[(base >> 6) + lane] = mine;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = cn[k];
+  }
+  // the partial last batch (one wave)
+  if (nfull < arcs && base == nfull) {
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = base + k * 64 + lane;
+      const bool v = i < arcs;
+      const int32_t x = v ? lab(col[i]) : 0;
+      if (v) al[i] = x;
+      const unsigned long long m = __ballot(v && x == G);
+      if (bits && lane == 0 && base + k * 64 < arcs) abits[(base >> 6) + k] = m;
     }
   }
 }
@@ -2031,23 +2120,27 @@ inline unsigned cap_grid(int64_t want, int64_t cap) {
 // tails of the small bins.  bev (nullable): events 2k / 2k+1 bracket tally kernel
 // k on its own stream (0 units, 1 hub combine, 2..11 bins w8 .. g1).
 int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* Ln, int64_t s0,
-                int64_t s1, bool sync, int par, int b0 = 0, int b1 = 0);
+                int64_t s1, bool sync, int par, int b0 = 0, int b1 = 0, int mode = 0);
 
 // diff (P = 1, concurrent schedule): each stream diffs the slots its own bins
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
 // rows after the hub combine), overlapping most of the diff with the tally tail
 // the per-bin dirty-row lists of this superstep (zeroes the other parity's counts)
-int launch_frontier_lists(lpa_graph* g) {
+int launch_frontier_lists(lpa_graph* g, const int32_t* build = nullptr) {
   BinBounds bnd;
   for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = g->bin_begin[b];
   const int64_t nbr = (g->slice + kListTile - 1) / kListTile;
   const int64_t nbu = (g->n_segs + kListTile - 1) / kListTile;
   hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, g->stream, g->rdirty[g->par],
                      g->slice, g->udirty[g->par], g->n_segs, bnd, g->fr_all + g->par, g->flist, g->ulist,
-                     g->fcnt + 16 * g->par, g->fcnt + 16 * (g->par ^ 1), nbr);
+                     g->fcnt + 16 * g->par, g->fcnt + 16 * (g->par ^ 1), nbr, build);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
+
+// label-dense superstep on one GPU: its diff only counts the changed slots, and its
+// refresh rebuilds al[] unless few changed (k_dense_decide)
+bool dense_refresh(const lpa_graph* g) { return g->since_reset < kDenseSupersteps && !exchanges(g); }
 
 // superstep 1 from L0 by column runs (k_first_runs); the caller's refresh diffs
 bool first_runs_now(const lpa_graph* g) {
@@ -2078,6 +2171,10 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   const int64_t* bb = g->bin_begin;
   const int32_t* fr_all = g->fr_all + g->par;
   int32_t* fcnt = g->fcnt + 16 * g->par;
+  // supersteps 2-4 (the label-dense ones after the column-run superstep 1): the tallies
+  // try the giant label first (giant_decide); gsel = its word, picked by the previous
+  // superstep's refresh from the labels this one reads
+  const int32_t* gsel = (g->since_reset >= 1 && g->since_reset <= 3) ? g->gword : nullptr;
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 4], s));
   // superstep 3: rows settled from the arc giant bits of superstep 2's rebuild (each
   // kernel returns at once unless they are valid): the others' dirty flags, then the
@@ -2097,8 +2194,21 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     hipLaunchKernelGGL(k_settle_commit, dim3(1), dim3(1), 0, s, const_cast<int32_t*>(fr_all), g->gword, fcnt);
     LPA_HIP(hipGetLastError());
   }
-  // frontier lists of this superstep (no-op when every row is tallied)
-  LPA_TRY(launch_frontier_lists(g));
+  // supersteps 2 and 4 (giant, full tallies): the rows of 8 < deg <= 128 one lane each
+  // (k_giant_lane); the ones it cannot settle are listed for their bins below
+  const bool lane_giant = gsel != nullptr && (g->since_reset == 1 || g->since_reset == 3) &&
+                          g->bin_begin[BIN_G4] > g->bin_begin[BIN_W2];
+  if (lane_giant) {
+    const int64_t r0 = g->bin_begin[BIN_W2], r1 = g->bin_begin[BIN_G4];
+    hipLaunchKernelGGL(k_giant_lane, dim3(cap_grid((r1 - r0 + 255) / 256, 4096)), dim3(256), 0, s, g->rp, g->al,
+                       r0, r1, g->gword, Lown, g->rdirty[g->par]);
+    LPA_HIP(hipGetLastError());
+  }
+  // frontier lists of this superstep (no-op when every row is tallied, unless the lane
+  // giant listed its rows)
+  LPA_TRY(launch_frontier_lists(g, lane_giant ? g->gword + 3 : nullptr));
+  // the lane-giant bins walk their lists (gword[3] == 0) or their ranges
+  const int32_t* fr_lane = lane_giant ? g->gword + 3 : fr_all;
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
@@ -2119,10 +2229,6 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // peel rounds of the row bins before a chunk is sorted: none in the label-dense
   // supersteps (measured best of 0/1/2/3 at C3), kPeelSortAfter otherwise
   const int sort_after = g->since_reset < kDenseSupersteps ? 0 : kPeelSortAfter;
-  // supersteps 2 and 3 (the label-dense ones after the column-run superstep 1): the
-  // tallies try the giant label first (giant_decide); gsel = its word, picked by the
-  // previous superstep's refresh from the labels this one reads
-  const int32_t* gsel = (g->since_reset >= 1 && g->since_reset <= 3) ? g->gword : nullptr;
   // superstep 2 in block mode: every hub row by giant counts first (k_lpa_units_giant
   // over all units, k_hub_decide); only the rows it cannot settle are tallied exactly --
   // block-tier rows by k_lpa_block from glist, the longer ones by their units
@@ -2139,7 +2245,9 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   auto launch_block_wide = [&](hipStream_t st) -> int {
     const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;
     if (hl > h2) {
-      hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, 1024)),
+      // giant mode: few undecided rows, so few fat blocks (a 128 KB-LDS block per CU
+      // would wait for the concurrent bins' blocks to leave)
+      hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, giant_units ? 32 : 1024)),
                          dim3(kBlockMaxDeg2 / kSegArcs * 64), 0, st, g->rp, g->al, Lown, h2, hl, blist, bcnt,
                          ball, pmax, bsel);
       LPA_HIP(hipGetLastError());
@@ -2149,7 +2257,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // rows <= 4096 (8 waves, 8K slots, two blocks per CU)
   auto launch_block_narrow = [&](hipStream_t st) -> int {
     const int64_t nb = g->n_hub - g->hub_lane_begin;
-    hipLaunchKernelGGL((k_lpa_block<13, kBlockMaxDeg / kSegArcs>), dim3(cap_grid(nb, 2048)),
+    hipLaunchKernelGGL((k_lpa_block<13, kBlockMaxDeg / kSegArcs>), dim3(cap_grid(nb, giant_units ? 64 : 2048)),
                        dim3(kBlockMaxDeg / kSegArcs * 64), 0, st, g->rp, g->al, Lown, g->hub_lane_begin, g->n_hub,
                        blist, bcnt, ball, pmax, bsel);
     LPA_HIP(hipGetLastError());
@@ -2178,12 +2286,9 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
                        g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
     LPA_HIP(hipGetLastError());
     LPA_TRY(launch_hub_decide(g, Lown, g->n_hub, gsel));
-    if (split) {  // the wide tier's undecided rows on the fourth stream
-      LPA_HIP(hipEventRecord(g->ev_join2[2], s));
-      LPA_HIP(hipStreamWaitEvent(g->aux_stream[2], g->ev_join2[2], 0));
-      LPA_TRY(launch_block_wide(g->aux_stream[2]));
-      LPA_HIP(hipEventRecord(g->ev_join2[1], g->aux_stream[2]));
-    }
+    // the wide tier's few undecided rows right here on the main stream (the fourth
+    // stream shares a hardware queue with aux1, whose row bins it would delay)
+    if (split) LPA_TRY(launch_block_wide(s));
   }
   // serialized profiling: the block kernel bracketed on its own (stats kernel 16),
   // ahead of the seg units' marks
@@ -2200,13 +2305,13 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRACE_POINT("seg");
   }
   LPA_TRY(mark(1, s));
-#define LPA_WAVE_LAUNCH(BIN, NC, ST)                                                              \
+#define LPA_WAVE_LAUNCH(BIN, NC, ST, FR)                                                          \
   {                                                                                           \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                  \
     LPA_TRY(mark(2 * (BIN + 1), ST));                                                         \
     if (n > 0) {                                                                              \
       hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, ST,  \
-                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, pmax, gsel); \
+                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, pmax, gsel); \
       LPA_HIP(hipGetLastError());                                                             \
     }                                                                                         \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                     \
@@ -2222,14 +2327,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
   }
-#define LPA_ROWS_LAUNCH(BIN, G)                                                              \
+#define LPA_ROWS_LAUNCH(BIN, G, FR)                                                          \
   {                                                                                          \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
     LPA_TRY(mark(2 * (BIN + 1), sc));                                                        \
     if (n > 0) {                                                                             \
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
       hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
-                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all, \
+                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, \
                          sort_after, gsel);                                                   \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
@@ -2237,14 +2342,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   }
   // stream balance (measured steady superstep): aux0 w16 + w8 + w4, aux1 w2 + the
   // row/group bins
-  LPA_WAVE_LAUNCH(BIN_W16, 16, sb)
-  LPA_WAVE_LAUNCH(BIN_W8, 8, sb)
-  LPA_WAVE_LAUNCH(BIN_W4, 4, sb)
-  LPA_WAVE_LAUNCH(BIN_W2, 2, sc)
-  LPA_ROWS_LAUNCH(BIN_G64, 64)
-  LPA_ROWS_LAUNCH(BIN_G32, 32)
-  LPA_ROWS_LAUNCH(BIN_G16, 16)
-  LPA_ROWS_LAUNCH(BIN_G8, 8)
+  LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_all)
+  LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_all)
+  LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_all)
+  LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_lane)
+  LPA_ROWS_LAUNCH(BIN_G64, 64, fr_lane)
+  LPA_ROWS_LAUNCH(BIN_G32, 32, fr_lane)
+  LPA_ROWS_LAUNCH(BIN_G16, 16, fr_lane)
+  LPA_ROWS_LAUNCH(BIN_G8, 8, fr_lane)
   LPA_GROUP_LAUNCH(BIN_G4, 4)
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
@@ -2262,14 +2367,16 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   }
   LPA_TRACE_POINT("hub_combine");
   // the block rows' labels are seg-bin slots: joined before the main stream's diff
-  if (split) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[1], 0));
+  if (split && !giant_units) LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[1], 0));
   LPA_TRY(mark(3, s));
   if (diff) {
-    // inside the concurrent tally: no Lc sync here, the scatter refresh does it
-    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2], false, g->par, BIN_W16, BIN_W2));
+    // inside the concurrent tally: no Lc sync here, the scatter refresh does it; the
+    // label-dense supersteps only count the changed slots (launch_refresh decides)
+    const int dm = dense_refresh(g) ? 1 : 0;
+    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2], false, g->par, BIN_W16, BIN_W2, dm));
     // isolated slots (and the padding) never change: the diff stops at the isolated bin
-    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], bb[BIN_ISO], false, g->par, BIN_W2, BIN_ISO));
-    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par, BIN_SEG, BIN_W16));
+    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], bb[BIN_ISO], false, g->par, BIN_W2, BIN_ISO, dm));
+    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par, BIN_SEG, BIN_W16, dm));
   }
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_join[0], sb));
@@ -2345,7 +2452,7 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
 // changed slots in [s0, s1) -> position chunks + dirty-arc count (counters of this
 // superstep's parity)
 int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* Ln, int64_t s0,
-                int64_t s1, bool sync, int par, int b0, int b1) {
+                int64_t s1, bool sync, int par, int b0, int b1, int mode) {
   if (s1 <= s0) return LPA_OK;
   const int64_t nq = (s1 + 3) / 4 - s0 / 4;
   BinBounds bnd;
@@ -2356,7 +2463,7 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
   hipLaunchKernelGGL(k_diff, dim3((unsigned)((nq + kDiffQuads - 1) / kDiffQuads)), dim3(256), 0, st,
                      (const int4*)Lc, (const int4*)Ln, sync ? const_cast<int32_t*>(Lc) : nullptr, s0, s1,
                      g->cptr, g->cch, g->chflag, g->chlist, g->counters + 4 * par, bnd, b0, b1,
-                     lists ? g->flist : nullptr, g->fcnt + 16 * g->par, g->fr_all + g->par);
+                     lists ? g->flist : nullptr, g->fcnt + 16 * g->par, g->fr_all + g->par, mode);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -2374,8 +2481,16 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   unsigned long long* ctr = g->counters + 4 * par;
   // one rank: its isolated slots (and the padding) never change; P > 1: the whole
   // replicated vector (other ranks' slots change through the exchange)
-  if (!diff_done)
-    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, !exchanges(g) ? g->bin_begin[BIN_ISO] : g->vpad, true, par));
+  const int64_t nd = !exchanges(g) ? g->bin_begin[BIN_ISO] : g->vpad;
+  if (dense_refresh(g)) {
+    // counted changed slots (in the tally, or here) -> rebuild, or the full diff
+    if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, false, par, 0, 0, 1));
+    hipLaunchKernelGGL(k_dense_decide, dim3(1), dim3(64), 0, s, ctr, nd);
+    LPA_HIP(hipGetLastError());
+    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, true, par, 0, 0, 2));
+  } else if (!diff_done) {
+    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, true, par));
+  }
   LPA_TRACE_POINT("diff");
   const int64_t thr = (int64_t)(kRebuildFrac * (double)g->arcs);
   FrontierMarks fm;
@@ -2475,8 +2590,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // the label / counter buffers, so there is one per (cur, par) state.
     // supersteps before `eager` are launched stream-ordered (their schedule differs
     // from the converged one a captured graph bakes)
-    // (superstep 3 too: its row settle is launched only then)
-    const int eager = kDenseSupersteps + 1;
+    // (supersteps 3 and 4 too: the row settle and the lane giant are launched only
+    // then, and a replayed graph would repeat them)
+    const int eager = kDenseSupersteps + 2;
     if (g->use_graphs && !exchanges(g) && !g->serial && g->since_reset >= eager) {
       const int key = g->cur * 2 + g->par;
       if (!g->gexec[key])
