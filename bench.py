@@ -260,8 +260,11 @@ def main():
         cfg["scale"] = args.scale
         config_id = {24: "C3", 26: "C4"}.get(args.scale, f"R-MAT-{args.scale}")
     if args.launch_check:   # no GPU: what each rank would run (tests/test_bench_launch.py)
-        print(json.dumps(dict(rank=rank, world=world, local_rank=local_rank, config_id=config_id,
-                              scaling=scaling, cfg=cfg)), flush=True)
+        # one write(2) per rank: ranks share the pipe, and print() may split a line
+        line = json.dumps(dict(rank=rank, world=world, local_rank=local_rank, config_id=config_id,
+                               scaling=scaling, cfg=cfg)) + "\n"
+        sys.stdout.flush()
+        os.write(1, line.encode())
         return
 
     import numpy as np
