@@ -35,7 +35,7 @@
 //   g4 .. g64 deg <= G  G lanes per vertex, ballot "peel": each round takes the
 //                       group's first unresolved label, counts its lanes with one
 //                       64-bit ballot, retires them; a chunk still unresolved after
-//                       3 rounds (label-dense) sorts each group's lanes instead
+//                       3 rounds (label-dense) counts its groups in an LDS hash
 //   w2..w16 deg <= 64*NC  one wave per vertex, NC chunks: cross-chunk peel in
 //                       registers, the residual through a per-wave LDS hash
 //   seg  deg > 1024     one wave per 512-arc unit (staged unit tally words), merged
@@ -407,50 +407,63 @@ __device__ __forceinline__ BinRows bin_rows(int64_t vbeg, int64_t vend, const in
   return br;
 }
 
-// Mode of each G-lane group's labels (one label per lane, kNone = empty) by sorting:
-// a bitonic network across the group's lanes (log2 G (log2 G + 1) / 2 exchange
-// stages, each a lane::lane_xor (lpa_lane.h); a group's direction may come out descending, which leaves equal labels
-// contiguous all the same), then run lengths from the ballot of run starts, then a
-// group max of the run tally words.  Every lane of a group returns its group's word.
-// The ballot peel costs one dependent round per distinct label; in the label-dense
-// supersteps a 32-lane row holds ~20-30 distinct labels, where the fixed ~15-stage
-// network is several times cheaper.
+// Mode of each G-lane group's labels through a wave-owned LDS table (kRowsHashSlots u64
+// slots, zero on entry and on return): group k owns slots [4G k, 4G (k + 1)) (load
+// <= 1/4), every lane inserts its label -- a CAS claims an empty slot with count 1, a
+// lane finding its own key adds 1 (lanes of one instruction that hit one address are
+// applied one after another, each seeing the previous result) -- then reads its slot
+// back: the slot holds its label's tally word.  A group max of the words gives the
+// mode (every lane of a group returns it).  ~35 vector instructions per 64 labels where
+// the 21-stage bitonic network it replaced (round 2: DPP / permlane exchanges) cost
+// ~150, and k_lpa_rows<64> was VALU-issue bound in the label-dense supersteps (C2: 884 K
+// rows of 33-64 arcs; C2 47.7 -> 55.5 GTEPS, dense supersteps 0.60 -> 0.49 ms).
+constexpr int kRowsHashSlots = 256;
 template <int G>
-__device__ __forceinline__ u64 group_mode_sort(u32 v, int lane) {
+__device__ __forceinline__ u64 group_mode_hash(u32 v, int lane, u64* tab) {
   static_assert(G >= 2 && G <= 64 && (G & (G - 1)) == 0, "group width");
-#pragma unroll
-  for (int k = 2; k <= G; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const u32 o = lane::lane_xor(v, j, lane);
-      const bool up = (lane & k) == 0, low = (lane & j) == 0;
-      v = (low == up) ? (v < o ? v : o) : (v > o ? v : o);
+  constexpr int kLg = (G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : G == 4 ? 2 : 1) + 2;
+  constexpr u32 kMask = (1u << kLg) - 1u;
+  u64* gt = tab + (lane & ~(G - 1)) * 4;
+  u64 w = 0ull;
+  if (v != kNone) {
+    const u64 word = (1ull << 32) | (u64)(u32)(~v);
+    u32 h = hash_slot(v, 32 - kLg);
+    while (true) {
+      const u64 old = atomicCAS(&gt[h], 0ull, word);
+      if (old == 0ull) break;
+      if ((u32)old == (u32)word) {
+        atomicAdd(&gt[h], 1ull << 32);
+        break;
+      }
+      h = (h + 1u) & kMask;
     }
+    __builtin_amdgcn_wave_barrier();
+    w = gt[h];
+    __builtin_amdgcn_wave_barrier();
+    gt[h] = 0ull;
   }
-  const int gj = lane & (G - 1);
-  const int gbase = lane - gj;
-  const u32 prev = lane::lane_prev(v);
-  const bool start = gj == 0 || v != prev;
-  const u64 bm = __ballot(start);
-  const u64 above = lane == 63 ? 0ull : (bm & ~((2ull << lane) - 1ull));
-  int nxt = above ? __ffsll((unsigned long long)above) - 1 : 64;
-  nxt = nxt < gbase + G ? nxt : gbase + G;
-  u64 w = (start && v != kNone) ? tally((u32)(nxt - lane), v) : 0ull;
+  if constexpr (G == 64) {
+    return wave_max_u64(w);
+  } else {
 #pragma unroll
-  for (int off = G >> 1; off > 0; off >>= 1) {
-    const u64 o = ((u64)lane::lane_xor((u32)(w >> 32), off, lane) << 32) | (u64)lane::lane_xor((u32)w, off, lane);
-    w = umax64(w, o);
+    for (int off = G >> 1; off > 0; off >>= 1) {
+      const u64 o = ((u64)lane::lane_xor((u32)(w >> 32), off, lane) << 32) | (u64)lane::lane_xor((u32)w, off, lane);
+      w = umax64(w, o);
+    }
+    return w;
   }
-  return w;
 }
-// peel rounds after which a chunk whose groups are still unresolved is sorted instead
+
+// peel rounds after which a chunk whose groups are still unresolved is hashed instead
 constexpr int kPeelSortAfter = 3;
+
+
 
 // lanes of the groups already decided after a peel round: a group whose best count
 // so far exceeds its untallied votes cannot change its mode (no remaining label can
 // reach, or tie, that count), so its lanes retire without further rounds -- a
 // converged row (one dominant label plus a few strays) stops after one round instead
-// of peeling the strays one by one and then sorting
+// of peeling the strays one by one and then hashing
 template <int G>
 __device__ __forceinline__ u64 decided_groups(u64 act, u64 my, u64 best, int gbase, u64 gm) {
   const u32 rem = (u32)__popcll((act >> gbase) & gm);
@@ -460,7 +473,8 @@ __device__ __forceinline__ u64 decided_groups(u64 act, u64 my, u64 best, int gba
 // G lanes per row (G <= 64, all 64 lanes of the wave call it: ballot peel)
 template <int G>
 __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
-                                          int32_t* __restrict__ Ln, int64_t v, bool live, int lane) {
+                                          int32_t* __restrict__ Ln, int64_t v, bool live, int lane,
+                                          u64* tab = nullptr) {
   const int j = lane & (G - 1);
   int64_t b = 0;
   int d = 0;
@@ -481,7 +495,7 @@ __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const 
     u64 best = 0ull;
     for (int round = 0; act; ++round) {
       if (G >= 8 && round == kPeelSortAfter) {  // uniform: a label-dense chunk
-        best = group_mode_sort<G>(lab, lane);
+        best = group_mode_hash<G>(lab, lane, tab);
         break;
       }
       const u64 my = (act >> gbase) & gm;
@@ -822,8 +836,12 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
   constexpr int RB = 512 / G;  // rows per batch
   constexpr int kGB = 16;      // giant-label histogram buckets per row (group)
   __shared__ u32 ghist_all[4][64 / G * kGB];
+  __shared__ u64 htab_all[4][kRowsHashSlots];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  u64* htab = htab_all[w];
+#pragma unroll
+  for (int k = 0; k < kRowsHashSlots / 64; ++k) htab[k * 64 + lane] = 0ull;
   if (!*fr_all) {
     // frontier: the listed dirty rows, G lanes each (rows are not consecutive, so
     // no batched offsets); every lane of a wave runs every trip (ballot peel)
@@ -832,7 +850,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
     for (int64_t i0 = ((int64_t)blockIdx.x * 4 + w) * per; i0 < br.n; i0 += nw * per) {
       const int64_t i = i0 + lane / G;
       const bool live = i < br.n;
-      group_row<G>(rp, al, Ln, live ? br.row(i) : 0, live, lane);
+      group_row<G>(rp, al, Ln, live ? br.row(i) : 0, live, lane, htab);
     }
     return;
   }
@@ -842,7 +860,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
   if (bi >= nb) return;  // no block-level barriers in this kernel
   // gsel (superstep 2, rows of > 8 arcs): a chunk whose every row is decided for the
   // giant label (its exact count above each of the row's kGB label-hash buckets of
-  // other votes, as giant_decide) skips the peel / sort
+  // other votes, as giant_decide) skips the peel / hash
   const bool giant = G >= 16 && gsel != nullptr && gsel[1] != 0;
   const u32 Gl = giant ? (u32)gsel[0] : 0u;
   u32* hg = &ghist_all[w][(lane / G) * kGB];
@@ -892,7 +910,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       for (int round = 0; act; ++round) {
         // uniform: a label-dense chunk after sort_after rounds
         if (round == sort_after) {
-          best = group_mode_sort<G>(lb, lane);
+          best = group_mode_hash<G>(lb, lane, htab);
           break;
         }
         const u64 my = (act >> gbase) & gm;
@@ -1304,15 +1322,13 @@ __global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rd
                                                         int32_t* __restrict__ ulist,
                                                         int32_t* __restrict__ fcnt,
                                                         int32_t* __restrict__ fcnt_next,
-                                                        int64_t nblk_rows, const int32_t* __restrict__ build) {
+                                                        int64_t nblk_rows) {
   __shared__ int32_t lcnt[LPA_NBINS + 1];
   __shared__ int32_t lpos[LPA_NBINS + 1];
   __shared__ int32_t gbase[LPA_NBINS + 1];
   __shared__ int64_t sbb[LPA_NBINS + 1];
   if (blockIdx.x == 0 && threadIdx.x < 16) fcnt_next[threadIdx.x] = 0;  // + kFcntSettled
-  // build (nullable) == 0: the lists are built in a full-tally superstep too (the
-  // lane-giant rows k_giant_lane could not settle; the other bins take their ranges)
-  if (*fr_all && !(build && *build == 0)) return;  // uniform
+  if (*fr_all) return;  // uniform
   const bool units = (int64_t)blockIdx.x >= nblk_rows;
   const int64_t n = units ? nunits : S;   // flag arrays are padded to 16 bytes
   uint8_t* flags = units ? udirty : rdirty;
@@ -1491,49 +1507,6 @@ __global__ __launch_bounds__(256) void k_settle_rows(const int64_t* __restrict__
     for (int64_t x = w0; x <= w1; ++x) c += (u32)__popcll(abits[x] & range_mask(x, w0, w1, a, b));
     const bool settled = 2 * (int64_t)c > b - a;
     if (settled) Ln[v] = G;
-    rdirty[v] = settled ? 0 : 1;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Giant supersteps (2 and 4), rows of 8 < deg <= 128 (bins w2, g64 .. g8): one LANE
-// per row.  The lane streams its row, counts G's votes and keeps 16 label-hash bucket
-// counts (8 bits each, in two registers: at most 128 votes); G above every bucket
-// settles the row (giant_decide's bound).  A row it cannot settle gets its dirty flag,
-// and those bins then walk the flagged rows' lists (k_frontier_lists with `build`)
-// while the rest of the superstep takes its ranges.  The per-group ballot / sort
-// kernels spent ~100 scalar + vector instructions per row here (scalar-issue bound:
-// SQ_INSTS_SALU 2x SQ_INSTS_VALU in k_lpa_rows<32>, profiles/r03/c_pmc).
-// mode_out (gword[3]) = 0: list mode for those bins; 1 (G not worth trying): ranges.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_giant_lane(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
-                                                    int64_t r0, int64_t r1, int32_t* __restrict__ gword,
-                                                    int32_t* __restrict__ Ln, uint8_t* __restrict__ rdirty) {
-  const bool on = gword[1] != 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) gword[3] = on ? 0 : 1;
-  if (!on) return;  // uniform
-  const u32 G = (u32)gword[0];
-  for (int64_t v = r0 + (int64_t)blockIdx.x * 256 + threadIdx.x; v < r1; v += (int64_t)gridDim.x * 256) {
-    const int64_t b = rp[v], e = rp[v + 1];
-    u32 cg = 0;
-    unsigned long long h0 = 0ull, h1 = 0ull;
-#pragma unroll 8
-    for (int64_t i = b; i < e; ++i) {
-      const u32 x = ld_stream(al + i);
-      if (x == G) {
-        ++cg;
-      } else {
-        const u32 hb = hash_slot(x, 28);
-        const unsigned long long inc = 1ull << (8 * (hb & 7u));
-        if (hb & 8u) h1 += inc;
-        else h0 += inc;
-      }
-    }
-    u32 mx = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) mx = max(mx, max((u32)(h0 >> (8 * k)) & 0xFFu, (u32)(h1 >> (8 * k)) & 0xFFu));
-    const bool settled = cg > mx;
-    if (settled) Ln[v] = (int32_t)G;
     rdirty[v] = settled ? 0 : 1;
   }
 }
@@ -2126,14 +2099,14 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
 // rows after the hub combine), overlapping most of the diff with the tally tail
 // the per-bin dirty-row lists of this superstep (zeroes the other parity's counts)
-int launch_frontier_lists(lpa_graph* g, const int32_t* build = nullptr) {
+int launch_frontier_lists(lpa_graph* g) {
   BinBounds bnd;
   for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = g->bin_begin[b];
   const int64_t nbr = (g->slice + kListTile - 1) / kListTile;
   const int64_t nbu = (g->n_segs + kListTile - 1) / kListTile;
   hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, g->stream, g->rdirty[g->par],
                      g->slice, g->udirty[g->par], g->n_segs, bnd, g->fr_all + g->par, g->flist, g->ulist,
-                     g->fcnt + 16 * g->par, g->fcnt + 16 * (g->par ^ 1), nbr, build);
+                     g->fcnt + 16 * g->par, g->fcnt + 16 * (g->par ^ 1), nbr);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -2194,21 +2167,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     hipLaunchKernelGGL(k_settle_commit, dim3(1), dim3(1), 0, s, const_cast<int32_t*>(fr_all), g->gword, fcnt);
     LPA_HIP(hipGetLastError());
   }
-  // supersteps 2 and 4 (giant, full tallies): the rows of 8 < deg <= 128 one lane each
-  // (k_giant_lane); the ones it cannot settle are listed for their bins below
-  const bool lane_giant = gsel != nullptr && (g->since_reset == 1 || g->since_reset == 3) &&
-                          g->bin_begin[BIN_G4] > g->bin_begin[BIN_W2];
-  if (lane_giant) {
-    const int64_t r0 = g->bin_begin[BIN_W2], r1 = g->bin_begin[BIN_G4];
-    hipLaunchKernelGGL(k_giant_lane, dim3(cap_grid((r1 - r0 + 255) / 256, 4096)), dim3(256), 0, s, g->rp, g->al,
-                       r0, r1, g->gword, Lown, g->rdirty[g->par]);
-    LPA_HIP(hipGetLastError());
-  }
-  // frontier lists of this superstep (no-op when every row is tallied, unless the lane
-  // giant listed its rows)
-  LPA_TRY(launch_frontier_lists(g, lane_giant ? g->gword + 3 : nullptr));
-  // the lane-giant bins walk their lists (gword[3] == 0) or their ranges
-  const int32_t* fr_lane = lane_giant ? g->gword + 3 : fr_all;
+  // frontier lists of this superstep (no-op when every row is tallied)
+  LPA_TRY(launch_frontier_lists(g));
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
@@ -2226,7 +2186,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // peel rounds of the wave / unit / block tallies (LPA_DENSE_PEEL in the label-dense
   // supersteps, where a round rarely retires more than a few votes)
   const int pmax = g->since_reset < kDenseSupersteps ? kDensePeel : kPeelMax;
-  // peel rounds of the row bins before a chunk is sorted: none in the label-dense
+  // peel rounds of the row bins before a chunk is hashed: none in the label-dense
   // supersteps (measured best of 0/1/2/3 at C3), kPeelSortAfter otherwise
   const int sort_after = g->since_reset < kDenseSupersteps ? 0 : kPeelSortAfter;
   // superstep 2 in block mode: every hub row by giant counts first (k_lpa_units_giant
@@ -2345,11 +2305,11 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_all)
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_all)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_all)
-  LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_lane)
-  LPA_ROWS_LAUNCH(BIN_G64, 64, fr_lane)
-  LPA_ROWS_LAUNCH(BIN_G32, 32, fr_lane)
-  LPA_ROWS_LAUNCH(BIN_G16, 16, fr_lane)
-  LPA_ROWS_LAUNCH(BIN_G8, 8, fr_lane)
+  LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_all)
+  LPA_ROWS_LAUNCH(BIN_G64, 64, fr_all)
+  LPA_ROWS_LAUNCH(BIN_G32, 32, fr_all)
+  LPA_ROWS_LAUNCH(BIN_G16, 16, fr_all)
+  LPA_ROWS_LAUNCH(BIN_G8, 8, fr_all)
   LPA_GROUP_LAUNCH(BIN_G4, 4)
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
@@ -2590,8 +2550,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // the label / counter buffers, so there is one per (cur, par) state.
     // supersteps before `eager` are launched stream-ordered (their schedule differs
     // from the converged one a captured graph bakes)
-    // (supersteps 3 and 4 too: the row settle and the lane giant are launched only
-    // then, and a replayed graph would repeat them)
+    // (supersteps 3 and 4 too: the row settle is launched only in superstep 3, and
+    // superstep 4 reads the giant word of the labels it tallies)
     const int eager = kDenseSupersteps + 2;
     if (g->use_graphs && !exchanges(g) && !g->serial && g->since_reset >= eager) {
       const int key = g->cur * 2 + g->par;

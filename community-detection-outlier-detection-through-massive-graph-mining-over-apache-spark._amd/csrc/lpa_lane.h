@@ -1,4 +1,4 @@
-// Cross-lane exchanges of the row-bin sort network (group_mode_sort, lpa_iter.hip),
+// Cross-lane exchanges of the row-bin group reductions (group_mode_hash, lpa_iter.hip),
 // kept in a header of their own so tools/microbench/lane_xor_check.hip (run by
 // tests/test_gpu_lane_exchange.py) checks the very function the kernels use.
 #pragma once

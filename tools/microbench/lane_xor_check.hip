@@ -1,5 +1,5 @@
-// Checks the DPP / permlane-swap lane exchanges of lpa_lane.h (the row-bin sort network,
-// lpa_iter.hip group_mode_sort) against lane ^ j for j = 1 .. 32 and lane - 1 on one full
+// Checks the DPP / permlane-swap lane exchanges of lpa_lane.h (the row-bin group reductions,
+// lpa_iter.hip group_mode_hash) against lane ^ j for j = 1 .. 32 and lane - 1 on one full
 // wave.  Built by the csrc Makefile into build/lpa_hip/lane_xor_check; exit status 0 = all
 // exchanges match (tests/test_gpu_lane_exchange.py).
 #include <hip/hip_runtime.h>
