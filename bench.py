@@ -47,10 +47,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "LPA GTEPS per iteration at 1/2/4/8 MI355X; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
-# measured HBM traffic per launch of the dominant kernel: rocprofv3 --pmc FETCH_SIZE /
-# WRITE_SIZE passes over this same bench command (tools/pmc_traffic.sh; FETCH doubled
-# per the gfx950 correction, cross-checked on k_diff's known byte count)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", "r02", "traffic", "pmc_traffic.json"),
+# measured HBM traffic per launch of the dominant kernels: rocprofv3 --pmc FETCH_SIZE /
+# WRITE_SIZE passes over the C3 workload (tools/pmc_r03.sh; FETCH doubled per the gfx950
+# correction, calibrated on a known-byte stream in profiles/r02/traffic)
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", "r03", "traffic", "pmc_traffic.json"),
+                 os.path.join(ROOT, "profiles", "r02", "traffic", "pmc_traffic.json"),
                  os.path.join(ROOT, "profiles", "r01", "e_traffic", "pmc_traffic.json")]
 
 CONFIGS = {

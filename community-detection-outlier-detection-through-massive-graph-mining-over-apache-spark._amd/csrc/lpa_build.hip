@@ -630,8 +630,8 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
 
   // ---- labels (replicated, ping-pong) ----
   LPA_TRY(dev_alloc(g, (void**)&g->gbits, sizeof(uint32_t) * ((g->vpad + 63) / 64 * 2)));
-  LPA_TRY(dev_alloc(g, (void**)&g->gword, sizeof(int32_t) * 4));
-  LPA_HIP(hipMemsetAsync(g->gword, 0, sizeof(int32_t) * 4, s));
+  LPA_TRY(dev_alloc(g, (void**)&g->gword, sizeof(int32_t) * 8));
+  LPA_HIP(hipMemsetAsync(g->gword, 0, sizeof(int32_t) * 8, s));
   LPA_TRY(dev_alloc(g, (void**)&g->abits, sizeof(unsigned long long) * ((g->arcs + 63) / 64 + 1)));
   LPA_TRY(dev_alloc(g, (void**)&g->lab[0], sizeof(int32_t) * g->vpad));
   LPA_TRY(dev_alloc(g, (void**)&g->lab[1], sizeof(int32_t) * g->vpad));

@@ -203,8 +203,9 @@ struct lpa_graph {
   int32_t* al0 = nullptr;       // [arcs] or nullptr
   bool al_pending = false;
   uint32_t* gbits = nullptr;    // [vpad / 32] rebuild: bit u = (L[u] == G), the giant label
-  int32_t* gword = nullptr;     // [4] G of the last refreshed vector (k_giant_pick), worth-trying flag,
-                                //     abits valid (bits-mode rebuild, no scatter since)
+  int32_t* gword = nullptr;     // [8] G of the last refreshed vector (k_giant_pick), worth-trying flag,
+                                //     abits valid (bits-mode rebuild, no scatter since), [3] hot-slot
+                                //     giant-bit count (k_giant_bits), [4] superstep 4 bins: 0 = lists
   unsigned long long* abits = nullptr;  // [arcs / 64] bit i = (al[i] == G): the bits-mode rebuild's by-product
   int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
   uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])

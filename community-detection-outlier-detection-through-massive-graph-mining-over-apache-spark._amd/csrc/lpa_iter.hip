@@ -1511,12 +1511,61 @@ __global__ __launch_bounds__(256) void k_settle_rows(const int64_t* __restrict__
   }
 }
 
+// Superstep 4: the arc giant bits (bit i = al[i] == G) of the words covering positions
+// [p0, arcs) -- the rows below the hubs -- from the labels the scatter of superstep 3
+// left, so that k_settle_rows settles their G-majority rows by popcounts as in superstep
+// 3 (after superstep 3 nearly every row's strict majority is G: R-MAT 100 % of the arcs).
+// One streaming pass over 4 B/arc (the bins' giant decision cost ~2.5x that: LDS
+// histogram atomics, scalar-issue bound row batches); the next batch's loads are in
+// flight while a batch is packed.  gword[2] = 1: abits valid (G worth trying only).
+__global__ __launch_bounds__(256) void k_abits_pass(const int32_t* __restrict__ al, int64_t p0, int64_t arcs,
+                                                    int32_t* __restrict__ gword,
+                                                    unsigned long long* __restrict__ abits) {
+  if (gword[1] == 0) return;  // uniform: no settle this superstep (gword[2] stays 0)
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[2] = 1;
+  const u32 G = (u32)gword[0];
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t w1 = (arcs + 63) >> 6;
+  int64_t g = (p0 >> 6) + (((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) << 3);
+  const int64_t step = nw << 3;
+  u32 v[8];
+  auto load = [&](u32 (&x)[8], int64_t g0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = (g0 + k) * 64 + lane;
+      x[k] = i < arcs ? ld_stream(al + i) : ~G;
+    }
+  };
+  if (g < w1) load(v, g);
+  for (; g < w1; g += step) {
+    u32 vn[8];
+    if (g + step < w1) load(vn, g + step);
+    unsigned long long mine = 0ull;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const unsigned long long m = __ballot(v[k] == G);
+      if (lane == k) mine = m;
+    }
+    if (lane < 8 && g + lane < w1) abits[g + lane] = mine;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = vn[k];
+  }
+}
+
 // the settled superstep runs in list mode over the unsettled rows; the diff scans all
 __global__ void k_settle_commit(int32_t* __restrict__ fr_all, const int32_t* __restrict__ gword,
                                 int32_t* __restrict__ fcnt) {
   if (!settle_on(fr_all, gword)) return;
   *fr_all = 0;
   fcnt[kFcntSettled] = 1;
+}
+
+// superstep 4: the bins below the hubs walk the lists of their unsettled rows (gword[4]
+// = 0, their "fr_all") when the settle ran, their ranges otherwise; the hub units and the
+// combine keep fr_all = 1 (every hub row re-tallied, concurrently with the settle)
+__global__ void k_settle_commit4(const int32_t* __restrict__ fr_all, int32_t* __restrict__ gword) {
+  gword[4] = settle_on(fr_all, gword) ? 0 : 1;
 }
 
 // rebuild al[] when the changed vertices touch more than `thr` arcs (host-set)
@@ -1775,6 +1824,10 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
 // own label is not (Chung-Lu superstep 2: the mode holds 43 % of the arcs' columns, the
 // top hub's label 0.3 %).  One block, a 2K-slot LDS table.  The choice of G only
 // affects speed: every use of it is exact for any G.
+constexpr int kHotLabels = 32768;          // rank-strided label set (P > 1: power-of-two shares)
+constexpr int kHotLabelsSingle = 40960;    // P = 1: the whole 160 KB of LDS
+// bits mode: 1,310,688 slots' bits (the last LDS word counts the set bits first)
+constexpr int64_t kHotBits = 32ll * (kHotLabelsSingle - 1);
 constexpr int kPickK = 1024;
 __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__ L, int64_t n_real, int64_t S,
                                                      int P, int32_t* __restrict__ gword) {
@@ -1797,6 +1850,7 @@ __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__
     const int32_t G = (int32_t)(~(u32)m);
     if (G != gword[0]) gword[2] = 0;  // the arc giant bits are relative to the old G
     gword[0] = G;
+    gword[3] = 0;  // k_giant_bits counts the set bits of the hot slots here
     gword[1] = n > 0 && 5 * (int64_t)(m >> 32) >= n ? 1 : 0;
   }
 }
@@ -1804,7 +1858,7 @@ __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__
 template <bool kIfWanted>
 __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __restrict__ counters, int64_t thr,
                                                     const int32_t* __restrict__ L, int64_t n,
-                                                    const int32_t* __restrict__ gword,
+                                                    int32_t* __restrict__ gword,
                                                     unsigned long long* __restrict__ bits) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   const int32_t G = gword[0];
@@ -1824,6 +1878,68 @@ __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __
       if (lane == k) mine = m;
     }
     if (lane < 8 && g0 + lane * 64 < n) bits[(g0 >> 6) + lane] = mine;
+    // the hot slots' set bits (the rebuild's bits-mode test without an LDS fill)
+    if (g0 < kHotBits) {
+      const u32 c = wave_sum_u32(lane < 8 && g0 + lane * 64 < kHotBits ? (u32)__popcll(mine) : 0u);
+      if (lane == 0 && c) atomicAdd(&gword[3], (int32_t)c);
+    }
+  }
+}
+
+// al[i] = lab(col[i]) over every arc by the calling grid (one wave per 512-arc batch,
+// grid-stride); bits: also the arc giant bits (abits: bit i = al[i] == G, one ballot
+// per 64 arcs), which the next superstep's full tally settles rows from (k_settle_*).
+template <typename Lab>
+__device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, const int32_t* __restrict__ col,
+                                               int64_t arcs, int32_t* __restrict__ al,
+                                               unsigned long long* __restrict__ abits) {
+  // lane-consecutive arcs: one gather instruction covers 64 consecutive arcs of
+  // a row, whose sorted columns often share lines (hub rows) -> fewer L2 requests.
+  // Full 512-arc batches are software-pipelined: the next batch's column loads are in
+  // flight while this batch's labels are looked up and stored.
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t step = nw * 512;
+  const int64_t nfull = arcs & ~(int64_t)511;  // arcs of the full batches
+  int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512;
+  int32_t c[8];
+  if (base < nfull) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + base + k * 64 + lane);
+  }
+  for (; base < nfull; base += step) {
+    int32_t cn[8], r[8];
+    const int64_t nb = base + step;
+    if (nb < nfull) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cn[k] = __builtin_nontemporal_load(col + nb + k * 64 + lane);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = lab(c[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
+    if (bits) {
+      unsigned long long mine = 0ull;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const unsigned long long m = __ballot(r[k] == G);
+        if (lane == k) mine = m;
+      }
+      if (lane < 8) abits[(base >> 6) + lane] = mine;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = cn[k];
+  }
+  // the partial last batch (one wave)
+  if (nfull < arcs && base == nfull) {
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = base + k * 64 + lane;
+      const bool v = i < arcs;
+      const int32_t x = v ? lab(col[i]) : 0;
+      if (v) al[i] = x;
+      const unsigned long long m = __ballot(v && x == G);
+      if (bits && lane == 0 && base + k * 64 < arcs) abits[(base >> 6) + k] = m;
+    }
   }
 }
 
@@ -1840,10 +1956,6 @@ __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __
 // r's slice are its first slots (degree rank k lives at slot (k mod P) S + k / P),
 // so the global top set is the first H slots of every slice: slot c is hot iff
 // (c mod S) < H, at LDS index (c / S) H + c mod S (H = 2^hot_lg labels or 2^hb_lg bits).
-constexpr int kHotLabels = 32768;          // rank-strided label set (P > 1: power-of-two shares)
-constexpr int kHotLabelsSingle = 40960;    // P = 1: the whole 160 KB of LDS
-// bits mode: 1,310,688 slots' bits (the last LDS word counts the set bits first)
-constexpr int64_t kHotBits = 32ll * (kHotLabelsSingle - 1);
 template <bool kIfWanted, bool kRanked>
 __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long long* __restrict__ counters,
                                                          int64_t thr, const int32_t* __restrict__ col,
@@ -1903,54 +2015,35 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
       return (u32)c < nh ? (int32_t)hot[c] : Ln[c];
     }
   };
-  // lane-consecutive arcs: one gather instruction covers 64 consecutive arcs of
-  // a row, whose sorted columns often share lines (hub rows) -> fewer L2 requests.
-  // Full 512-arc batches are software-pipelined: the next batch's column loads are in
-  // flight while this batch's labels are looked up and stored.
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t step = nw * 512;
-  const int64_t nfull = arcs & ~(int64_t)511;  // arcs of the full batches
-  int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512;
-  int32_t c[8];
-  if (base < nfull) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + base + k * 64 + lane);
+  rebuild_stream(lab, G, bits, col, arcs, al, abits);
+}
+
+// al[] rebuild of a small label vector (P = 1, < kHotMinSlots slots: it stays in L2 /
+// the Infinity Cache, so an LDS hot set saves no misses while every block's 160 KB fill
+// costs as much as the arcs' stream at C2 scale): the same bits / labels modes, the
+// bits-mode test from k_giant_bits' count of the hot slots' set bits (gword[3]).
+constexpr int64_t kHotMinSlots = 4ll << 20;
+template <bool kIfWanted>
+__global__ __launch_bounds__(256) void k_al_rebuild_small(const unsigned long long* __restrict__ counters,
+                                                          int64_t thr, const int32_t* __restrict__ col, int64_t arcs,
+                                                          const int32_t* __restrict__ Ln, int32_t* __restrict__ al,
+                                                          const uint32_t* __restrict__ gbits, int64_t nbits,
+                                                          int32_t* __restrict__ gword,
+                                                          unsigned long long* __restrict__ abits) {
+  if (kIfWanted && !rebuild_wanted(counters, thr)) return;
+  const int64_t nhb = nbits < kHotBits ? nbits : kHotBits;
+  const bool bits = nhb > 0 && 2 * (int64_t)gword[3] >= nhb;  // uniform
+  const int32_t G = gword[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[2] = bits ? 1 : 0;
+  if (!bits) {  // labels mode: the plain 16 B/lane gather stream (C2: 0.21 -> ~0.17 ms)
+    rebuild_all(col, arcs, Ln, al);
+    return;
   }
-  for (; base < nfull; base += step) {
-    int32_t cn[8], r[8];
-    const int64_t nb = base + step;
-    if (nb < nfull) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) cn[k] = __builtin_nontemporal_load(col + nb + k * 64 + lane);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r[k] = lab(c[k]);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
-    if (bits) {
-      unsigned long long mine = 0ull;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const unsigned long long m = __ballot(r[k] == G);
-        if (lane == k) mine = m;
-      }
-      if (lane < 8) abits[(base >> 6) + lane] = mine;
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = cn[k];
-  }
-  // the partial last batch (one wave)
-  if (nfull < arcs && base == nfull) {
-    for (int k = 0; k < 8; ++k) {
-      const int64_t i = base + k * 64 + lane;
-      const bool v = i < arcs;
-      const int32_t x = v ? lab(col[i]) : 0;
-      if (v) al[i] = x;
-      const unsigned long long m = __ballot(v && x == G);
-      if (bits && lane == 0 && base + k * 64 < arcs) abits[(base >> 6) + k] = m;
-    }
-  }
+  auto lab = [&](int c) -> int32_t {
+    if ((gbits[(u32)c >> 5] >> ((u32)c & 31u)) & 1u) return G;
+    return Ln[c];
+  };
+  rebuild_stream(lab, G, true, col, arcs, al, abits);
 }
 
 __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __restrict__ new_of,
@@ -2099,13 +2192,15 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
 // rows after the hub combine), overlapping most of the diff with the tally tail
 // the per-bin dirty-row lists of this superstep (zeroes the other parity's counts)
-int launch_frontier_lists(lpa_graph* g) {
+int launch_frontier_lists(lpa_graph* g, hipStream_t st = nullptr, const int32_t* fr = nullptr) {
+  if (!st) st = g->stream;
+  if (!fr) fr = g->fr_all + g->par;
   BinBounds bnd;
   for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = g->bin_begin[b];
   const int64_t nbr = (g->slice + kListTile - 1) / kListTile;
   const int64_t nbu = (g->n_segs + kListTile - 1) / kListTile;
-  hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, g->stream, g->rdirty[g->par],
-                     g->slice, g->udirty[g->par], g->n_segs, bnd, g->fr_all + g->par, g->flist, g->ulist,
+  hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, st, g->rdirty[g->par],
+                     g->slice, g->udirty[g->par], g->n_segs, bnd, fr, g->flist, g->ulist,
                      g->fcnt + 16 * g->par, g->fcnt + 16 * (g->par ^ 1), nbr);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
@@ -2152,23 +2247,58 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // superstep 3: rows settled from the arc giant bits of superstep 2's rebuild (each
   // kernel returns at once unless they are valid): the others' dirty flags, then the
   // lists of this superstep are built from them in list mode
-  if (g->since_reset == 2 && g->abits && !block_mode_now(g)) {
-    if (g->n_hub > 0) {
-      hipLaunchKernelGGL(k_settle_big, dim3(cap_grid((g->n_hub + 3) / 4, 2048)), dim3(256), 0, s, g->rp, g->abits,
-                         g->n_hub, fr_all, g->gword, Lown, g->rdirty[g->par], g->udirty[g->par], g->hub_uoff);
-      LPA_HIP(hipGetLastError());
+  // superstep 4 (one GPU): the same settle for the rows below the hubs, from a fresh
+  // abits pass, on aux0 while the main stream re-tallies every hub unit and row (range
+  // mode: their staged words are current again for the frontier supersteps); the bins
+  // below the hubs then walk their unsettled rows' lists (fr_bins = gword[4])
+  const bool settle4 = g->since_reset == 3 && !exchanges(g) && g->abits != nullptr;
+  const int32_t* fr_bins = settle4 ? g->gword + 4 : fr_all;
+  if (settle4) {
+    if (!g->serial) {
+      LPA_HIP(hipEventRecord(g->ev_fork, s));
+      LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
     }
+    const int64_t p0 = g->bin_arcs[0];
+    const int64_t nwd = (g->arcs + 63) / 64 - p0 / 64;
+    hipLaunchKernelGGL(k_abits_pass, dim3(cap_grid((nwd + 31) / 32, 8192)), dim3(256), 0, sb, g->al, p0, g->arcs,
+                       g->gword, g->abits);
+    LPA_HIP(hipGetLastError());
     const int64_t r0 = g->n_hub, r1 = g->bin_begin[BIN_ISO];
     if (r1 > r0) {
-      hipLaunchKernelGGL(k_settle_rows, dim3(cap_grid((r1 - r0 + 255) / 256, 8192)), dim3(256), 0, s, g->rp,
+      hipLaunchKernelGGL(k_settle_rows, dim3(cap_grid((r1 - r0 + 255) / 256, 8192)), dim3(256), 0, sb, g->rp,
                          g->abits, r0, r1, fr_all, g->gword, Lown, g->rdirty[g->par]);
       LPA_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_settle_commit, dim3(1), dim3(1), 0, s, const_cast<int32_t*>(fr_all), g->gword, fcnt);
+    hipLaunchKernelGGL(k_settle_commit4, dim3(1), dim3(1), 0, sb, fr_all, g->gword);
     LPA_HIP(hipGetLastError());
+    LPA_TRY(launch_frontier_lists(g, sb, fr_bins));
+    if (!g->serial) {
+      LPA_HIP(hipEventRecord(g->ev_join2[2], sb));
+      LPA_HIP(hipStreamWaitEvent(sc, g->ev_join2[2], 0));
+    }
+  } else {
+    // superstep 3: rows settled from the arc giant bits of superstep 2's rebuild (each
+    // kernel returns at once unless they are valid): the others' dirty flags, then the
+    // lists of this superstep are built from them in list mode
+    if (g->since_reset == 2 && g->abits && !block_mode_now(g)) {
+      if (g->n_hub > 0) {
+        hipLaunchKernelGGL(k_settle_big, dim3(cap_grid((g->n_hub + 3) / 4, 2048)), dim3(256), 0, s, g->rp,
+                           g->abits, g->n_hub, fr_all, g->gword, Lown, g->rdirty[g->par], g->udirty[g->par],
+                           g->hub_uoff);
+        LPA_HIP(hipGetLastError());
+      }
+      const int64_t r0 = g->n_hub, r1 = g->bin_begin[BIN_ISO];
+      if (r1 > r0) {
+        hipLaunchKernelGGL(k_settle_rows, dim3(cap_grid((r1 - r0 + 255) / 256, 8192)), dim3(256), 0, s, g->rp,
+                           g->abits, r0, r1, fr_all, g->gword, Lown, g->rdirty[g->par]);
+        LPA_HIP(hipGetLastError());
+      }
+      hipLaunchKernelGGL(k_settle_commit, dim3(1), dim3(1), 0, s, const_cast<int32_t*>(fr_all), g->gword, fcnt);
+      LPA_HIP(hipGetLastError());
+    }
+    // frontier lists of this superstep (no-op when every row is tallied)
+    LPA_TRY(launch_frontier_lists(g));
   }
-  // frontier lists of this superstep (no-op when every row is tallied)
-  LPA_TRY(launch_frontier_lists(g));
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (!g->serial) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
@@ -2186,9 +2316,12 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // peel rounds of the wave / unit / block tallies (LPA_DENSE_PEEL in the label-dense
   // supersteps, where a round rarely retires more than a few votes)
   const int pmax = g->since_reset < kDenseSupersteps ? kDensePeel : kPeelMax;
-  // peel rounds of the row bins before a chunk is hashed: none in the label-dense
-  // supersteps (measured best of 0/1/2/3 at C3), kPeelSortAfter otherwise
-  const int sort_after = g->since_reset < kDenseSupersteps ? 0 : kPeelSortAfter;
+  // peel rounds of the row bins (range mode) before a chunk is hashed: none in the
+  // label-dense supersteps (measured best of 0/1/2/3 at C3), one in supersteps 3 and 4
+  // (C2's rows are still label-dense there: 0.59 -> 0.52 ms each; both are launched
+  // eagerly, so no captured graph bakes the value), kPeelSortAfter after that (1 there:
+  // C3's converged supersteps +10 %)
+  const int sort_after = g->since_reset < kDenseSupersteps ? 0 : g->since_reset <= 3 ? 1 : kPeelSortAfter;
   // superstep 2 in block mode: every hub row by giant counts first (k_lpa_units_giant
   // over all units, k_hub_decide); only the rows it cannot settle are tallied exactly --
   // block-tier rows by k_lpa_block from glist, the longer ones by their units
@@ -2205,9 +2338,9 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   auto launch_block_wide = [&](hipStream_t st) -> int {
     const int64_t h2 = g->hub_block2_begin, hl = g->hub_lane_begin;
     if (hl > h2) {
-      // giant mode: few undecided rows, so few fat blocks (a 128 KB-LDS block per CU
-      // would wait for the concurrent bins' blocks to leave)
-      hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, giant_units ? 32 : 1024)),
+      // (giant mode: the undecided rows only; a grid sized to few rows measured slower
+      // at C5, superstep 2 48.7 -> 54.3 ms, and the same at C3)
+      hipLaunchKernelGGL((k_lpa_block<14, kBlockMaxDeg2 / kSegArcs>), dim3(cap_grid(hl - h2, 1024)),
                          dim3(kBlockMaxDeg2 / kSegArcs * 64), 0, st, g->rp, g->al, Lown, h2, hl, blist, bcnt,
                          ball, pmax, bsel);
       LPA_HIP(hipGetLastError());
@@ -2217,7 +2350,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // rows <= 4096 (8 waves, 8K slots, two blocks per CU)
   auto launch_block_narrow = [&](hipStream_t st) -> int {
     const int64_t nb = g->n_hub - g->hub_lane_begin;
-    hipLaunchKernelGGL((k_lpa_block<13, kBlockMaxDeg / kSegArcs>), dim3(cap_grid(nb, giant_units ? 64 : 2048)),
+    hipLaunchKernelGGL((k_lpa_block<13, kBlockMaxDeg / kSegArcs>), dim3(cap_grid(nb, 2048)),
                        dim3(kBlockMaxDeg / kSegArcs * 64), 0, st, g->rp, g->al, Lown, g->hub_lane_begin, g->n_hub,
                        blist, bcnt, ball, pmax, bsel);
     LPA_HIP(hipGetLastError());
@@ -2282,7 +2415,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(mark(2 * (BIN + 1), sc));                                                        \
     if (n > 0) {                                                                             \
       hipLaunchKernelGGL(k_lpa_group<G>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
-                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_all); \
+                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_bins); \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
@@ -2302,14 +2435,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   }
   // stream balance (measured steady superstep): aux0 w16 + w8 + w4, aux1 w2 + the
   // row/group bins
-  LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_all)
-  LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_all)
-  LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_all)
-  LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_all)
-  LPA_ROWS_LAUNCH(BIN_G64, 64, fr_all)
-  LPA_ROWS_LAUNCH(BIN_G32, 32, fr_all)
-  LPA_ROWS_LAUNCH(BIN_G16, 16, fr_all)
-  LPA_ROWS_LAUNCH(BIN_G8, 8, fr_all)
+  LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_bins)
+  LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_bins)
+  LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_bins)
+  LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_bins)
+  LPA_ROWS_LAUNCH(BIN_G64, 64, fr_bins)
+  LPA_ROWS_LAUNCH(BIN_G32, 32, fr_bins)
+  LPA_ROWS_LAUNCH(BIN_G16, 16, fr_bins)
+  LPA_ROWS_LAUNCH(BIN_G8, 8, fr_bins)
   LPA_GROUP_LAUNCH(BIN_G4, 4)
   LPA_GROUP_LAUNCH(BIN_G2, 2)
   LPA_GROUP_LAUNCH(BIN_G1, 1)
@@ -2361,7 +2494,21 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
   const auto pow2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
   const bool ranked = g->nranks > 1 && pow2(g->nranks) && pow2(g->slice) && g->nranks <= kHotLabels &&
                       g->slice >= kHotLabels / g->nranks;
-  if (g->rebuild_hot && (g->nranks == 1 || ranked)) {
+  if (g->rebuild_hot && g->nranks == 1 && g->vpad < kHotMinSlots) {
+    const int64_t ngrp = (g->vpad + 511) / 512;
+    const unsigned gb = cap_grid((ngrp + 3) / 4, 4096), gr = cap_grid((g->arcs + 2047) / 2048, 8192);
+    if (if_wanted) {
+      hipLaunchKernelGGL(k_giant_bits<true>, dim3(gb), dim3(256), 0, s, ctr, thr, L, g->vpad, g->gword,
+                         (unsigned long long*)g->gbits);
+      hipLaunchKernelGGL(k_al_rebuild_small<true>, dim3(gr), dim3(256), 0, s, ctr, thr, g->col, g->arcs, L, g->al,
+                         g->gbits, g->vpad, g->gword, g->abits);
+    } else {
+      hipLaunchKernelGGL(k_giant_bits<false>, dim3(gb), dim3(256), 0, s, ctr, thr, L, g->vpad, g->gword,
+                         (unsigned long long*)g->gbits);
+      hipLaunchKernelGGL(k_al_rebuild_small<false>, dim3(gr), dim3(256), 0, s, ctr, thr, g->col, g->arcs, L, g->al,
+                         g->gbits, g->vpad, g->gword, g->abits);
+    }
+  } else if (g->rebuild_hot && (g->nranks == 1 || ranked)) {
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
     int slice_lg = 0, hot_lg = 0, hb_lg = 0;
