@@ -1943,6 +1943,93 @@ __device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, co
   }
 }
 
+// The same stream in a three-stage software pipeline over 512-arc batches (P = 1 hot
+// kernel): at step t the column loads of batch t + 3 are issued, batch t + 2's probe
+// words fetched (p1: an LDS word, or an L2 word of gbits for a cold column), batch
+// t + 1's labels resolved (p2: from the word, else a gather of L[c]) and batch t stored,
+// so each wave keeps three batches' dependent loads in flight instead of one batch's
+// chain (col -> bit word -> label).  Rings of 3 column sets and 2 word / label sets,
+// six steps unrolled so no set is copied while its loads are in flight.
+template <typename P1, typename P2>
+__device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits, const int32_t* __restrict__ col,
+                                             int64_t arcs, int32_t* __restrict__ al,
+                                             unsigned long long* __restrict__ abits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t step = nw * 512;
+  const int64_t nfull = arcs & ~(int64_t)511;
+  int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512;
+  auto L = [&](int32_t (&c)[8], int64_t b) {
+    if (b < nfull) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + b + k * 64 + lane);
+    }
+  };
+  auto Q1 = [&](const int32_t (&c)[8], u32 (&w)[8], int64_t b) {
+    if (b < nfull) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w[k] = p1(c[k]);
+    }
+  };
+  auto Q2 = [&](const int32_t (&c)[8], const u32 (&w)[8], int32_t (&r)[8], int64_t b) {
+    if (b < nfull) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = p2(c[k], w[k]);
+    }
+  };
+  auto S = [&](const int32_t (&r)[8], int64_t b) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + b + k * 64 + lane);
+    if (bits) {
+      unsigned long long mine = 0ull;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const unsigned long long m = __ballot(r[k] == G);
+        if (lane == k) mine = m;
+      }
+      if (lane < 8) abits[(b >> 6) + lane] = mine;
+    }
+  };
+  int32_t c0[8], c1[8], c2[8], r0[8], r1[8];
+  u32 w0[8], w1[8];
+  if (base < nfull) {
+    L(c0, base);
+    L(c1, base + step);
+    L(c2, base + 2 * step);
+    Q1(c0, w0, base);
+    Q1(c1, w1, base + step);
+    Q2(c0, w0, r0, base);
+#define LPA_PIPE_STEP(CA, CB, CC, WA, WB, RA, RB) \
+    L(CA, base + 3 * step);                       \
+    Q1(CC, WA, base + 2 * step);                  \
+    Q2(CB, WB, RB, base + step);                  \
+    S(RA, base);                                  \
+    base += step;                                 \
+    if (base >= nfull) break;
+    while (true) {
+      LPA_PIPE_STEP(c0, c1, c2, w0, w1, r0, r1)
+      LPA_PIPE_STEP(c1, c2, c0, w1, w0, r1, r0)
+      LPA_PIPE_STEP(c2, c0, c1, w0, w1, r0, r1)
+      LPA_PIPE_STEP(c0, c1, c2, w1, w0, r1, r0)
+      LPA_PIPE_STEP(c1, c2, c0, w0, w1, r0, r1)
+      LPA_PIPE_STEP(c2, c0, c1, w1, w0, r1, r0)
+    }
+#undef LPA_PIPE_STEP
+  }
+  // the partial last batch (one wave)
+  if (nfull < arcs && base == nfull) {
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = base + k * 64 + lane;
+      const bool v = i < arcs;
+      const int32_t c = v ? col[i] : 0;
+      const int32_t x = v ? p2(c, p1(c)) : 0;
+      if (v) al[i] = x;
+      const unsigned long long m = __ballot(v && x == G);
+      if (bits && lane == 0 && base + k * 64 < arcs) abits[(base >> 6) + k] = m;
+    }
+  }
+}
+
 // al[] rebuild with an LDS hot set (the slots of the highest-degree vertices: at P = 1
 // the first slots, 30-40 % of all arc targets on R-MAT).  The rebuild is bound by the
 // line traffic of its L2-missing 4-B gathers, and every gather served from LDS is one
@@ -2015,7 +2102,19 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
       return (u32)c < nh ? (int32_t)hot[c] : Ln[c];
     }
   };
-  rebuild_stream(lab, G, bits, col, arcs, al, abits);
+  if constexpr (kRanked) {
+    rebuild_stream(lab, G, bits, col, arcs, al, abits);
+  } else {
+    auto p1 = [&](int c) -> u32 {
+      if (bits) return (u32)c < (u32)nhb ? hot[(u32)c >> 5] : gbits[(u32)c >> 5];
+      return (u32)c < nh ? hot[c] : 0u;
+    };
+    auto p2 = [&](int c, u32 w) -> int32_t {
+      if (bits) return ((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c];
+      return (u32)c < nh ? (int32_t)w : Ln[c];
+    };
+    rebuild_pipe(p1, p2, G, bits, col, arcs, al, abits);
+  }
 }
 
 // al[] rebuild of a small label vector (P = 1, < kHotMinSlots slots: it stays in L2 /
