@@ -316,6 +316,7 @@ def main():
     progress("timed calls")
     # ---- timed: K labelPropagation(10) calls, supersteps 2..10 of each ----
     t_sum = 0.0
+    call_ms = []
     for _ in range(args.steps):
         g.reset()
         g.step(1)                      # superstep 1 (from L0), untimed
@@ -325,12 +326,16 @@ def main():
         g.step(MAX_ITER - 1)           # supersteps 2..10: no per-kernel events
         torch.cuda.synchronize()
         barrier()
-        t_sum += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        t_sum += dt
+        call_ms.append(dt * 1e3)
     t_sum = max_over_ranks(t_sum)
     n_timed = (MAX_ITER - 1) * args.steps
     value = m * n_timed / t_sum / 1e9
 
-    progress(f"timed: {value:.1f} GTEPS; per-superstep method")
+    cs = sorted(call_ms)
+    progress(f"timed: {value:.1f} GTEPS (per call ms: min {cs[0]:.3f} median {cs[len(cs) // 2]:.3f} "
+             f"max {cs[-1]:.3f}); per-superstep method")
     # ---- BASELINE.md:48 method: median superstep time of iterations 2..10 over >= 5
     # runs (HIP events around each superstep, concurrent schedule, graphs replayed) ----
     runs = max(5, args.steps)
@@ -431,6 +436,7 @@ def main():
         "timed_window": f"supersteps 2..{MAX_ITER} of each of {args.steps} labelPropagation(maxIter={MAX_ITER}) "
                         f"calls ({n_timed} supersteps); step = one call",
         "ms_per_superstep": round(t_sum * 1e3 / n_timed, 4),
+        "call_ms_min_median_max": [round(cs[0], 4), round(cs[len(cs) // 2], 4), round(cs[-1], 4)],
         "baseline_method": {
             "what": f"BASELINE.md:48: median superstep time over iterations 2..{MAX_ITER}, {runs} runs, HIP events",
             "median_iter_ms": round(med_ms, 4),

@@ -221,7 +221,9 @@ struct lpa_graph {
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
-  hipGraphExec_t gexec[4] = {};             // captured converged superstep per (cur, par)
+  // captured supersteps: [0, 4) converged per (cur, par); [4, 16) supersteps 2..4 per
+  // (superstep, cur, par)
+  hipGraphExec_t gexec[16] = {};
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 

@@ -2799,6 +2799,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // (supersteps 3 and 4 too: the row settle is launched only in superstep 3, and
     // superstep 4 reads the giant word of the labels it tallies)
     const int eager = kDenseSupersteps + 2;
+    const bool early_graph = g->use_graphs && !exchanges(g) && !g->serial && !first && g->since_reset >= 1 &&
+                             g->since_reset < eager;
     if (g->use_graphs && !exchanges(g) && !g->serial && g->since_reset >= eager) {
       const int key = g->cur * 2 + g->par;
       if (!g->gexec[key])
@@ -2829,6 +2831,18 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
     } else if (first) {
       LPA_TRY(launch_first(g, Lown));
+    } else if (early_graph) {
+      // supersteps 2..4 on one GPU: a captured graph per (superstep, cur, par) too --
+      // each has its own fixed schedule (giant decision, row settle, superstep-4 settle),
+      // and ~40-50 launches each are one graph launch
+      const int key = 4 + ((g->since_reset - 1) * 2 + g->cur) * 2 + g->par;
+      if (!g->gexec[key])
+        LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
+          int rc = launch_tally(g, Lown, nullptr, Lc, Ln, true);
+          if (rc == LPA_OK) rc = launch_refresh(g, Lc, Ln, true, g->par);
+          return rc;
+        }));
+      LPA_HIP(hipGraphLaunch(g->gexec[key], s));
     } else {
       LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
     }
@@ -2841,7 +2855,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
     // (changes + refresh); a refresh here would see a partial vector
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));  // stays if there is no refresh
-    if (!exchanges(g) || has_collective(g))
+    if ((!exchanges(g) || has_collective(g)) && !early_graph)
       LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par,
                              bev ? bev[kTallyEv + 2] : nullptr));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 3], s));
