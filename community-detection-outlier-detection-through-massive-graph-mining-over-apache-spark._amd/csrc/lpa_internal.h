@@ -221,7 +221,7 @@ struct lpa_graph {
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
-  // captured supersteps: [0, 4) converged per (cur, par); [4, 16) supersteps 2..4 per
+  // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per
   // (superstep, cur, par)
   hipGraphExec_t gexec[16] = {};
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)

@@ -2799,8 +2799,10 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // (supersteps 3 and 4 too: the row settle is launched only in superstep 3, and
     // superstep 4 reads the giant word of the labels it tallies)
     const int eager = kDenseSupersteps + 2;
+    // supersteps 2 and 3 (not 4: its settle chain on aux0 stops overlapping the hub
+    // units inside a graph, 0.67 -> 0.75 ms at C3)
     const bool early_graph = g->use_graphs && !exchanges(g) && !g->serial && !first && g->since_reset >= 1 &&
-                             g->since_reset < eager;
+                             g->since_reset <= 2;
     if (g->use_graphs && !exchanges(g) && !g->serial && g->since_reset >= eager) {
       const int key = g->cur * 2 + g->par;
       if (!g->gexec[key])
@@ -2832,9 +2834,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     } else if (first) {
       LPA_TRY(launch_first(g, Lown));
     } else if (early_graph) {
-      // supersteps 2..4 on one GPU: a captured graph per (superstep, cur, par) too --
-      // each has its own fixed schedule (giant decision, row settle, superstep-4 settle),
-      // and ~40-50 launches each are one graph launch
+      // supersteps 2 and 3 on one GPU: a captured graph per (superstep, cur, par) too --
+      // each has its own fixed schedule (giant decision, row settle), and their ~40-50
+      // launches become one graph launch (C2: supersteps 2-3 0.46 / 0.50 -> 0.41 / 0.45 ms)
       const int key = 4 + ((g->since_reset - 1) * 2 + g->cur) * 2 + g->par;
       if (!g->gexec[key])
         LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
