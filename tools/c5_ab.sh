@@ -11,6 +11,6 @@ for v in "${VARS[@]}"; do
   env $v timeout -k 10 ${LIMIT:-400} python3 -u bench.py --config C5 --no-cpu-baseline --no-outlier --steps 2 --warmup 1 > gpurun_out/${TAG}_v$k.json 2> gpurun_out/${TAG}_v$k.err || { tail -5 gpurun_out/${TAG}_v$k.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('gpurun_out/${TAG}_v$k.json'))
-print(d['value'], d['ms_per_superstep'], d['baseline_method']['median_ms_per_superstep_2_to_10'], d['run_maxiter10_ms'], d.get('roofline_rebuild', {}) and d['roofline_rebuild']['avg_launch_ms'])"
+print(d['value'], d['ms_per_superstep'], d['baseline_method']['median_ms_per_superstep_2_to_10'], d['run_maxiter10_ms'], d['roofline']['avg_launch_ms'])"
   k=$((k+1))
 done
