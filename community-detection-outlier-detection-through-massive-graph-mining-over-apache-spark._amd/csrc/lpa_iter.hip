@@ -150,6 +150,16 @@ __device__ __forceinline__ u32 wave_max_u32(u32 v) {
   return max(max((u32)__builtin_amdgcn_readlane((int)v, 0), (u32)__builtin_amdgcn_readlane((int)v, 16)),
              max((u32)__builtin_amdgcn_readlane((int)v, 32), (u32)__builtin_amdgcn_readlane((int)v, 48)));
 }
+// u64 max as two 32-bit reductions (the high words, then the low words of the lanes
+// holding that high word): each DPP step is one v_max_u32 instead of two moves, a
+// 64-bit compare and two selects -- fewer VALU issues, a longer dependent chain, so it
+// serves only the issue-bound g64 row hash (C2 60.4 -> 61.6 GTEPS; as every kernel's
+// wave max, C3's latency-bound converged supersteps lost 1.5 %)
+__device__ __forceinline__ u64 wave_max_u64_split(u64 v) {
+  const u32 hi = wave_max_u32((u32)(v >> 32));
+  const u32 lo = wave_max_u32((u32)(v >> 32) == hi ? (u32)v : 0u);
+  return ((u64)hi << 32) | lo;
+}
 
 __device__ __forceinline__ u32 hash_slot(u32 label, int shift) {
   return (label * 0x9E3779B1u) >> shift;
@@ -443,7 +453,7 @@ __device__ __forceinline__ u64 group_mode_hash(u32 v, int lane, u64* tab) {
     gt[h] = 0ull;
   }
   if constexpr (G == 64) {
-    return wave_max_u64(w);
+    return wave_max_u64_split(w);
   } else {
 #pragma unroll
     for (int off = G >> 1; off > 0; off >>= 1) {
