@@ -4,12 +4,14 @@
 
 Workloads (synthetic, generated in HBM; CSR construction not timed):
   C3  R-MAT scale 24, edgefactor 16 (16.7 M V / 268 M E)          default at N = 1
-      N > 1 default: R-MAT scale 24 + log2 N (weak scaling, 268 M edges per GPU;
-      N = 4 is C4), every rank holding 1/N of the arcs
-  C4  R-MAT scale 26, edgefactor 16 (67 M V / 1.07 B E)            (--config C4, any N)
-  C5  Chung-Lu gamma 2.1, 40 M V / 1.4 B E, max degree ~1.25 M (--config C5)
+  C4  R-MAT scale 26, edgefactor 16 (67 M V / 1.07 B E)            default at N > 1
+      (BASELINE config 4: "vertex-partitioned across 2/4/8 MI355X"), strong scaling:
+      the same graph split over the N ranks, every rank holding ~1/N of the arcs
+  C5  Chung-Lu gamma 2.1, 40 M V / 1.4 B E, max degree ~1.25 M (--config C5; BASELINE
+      config 5 is quoted at 8 GPUs)
   C2  planted-partition SBM, 1 M V / 20 M E, 100 blocks            (--config C2)
-  A --config at N > 1 is strong scaling (the same graph split over the N ranks).
+  --weak (N a power of two): R-MAT scale 24 + log2 N instead, 268 M edges per GPU
+  (N = 4 is C4; scale 27 at N = 8 has no at-size parity test: unvalidated).
 
 --gpus N > 1 without a torch.distributed environment re-launches this script under
 torch.distributed.run (one rank per GPU) as a child process, before any GPU call.
@@ -51,7 +53,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
 # measured HBM traffic per launch of the dominant kernels: rocprofv3 --pmc FETCH_SIZE /
 # WRITE_SIZE passes over the C3 workload (tools/pmc_r03.sh; FETCH doubled per the gfx950
 # correction, calibrated on a known-byte stream in profiles/r02/traffic)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", "r03", "traffic", "pmc_traffic.json"),
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", "r04", "traffic", "pmc_traffic.json"),
+                 os.path.join(ROOT, "profiles", "r03", "traffic", "pmc_traffic.json"),
                  os.path.join(ROOT, "profiles", "r02", "traffic", "pmc_traffic.json"),
                  os.path.join(ROOT, "profiles", "r01", "e_traffic", "pmc_traffic.json")]
 
@@ -233,6 +236,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1, help="untimed labelPropagation(10) calls")
     ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
                     help="default C3 at N = 1, C4 at N > 1")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: weak scaling from C3 (R-MAT scale 24 + log2 N; N a power of two)")
     ap.add_argument("--scale", type=int, default=None, help="R-MAT scale override (custom config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-outlier", action="store_true")
@@ -249,12 +254,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     args.gpus = world
     scaling = "strong"
-    if args.config is None and args.scale is None and world > 1:
+    if args.weak and world > 1 and args.config is None and args.scale is None:
         # weak scaling from C3: 2^24 * N vertices, 268 M edges per GPU (N = 4: C4)
-        lg = world.bit_length() - 1
-        args.scale = 24 + lg
+        if world & (world - 1):
+            raise SystemExit(f"--weak needs a power-of-two rank count (268 M edges per GPU), got {world}")
+        args.scale = 24 + world.bit_length() - 1
         scaling = "weak"
-    config_id = args.config or "C3"
+    # N > 1 default: BASELINE config 4, R-MAT-26 partitioned over the N ranks
+    config_id = args.config or ("C4" if world > 1 and args.scale is None else "C3")
     cfg = dict(CONFIGS[config_id])
     if args.scale is not None:
         if cfg["kind"] != "rmat":
@@ -358,6 +365,9 @@ def main():
         off_ms.append(g.step(MAX_ITER - 1, stats=True)["iter_ms"])
     g.set_frontier(True)
     conv_ms = max_over_ranks(statistics.median(x for r in off_ms for x in r[2:]))  # supersteps 4..10
+    # full-work figure: supersteps 2..10 with the frontier off (every row tallied every
+    # superstep; only the exact giant-label settles of supersteps 3-4 still skip reads)
+    full_ms = max_over_ranks(statistics.median(sum(r) for r in off_ms))
 
     progress("lpa_run(10) wall time")
     # ---- whole call: lpa_run(10) from reset, labels gathered into a device tensor ----
@@ -372,6 +382,12 @@ def main():
         barrier()
         run_ms.append((time.perf_counter() - t0) * 1e3)
     run_ms = max_over_ranks(statistics.median(run_ms))
+    # superstep 1 (from L0, column runs + the first al[] rebuild) of those calls, events
+    ss1 = []
+    for _ in range(3):
+        g.reset()
+        ss1.append(g.step(1, stats=True)["iter_ms"][0])
+    ss1_ms = max_over_ranks(statistics.median(ss1))
     # partition quality of the labels of that call (rank 0: the full dense vector)
     quality = None
     if rank == 0 and not args.no_quality:
@@ -411,6 +427,10 @@ def main():
     S = info["slice"]
     iter_bytes = 8 * info["arcs"] + 12 * S + 8     # SURVEY §8(d) contract, this rank's share
     moved = moved_bytes_converged(info)
+    # contract roofline of the whole job: every rank moves its share at 8 TB/s at once
+    roof_gteps = m / (iter_bytes / (HBM_PEAK_GBS * 1e9)) / 1e9
+    full_gteps = m * (MAX_ITER - 1) / (full_ms * 1e-3) / 1e9
+    call_gteps = m * MAX_ITER / (run_ms * 1e-3) / 1e9
 
     tally_obj = {
         "bound": "hbm",
@@ -464,7 +484,8 @@ def main():
             "vertices": V, "edges": m, "arcs_rank0": info["arcs"],
             "parallelism": f"1D degree-ranked vertex partition x{world}, RCCL label allgather",
             "scaling_note": ("weak: R-MAT scale 24 + log2 N, 268 M edges per GPU" if scaling == "weak" else
-                             "the same graph at every N"),
+                             "strong: the same graph at every N (N = 1 default C3, the north-star config; "
+                             "N > 1 default C4, BASELINE's partitioned config)"),
         },
         "timed_window": f"supersteps 2..{MAX_ITER} of each of {args.steps} labelPropagation(maxIter={MAX_ITER}) "
                         f"calls ({n_timed} supersteps); step = one call",
@@ -484,12 +505,33 @@ def main():
         "roofline": rb_obj if rb_obj is not None else tally_obj,
         "roofline_tally": tally_obj,
         "iteration_roofline": {
-            "what": ("north_star 'fraction of HBM-roofline TEPS': value / (m / (B_iter / 8 TB/s)), B_iter = "
-                     "SURVEY §8(d) contract bytes 16m+12V+8 of one superstep (8 B/arc: col + gathered label)"),
+            "what": ("north_star 'fraction of HBM-roofline TEPS' against the SURVEY §8(d) contract: B_iter = "
+                     "16m+12V+8 bytes per superstep (col 4 B/arc + gathered label 4 B/arc + row offsets + label "
+                     "write), roofline TEPS = m / (B_iter / 8 TB/s).  frac = the full-work figure (every row "
+                     "tallied every superstep) over that roofline"),
             "bytes": iter_bytes,
-            "roofline_gteps": round(m / (iter_bytes / (HBM_PEAK_GBS * 1e9)) / 1e9, 1),
-            "frac": round(value / (m / (iter_bytes / (HBM_PEAK_GBS * 1e9)) / 1e9), 4),
-            "ms_per_superstep": round(t_sum * 1e3 / n_timed, 4),
+            "roofline_gteps": round(roof_gteps, 1),
+            "frac": round(full_gteps / roof_gteps, 4),
+            "full_work": {
+                "what": f"supersteps 2..{MAX_ITER} with the frontier OFF (every row re-tallied; the exact "
+                        f"giant-label row settles of supersteps 3-4 stay on), median of 3 calls, HIP events",
+                "ms": round(full_ms, 4),
+                "gteps": round(full_gteps, 2),
+                "frac": round(full_gteps / roof_gteps, 4),
+            },
+            "whole_call": {
+                "what": f"lpa_run({MAX_ITER}) wall time from reset: supersteps 1..{MAX_ITER} + labels gathered "
+                        f"to HBM (median of 3)",
+                "ms": round(run_ms, 4),
+                "superstep1_ms": round(ss1_ms, 4),
+                "gteps": round(call_gteps, 2),
+                "frac": round(call_gteps / roof_gteps, 4),
+            },
+            "shipped_vs_contract_roofline": round(value / roof_gteps, 4),
+            "shipped_note": ("value (frontier on) over the contract roofline TEPS: a time-to-result ratio, NOT a "
+                             "bandwidth fraction -- the exact frontier and the giant-label settle skip most rows "
+                             "after superstep 4, so the shipped window moves far fewer bytes than B_iter per "
+                             "superstep"),
         },
         "moved_bytes_frac": round(moved / (conv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "moved_bytes_note": (f"{moved} B the replicated-label formulation moves per converged superstep "

@@ -643,6 +643,15 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     LPA_HIP(hipMemcpyAsync(g->al0, g->al, sizeof(int32_t) * g->arcs, hipMemcpyDeviceToDevice, s));
   }
   LPA_HIP(hipStreamSynchronize(s));
+  // the kept edge list serves the outlier stage (single-GPU handles) and lpa_quality,
+  // which a distributed job runs on rank 0: the other ranks release it (at C5 over 8
+  // ranks, 11 GB per rank)
+  if (P > 1 && r != 0) {
+    dev_free(g, g->e_src);
+    dev_free(g, g->e_dst);
+    g->device_bytes -= 2 * (int64_t)sizeof(int32_t) * (m > 0 ? m : 1);
+    g->e_src = g->e_dst = nullptr;
+  }
   return LPA_OK;
 }
 

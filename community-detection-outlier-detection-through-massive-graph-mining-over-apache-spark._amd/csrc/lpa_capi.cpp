@@ -501,6 +501,10 @@ int lpa_quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, l
     set_error("null handle, labels or output");
     return LPA_EINVAL;
   }
+  if (g->m > 0 && !g->e_src) {
+    set_error("lpa_quality of a distributed job runs on rank 0 (the rank that keeps the edge list)");
+    return LPA_EINVAL;
+  }
   LPA_HIP(hipSetDevice(g->device));
   return quality(g, labels, labels_on_device, out);
 }

@@ -80,10 +80,23 @@ int loopback_attach(lpa_graph* g, Loopback* lb) {
     set_error("loopback rank %d is already attached", g->rank);
     return LPA_EINVAL;
   }
-  for (auto& e : g->loop_ev) LPA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (lb->destroy_pending) {
     set_error("loopback group is being destroyed");
     return LPA_EINVAL;
+  }
+  // events last: an error return above leaves nothing to release (g->loop stays null,
+  // so loopback_detach would not destroy them)
+  for (auto& e : g->loop_ev) {
+    const hipError_t er = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (er != hipSuccess) {
+      for (auto& f : g->loop_ev)
+        if (f) {
+          (void)hipEventDestroy(f);
+          f = nullptr;
+        }
+      set_error("hipEventCreateWithFlags failed: %s", hipGetErrorString(er));
+      return LPA_EHIP;
+    }
   }
   lb->rank_g[g->rank] = g;
   ++lb->attached;

@@ -1610,11 +1610,9 @@ static_assert(kSegArcs == 512, "unit of a position: (p - rp[row]) >> 9");
 // lanes (lane -> piece by a binary search over the inclusive piece prefix), so a
 // wave whose lanes hold runs of 17..256 positions writes them in parallel instead of
 // run after run with the whole wave.  Every lane of the wave must call it.
-// ab != nullptr: the arc giant bits are kept in step (bit p = (lab == G); no-return
-// 64-bit atomics, the positions of other columns share the words)
 __device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, const uint32_t* __restrict__ cpos,
                                              int32_t* __restrict__ al, bool all, const FrontierMarks& fm,
-                                             int lane, unsigned long long* __restrict__ ab, int32_t G) {
+                                             int lane) {
   const int k = (n + 15) >> 4;
   int incl = k;
 #pragma unroll
@@ -1649,11 +1647,6 @@ __device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, cons
           if (q + u < cnt) {
             al[p[u]] = lv;
             if (!all) fm.mark(p[u]);
-            if (ab) {
-              const unsigned long long bit = 1ull << (p[u] & 63);
-              if (lv == G) atomicOr(&ab[p[u] >> 6], bit);
-              else atomicAnd(&ab[p[u] >> 6], ~bit);
-            }
           }
       }
     }
@@ -1705,20 +1698,16 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
                                                     int frontier, int64_t fr_thr,
                                                     int32_t* __restrict__ Lold,
                                                     const int32_t* __restrict__ col_fold, int64_t arcs,
-                                                    int32_t* __restrict__ gword,
-                                                    unsigned long long* __restrict__ abits) {
+                                                    int32_t* __restrict__ gword) {
   // the next superstep's counters (the other parity; no memset launch)
   if (blockIdx.x == 0 && threadIdx.x < 3) counters_next[threadIdx.x] = 0ull;
   const bool rebuild = rebuild_wanted(counters, thr);
-  // the arc giant bits: kept in step by the scatter while valid (read before any block
-  // can clear the flag: the clear below only follows a plain folded rebuild)
-  // al changes here (scatter, or the plain folded rebuild): the arc giant bits go stale
-  // (keeping them in step cost 0.25 ms of 64-bit atomics in superstep 3, more than a
-  // settled superstep 4 would save)
+  // al changes here (scatter, or the plain folded rebuild), so the arc giant bits go
+  // stale: gword[2] = 0.  (Keeping them in step with 64-bit atomics in the scatter cost
+  // 0.25 ms in superstep 3, more than a settled superstep 4 saves; superstep 4
+  // re-derives them with k_abits_pass instead.)  A wanted, non-folded rebuild follows
+  // this kernel and sets gword[2] itself.
   if (blockIdx.x == 0 && threadIdx.x == 0 && (!rebuild || col_fold)) gword[2] = 0;
-  unsigned long long* ab = nullptr;
-  const int32_t G = 0;
-  (void)abits;
   // The next superstep tallies every row after a rebuild, with the frontier off, or
   // when more than fr_thr arcs changed: then nearly every row has a changed neighbour
   // anyway (R-MAT superstep 3 -> 4: 1.5 % of arcs dirty, 88 % of the arcs in dirty
@@ -1747,7 +1736,7 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
         lab = Ln[u];
         Lold[u] = lab;  // frontier sync (after the join)
       }
-      scatter_runs(b, n, lab, cpos, al, all, fm, lane, ab, G);
+      scatter_runs(b, n, lab, cpos, al, all, fm, lane);
     }
   }
   uint4* __restrict__ flw = const_cast<uint4*>(chflag16);
@@ -1786,7 +1775,7 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
         // (after the join; every changed vertex with local arcs has a chunk 0)
         if (kk == 0) Lold[u] = lab;
       }
-      scatter_runs(b, n, lab, cpos, al, all, fm, lane, ab, G);
+      scatter_runs(b, n, lab, cpos, al, all, fm, lane);
     }
   }
 }
@@ -2727,7 +2716,7 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
                      g->counters + 4 * (par ^ 1), g->cptr,
                      g->cpos, Ln, g->al, thr, fm, g->fr_all + (par ^ 1), g->frontier,
                      (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc),
-                     fold_rebuild ? g->col : (const int32_t*)nullptr, g->arcs, g->gword, g->abits);
+                     fold_rebuild ? g->col : (const int32_t*)nullptr, g->arcs, g->gword);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   if (ev_scatter) LPA_HIP(hipEventRecord(ev_scatter, s));  // profiling: scatter | rebuild

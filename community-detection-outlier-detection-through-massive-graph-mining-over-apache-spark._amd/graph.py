@@ -217,9 +217,19 @@ class Graph:
         dense-id labels) on this graph's symmetrised multigraph (lpa_quality)."""
         q = _lib.LpaQualitySummary()
         if _is_device_tensor(labels):
+            import torch
+
+            # the library reads V int32 values on its own stream (as _edge_ptrs guards the
+            # edge tensors): wrong dtype / device would be read silently, an unfinished
+            # producer on torch's stream too early
+            if labels.dtype != torch.int32:
+                raise ValueError(f"device labels must be int32, got {labels.dtype}")
+            if labels.device.index != self.device:
+                raise ValueError(f"device labels must be on cuda:{self.device}, got {labels.device}")
             if labels.numel() != self.num_vertices:
                 raise ValueError(f"labels must hold {self.num_vertices} entries")
-            lab, ptr, on_dev = labels.contiguous(), None, 1
+            lab, on_dev = labels.contiguous(), 1
+            torch.cuda.current_stream(lab.device).synchronize()
             ptr = lab.data_ptr()
         else:
             lab = np.ascontiguousarray(labels, dtype=np.int32)

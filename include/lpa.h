@@ -217,7 +217,9 @@ int lpa_outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, i
  *   modularity = intra_arcs / A - degree_term,  degree_term = sum_c (D_c / A)^2,
  * D_c the degree sum of community c, plus the community count (the distinct-label
  * count of Graphframes.py:85).  Exact integer sums on the device.  North-star
- * "community-count / modularity agreement" report; not a GraphFrames call. */
+ * "community-count / modularity agreement" report; not a GraphFrames call.
+ * On a distributed job (nranks > 1) only rank 0 keeps the edge list this needs; the
+ * other ranks return LPA_EINVAL. */
 typedef struct lpa_quality_summary {
   int64_t n_communities;
   int64_t intra_arcs;

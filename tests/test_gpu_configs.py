@@ -1,17 +1,21 @@
-"""BASELINE.json configs at their FULL sizes on one MI355X, bit-exact against the CPU
-oracle (SURVEY.md §8(d) workloads; reference call: Graphframes.py:81
-``labelPropagation(maxIter)``).
+"""BASELINE.json configs at their FULL sizes, bit-exact against the CPU oracle at every
+superstep (SURVEY.md §8(d) workloads; reference call: Graphframes.py:81
+``labelPropagation(maxIter)``; the partitioned forms stand in for the Spark
+``local[*]`` parallelism of Graphframes.py:12 and the shuffle behind :81).
 
   C3  R-MAT scale 24, edgefactor 16 (16.7 M V / 268 M E): supersteps 1..10 from L0,
-      every superstep, plus lpa_run(10) as a user calls it
-  C4  R-MAT scale 26, edgefactor 16 (67 M V / 1.07 B E, 2.1 B arcs) on ONE GPU (the
-      config is quoted on 2/4/8 GPUs; the partitioned path is bit-identical by
-      construction and tested separately): supersteps 1..10 from L0 (the giant
-      decision, the row settle, the frontier and the scatter paths at 2.1 B arcs)
-  C5  Chung-Lu gamma 2.1, 40 M V / 1.4 B E (2.8 B arcs, max degree ~1.25 M) on ONE
-      GPU: lpa_run(maxIter=10) final labels
+      plus lpa_run(10) as a user calls it
+  C4  R-MAT scale 26, edgefactor 16 (67 M V / 1.07 B E, 2.1 B arcs): one GPU, and as
+      configured -- vertex-partitioned over P = 2 and P = 8 ranks (an in-process
+      loopback group on the one GPU: the library's own exchange code, full allgather
+      and changed-label deltas, with D2D copies in place of ncclAllGather)
+  C5  Chung-Lu gamma 2.1, 40 M V / 1.4 B E (2.8 B arcs, max degree ~1.25 M): one GPU,
+      and as configured -- partitioned over P = 8 ranks
+  C2  SBM 1 M V / 20 M E: the outlier stage (L1 / L2)
 
-The oracle here is oracle/lpa_oracle.c (OpenMP), the checker only.
+Every superstep of every rank is compared with the oracle's history; the oracle here
+is oracle/lpa_oracle.c (OpenMP), the checker only.  Each oracle history is computed
+once per module (a fixture) and shared by the single-GPU and the partitioned tests.
 """
 import time
 
@@ -19,6 +23,8 @@ import numpy as np
 import pytest
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+MAX_ITER = 10
 
 
 @pytest.fixture(scope="module")
@@ -32,12 +38,79 @@ def _host(t):
     return t.cpu().numpy()
 
 
-def _steps(g, n):
-    out = []
-    for _ in range(n):
+def _mismatch_per_step(g, hist, n):
+    """Steps the handle n times; the number of labels that differ at each superstep."""
+    bad = []
+    for t in range(n):
         g.step(1)
-        out.append(g.labels())
-    return out
+        bad.append(int((g.labels() != hist[t]).sum()))
+    return bad
+
+
+class _Config:
+    """Host edge list + the oracle's per-superstep history of one config."""
+
+    def __init__(self, V, src, dst, oracle):
+        self.V, self.src, self.dst = V, src, dst
+        t0 = time.perf_counter()
+        _, self.hist, _ = oracle.lpa(V, src, dst, MAX_ITER, per_iter=True)
+        self.oracle_s = time.perf_counter() - t0
+
+
+@pytest.fixture(scope="module")
+def c4(gfa, oracle):
+    s, d = gfa.gen_rmat(26, 16, seed=1)
+    src, dst = _host(s), _host(d)
+    del s, d
+    return _Config(1 << 26, src, dst, oracle)
+
+
+@pytest.fixture(scope="module")
+def c5(gfa, oracle):
+    s, d = gfa.gen_chunglu(40_000_000, 1_400_000_000, 2.1, 1.25e6, seed=7)
+    src, dst = _host(s), _host(d)
+    del s, d
+    return _Config(40_000_000, src, dst, oracle)
+
+
+def _empty_cache():
+    import torch
+
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def _partitioned_every_superstep(gfa, cfg, P, what):
+    """A loopback group of P ranks on the one GPU, built from the same edge list (as
+    P processes of `bench.py --gpus P` build theirs), every rank checked against the
+    oracle at every superstep 1..10, then lpa_run(10) on every rank concurrently."""
+    import torch
+
+    lb = gfa.Loopback(P)
+    ranks = []
+    try:
+        dev_s = torch.from_numpy(cfg.src).cuda()
+        dev_d = torch.from_numpy(cfg.dst).cuda()
+        for r in range(P):
+            ranks.append(gfa.Graph(dev_s, dev_d, cfg.V, rank=r, loopback=lb))
+        del dev_s, dev_d
+        _empty_cache()
+        infos = [g.info() for g in ranks]
+        assert sum(i["arcs"] for i in infos) == 2 * cfg.src.size
+        bad = gfa.run_ranks(ranks, lambda r, g: _mismatch_per_step(g, cfg.hist, MAX_ITER))
+        for r in range(P):
+            for t in range(MAX_ITER):
+                assert bad[r][t] == 0, f"{what} P={P} rank {r} superstep {t + 1}: {bad[r][t]} labels differ"
+        infos = [g.info() for g in ranks]
+        # label-dense supersteps exchange full slices, converging ones changed-label deltas
+        assert all(i["exchanges_full"] >= 2 and i["exchanges_delta"] >= 2 for i in infos), infos
+        runs = gfa.run_ranks(ranks, lambda r, g: int((g.run(MAX_ITER) != cfg.hist[MAX_ITER - 1]).sum()))
+        assert runs == [0] * P, f"{what} P={P} lpa_run(10) mismatches per rank: {runs}"
+    finally:
+        for g in ranks:
+            g.close()
+        lb.close()
+        _empty_cache()
 
 
 def test_c3_rmat24_every_superstep(gfa, oracle):
@@ -50,52 +123,61 @@ def test_c3_rmat24_every_superstep(gfa, oracle):
         sn, dn = _host(s), _host(d)
         del s, d
         torch.cuda.empty_cache()
-        got = _steps(g, 10)
-        run10 = g.run(10)
+        got = []
+        for _ in range(MAX_ITER):
+            g.step(1)
+            got.append(g.labels())
+        run10 = g.run(MAX_ITER)
     t0 = time.perf_counter()
-    _, hist, _ = oracle.lpa(V, sn, dn, 10, per_iter=True)
+    _, hist, _ = oracle.lpa(V, sn, dn, MAX_ITER, per_iter=True)
     t_or = time.perf_counter() - t0
-    for t in range(10):
+    for t in range(MAX_ITER):
         bad = int((got[t] != hist[t]).sum())
         assert bad == 0, f"C3 superstep {t + 1}: {bad} labels differ (oracle {t_or:.1f}s)"
-    assert np.array_equal(run10, hist[9]), "C3 lpa_run(10) differs from superstep-by-superstep"
+    assert np.array_equal(run10, hist[MAX_ITER - 1]), "C3 lpa_run(10) differs from superstep-by-superstep"
 
 
-def test_c4_rmat26_every_superstep(gfa, oracle):
+def test_c4_rmat26_every_superstep(gfa, c4):
     import torch
 
-    scale = 26
-    V = 1 << scale
-    s, d = gfa.gen_rmat(scale, 16, seed=1)
-    with gfa.Graph(s, d, V) as g:
-        assert g.info()["arcs"] == 2 * (16 << scale)   # > 2^31: int64 row offsets
-        sn, dn = _host(s), _host(d)
-        del s, d
-        torch.cuda.empty_cache()
-        got = _steps(g, 10)
-    _, hist, _ = oracle.lpa(V, sn, dn, 10, per_iter=True)
-    del sn, dn
-    for t in range(10):
-        bad = int((got[t] != hist[t]).sum())
-        assert bad == 0, f"C4 superstep {t + 1}: {bad} labels differ"
+    dev_s = torch.from_numpy(c4.src).cuda()
+    dev_d = torch.from_numpy(c4.dst).cuda()
+    with gfa.Graph(dev_s, dev_d, c4.V) as g:
+        assert g.info()["arcs"] == 2 * (16 << 26)   # > 2^31: int64 row offsets
+        del dev_s, dev_d
+        _empty_cache()
+        bad = _mismatch_per_step(g, c4.hist, MAX_ITER)
+    _empty_cache()
+    assert bad == [0] * MAX_ITER, f"C4 one GPU: labels differing per superstep {bad}"
 
 
-def test_c5_chunglu_full_maxiter10(gfa, oracle):
+@pytest.mark.parametrize("P", [2, 8])
+def test_c4_rmat26_partitioned_every_superstep(gfa, c4, P):
+    """BASELINE C4 as configured: R-MAT-26 vertex-partitioned over P ranks."""
+    _partitioned_every_superstep(gfa, c4, P, "C4")
+
+
+def test_c5_chunglu_every_superstep(gfa, c5):
+    """C5 on one GPU, every superstep (the giant decision, the hub bucket path and the
+    settles of supersteps 2-4 on 1 M-arc hub rows)."""
     import torch
 
-    V, m = 40_000_000, 1_400_000_000
-    s, d = gfa.gen_chunglu(V, m, 2.1, 1.25e6, seed=7)
-    with gfa.Graph(s, d, V) as g:
-        info = g.info()
-        assert info["max_degree"] > 1_000_000   # the hub-bin spill path is exercised
-        sn, dn = _host(s), _host(d)
-        del s, d
-        torch.cuda.empty_cache()
-        lab = g.run(10)
-    ref = oracle.lpa(V, sn, dn, 10)
-    del sn, dn
-    bad = int((lab != ref).sum())
-    assert bad == 0, f"C5 maxIter=10: {bad} labels differ"
+    dev_s = torch.from_numpy(c5.src).cuda()
+    dev_d = torch.from_numpy(c5.dst).cuda()
+    with gfa.Graph(dev_s, dev_d, c5.V) as g:
+        assert g.info()["max_degree"] > 1_000_000   # the hub-bin spill path is exercised
+        del dev_s, dev_d
+        _empty_cache()
+        bad = _mismatch_per_step(g, c5.hist, MAX_ITER)
+        run10 = int((g.run(MAX_ITER) != c5.hist[MAX_ITER - 1]).sum())
+    _empty_cache()
+    assert bad == [0] * MAX_ITER, f"C5 one GPU: labels differing per superstep {bad}"
+    assert run10 == 0, f"C5 lpa_run(10): {run10} labels differ"
+
+
+def test_c5_chunglu_partitioned_p8_every_superstep(gfa, c5):
+    """BASELINE C5 as configured: the heavy-hub graph over 8 ranks."""
+    _partitioned_every_superstep(gfa, c5, 8, "C5")
 
 
 def test_c2_outlier_l1_l2_vs_oracle(gfa, oracle):

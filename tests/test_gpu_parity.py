@@ -571,3 +571,12 @@ def test_quality_matches_numpy(gfa, golden, graph):
             assert abs(q["modularity"] - Q) < 1e-9
         with pytest.raises(ValueError, match="outside"):
             g.quality(np.full(V, V, dtype=np.int32))
+        # device tensors: int32 on this device equals the host result; an
+        # int64 tensor (torch.arange's default) is refused, not read as int32 pairs
+        import torch
+
+        lab = g.run(5)
+        dl = torch.from_numpy(lab).cuda()
+        assert g.quality(dl) == g.quality(lab)
+        with pytest.raises(ValueError, match="int32"):
+            g.quality(torch.arange(V, device="cuda"))
