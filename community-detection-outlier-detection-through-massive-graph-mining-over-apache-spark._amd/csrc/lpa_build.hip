@@ -201,6 +201,20 @@ __global__ void k_keys_to_col(const u64* __restrict__ keys, int64_t n, int32_t* 
   }
 }
 
+// row-start bits of the arc positions (bit i of word w: position 64 w + i starts a row):
+// one ballot per 64 positions; words past the arcs stay zero
+__global__ void k_row_starts(const int32_t* __restrict__ crow, int64_t arcs, int64_t nwords,
+                             u64* __restrict__ bits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nwords; w += nw) {
+    const int64_t i = w * 64 + lane;
+    const bool st = i < arcs && (i == 0 || crow[i] != crow[i - 1]);
+    const u64 m = __ballot(st);
+    if (lane == 0) bits[w] = m;
+  }
+}
+
 // CSC keys: (column << 32 | position), generated in position order so a stable
 // sort on the column bits alone leaves positions ascending within a column
 // (colcnt == nullptr: keys only -- at P = 1 the column counts are the degrees;
@@ -625,6 +639,14 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   if (g->cols_sorted) {
     LPA_TRY(dev_alloc(g, (void**)&g->first_best, sizeof(u64) * S));
     LPA_HIP(hipMemsetAsync(g->first_best, 0, sizeof(u64) * S, s));
+    if (arcs > 0) {
+      // whole 512-arc tiles of words plus the next tile's first word (k_first_runs)
+      const int64_t nwords = (arcs + 511) / 512 * 8 + 8;
+      LPA_TRY(dev_alloc(g, (void**)&g->rstart, sizeof(u64) * nwords));
+      hipLaunchKernelGGL(k_row_starts, dim3(grid_for(nwords * 64)), dim3(256), 0, s, g->crow, arcs, nwords,
+                         g->rstart);
+      LPA_HIP(hipGetLastError());
+    }
   }
   if (g->crow == nullptr) LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t)));
 

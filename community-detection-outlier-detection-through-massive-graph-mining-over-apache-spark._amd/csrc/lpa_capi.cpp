@@ -85,7 +85,7 @@ void destroy(lpa_graph* g) {
                   g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
-                  g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best,
+                  g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best, g->rstart,
                   g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword, g->al0, g->abits,
                   g->glist};
   for (void* p : bufs) dev_free(g, p);

@@ -167,6 +167,8 @@ struct lpa_graph {
   int first_runs = 1;             // LPA_FIRST_RUNS=0: superstep 1 by the hash tallies, not column runs
   bool cols_sorted = true;        // columns ascending inside each row (false: row-only sorted build)
   lpa::u64* first_best = nullptr; // [slice] superstep-1 best run word of rows spanning run tiles
+  lpa::u64* rstart = nullptr;     // [arcs / 64 + pad] bit i: arc position i starts a row (crow[i] !=
+                                  //   crow[i - 1]); k_first_runs reads it instead of crow (1 bit/arc)
   int64_t unit_lane_begin = 0;    // hub_uoff[hub_lane_begin]
   int64_t unit_block2_begin = 0;  // hub_uoff[hub_block2_begin]
   bool force_all_next = false;    // the next superstep tallies every row (after block mode)

@@ -2178,14 +2178,36 @@ __device__ __forceinline__ void seg_max_step(u64& w, int32_t r) {
   if (ro == r && wo > w) w = wo;
 }
 
+// Row ids come from the row-start bitmap (1 bit per arc; crow is read once per tile):
+// the row of position i is crow[t0] + the number of row starts in (t0, i].  Rows are
+// degree-sorted, so every row between two rows with arcs has arcs too.
 __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ al,
-                                                    const int32_t* __restrict__ crow, int64_t arcs,
+                                                    const int32_t* __restrict__ crow,
+                                                    const u64* __restrict__ rstart, int64_t arcs,
                                                     int32_t* __restrict__ Ln, u64* __restrict__ best) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRunTile; t0 < arcs;
-       t0 += nw * kRunTile) {
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  for (int64_t t0 = ((int64_t)blockIdx.x * 4 + wv) * kRunTile; t0 < arcs; t0 += nw * kRunTile) {
     const int64_t t1 = t0 + kRunTile < arcs ? t0 + kRunTile : arcs;
+    constexpr int kC = kRunTile / 64;
+    // the tile's labels first (every load in flight before the first chunk's scan)
+    u32 aa[kC];
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+      const int64_t i = t0 + c * 64 + lane;
+      aa[c] = i < t1 ? (u32)__builtin_nontemporal_load(al + i) : kNone;
+    }
+    // row-start words of the tile (wave-uniform) and the first word of the next tile
+    const int64_t wb = t0 >> 6;
+    u64 W[kC];
+#pragma unroll
+    for (int c = 0; c < kC; ++c) W[c] = rstart[wb + c];
+    // a row ends at the tile's last position when the next tile starts one (a partial
+    // last tile ends its last row at position arcs - 1, tested per lane below)
+    const u64 wnext = t1 < arcs ? rstart[wb + kC] : 1ull;
+    const int32_t r_t0 = crow[t0];
     // carry: row, label, run length and row maximum at the position before the chunk
     // (the row maximum starts at 0 in a tile: the previous tile folded its part)
     int32_t cr = -1;
@@ -2194,38 +2216,28 @@ __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ 
     if (t0 > 0) {
       cr = crow[t0 - 1];
       ca = (u32)al[t0 - 1];
-      if (crow[t0] == cr && (u32)al[t0] == ca) {
+      if (r_t0 == cr && (u32)al[t0] == ca) {
         // a run continues into the tile (rare): its length up to t0 - 1
         int64_t k = 1;
         while (t0 - 1 - k >= 0 && crow[t0 - 1 - k] == cr && (u32)al[t0 - 1 - k] == ca) ++k;
         ck = (u32)k;
       }
     }
-    // the tile's labels and rows, every load in flight before the first chunk's scan;
-    // rows are contiguous, so a row started inside the tile iff it differs from the
-    // row before the tile, and ends at i iff position i + 1 holds another row
+    // rows are contiguous, so a row started inside the tile iff it differs from the row
+    // before the tile
     const int32_t r_before = cr;
-    const int32_t r_after = t1 < arcs ? crow[t1] : -3;
-    constexpr int kC = kRunTile / 64;
-    int32_t rr[kC];
-    u32 aa[kC];
-#pragma unroll
-    for (int c = 0; c < kC; ++c) {
-      const int64_t i = t0 + c * 64 + lane;
-      rr[c] = i < t1 ? __builtin_nontemporal_load(crow + i) : -2;
-      aa[c] = i < t1 ? (u32)__builtin_nontemporal_load(al + i) : kNone;
-    }
+    int32_t rbase = r_t0;   // row of the chunk's first position, minus its own start bit
 #pragma unroll
     for (int c = 0; c < kC; ++c) {
       const int64_t i = t0 + c * 64 + lane;
       const bool live = i < t1;  // every lane runs every shuffle
-      const int32_t r = rr[c];
+      // starts after t0 only (position t0 is row r_t0 whatever its bit)
+      const u64 wc = c == 0 ? (W[0] & ~1ull) : W[c];
+      const int32_t r = rbase + (int32_t)__popcll(wc & upto);
       const u32 a = aa[c];
-      // lane - 1's row and label (DPP wave_shr:1; lane 0 takes the carry)
-      const int32_t rprev = __builtin_amdgcn_update_dpp(cr, r, 0x138, 0xF, 0xF, false);
+      // lane - 1's label (DPP wave_shr:1; lane 0 takes the carry)
       const u32 aprev = (u32)__builtin_amdgcn_update_dpp((int)ca, (int)a, 0x138, 0xF, 0xF, false);
-      const u64 starts = __ballot(r != rprev || a != aprev);
-      const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+      const u64 starts = W[c] | __ballot(a != aprev);
       const u64 m = starts & upto;
       const u32 k = m ? (u32)(lane - (63 - __clzll((long long)m)) + 1) : (u32)lane + 1u + ck;
       u64 w = live ? (((u64)k << 32) | (u64)(~a)) : 0ull;
@@ -2236,15 +2248,16 @@ __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ 
       seg_max_step<0x118, 0xF>(w, r);  // row_shr:8
       seg_max_step<0x142, 0xA>(w, r);  // row_bcast:15 into rows 1, 3
       seg_max_step<0x143, 0xC>(w, r);  // row_bcast:31 into rows 2, 3
-      // lane + 1's row (DPP wave_shl:1; lane 63: the next chunk's first row)
-      const int32_t r63 = c + 1 < kC ? __builtin_amdgcn_readlane(rr[c + 1 < kC ? c + 1 : c], 0) : r_after;
-      const int32_t rnext = __builtin_amdgcn_update_dpp(r63, r, 0x130, 0xF, 0xF, false);
-      if (live && rnext != r) {  // the row ends at i
+      // the row ends at i iff position i + 1 starts a row (the next chunk's / tile's bit 0)
+      const u64 nb = c + 1 < kC ? (W[c + 1 < kC ? c + 1 : c] & 1ull) : (wnext & 1ull);
+      const u64 ends = (W[c] >> 1) | (nb << 63);
+      if (live && (((ends >> lane) & 1ull) || i + 1 == arcs)) {  // the row ends at i
         if (r != r_before) Ln[r] = (int32_t)(~(u32)w);
         else atomicMax(&best[r], w);
       } else if (live && i + 1 == t1) {
         atomicMax(&best[r], w);  // continues in the next tile
       }
+      rbase += (int32_t)__popcll(wc);
       cr = __builtin_amdgcn_readlane(r, 63);
       ca = (u32)__builtin_amdgcn_readlane((int)a, 63);
       ck = (u32)__builtin_amdgcn_readlane((int)k, 63);
@@ -2304,13 +2317,15 @@ int launch_frontier_lists(lpa_graph* g, hipStream_t st = nullptr, const int32_t*
   return LPA_OK;
 }
 
-// label-dense superstep on one GPU: its diff only counts the changed slots, and its
-// refresh rebuilds al[] unless few changed (k_dense_decide)
-bool dense_refresh(const lpa_graph* g) { return g->since_reset < kDenseSupersteps && !exchanges(g); }
+// label-dense superstep: its diff only counts the changed slots, and its refresh
+// rebuilds al[] unless few changed (k_dense_decide).  P > 1: the count runs after the
+// exchange over the whole replicated vector (launch_refresh), P = 1 per stream inside
+// the tally
+bool dense_refresh(const lpa_graph* g) { return g->since_reset < kDenseSupersteps; }
 
 // superstep 1 from L0 by column runs (k_first_runs); the caller's refresh diffs
 bool first_runs_now(const lpa_graph* g) {
-  return g->first_runs && g->cols_sorted && g->first_best && g->since_reset == 0 && g->arcs > 0 &&
+  return g->first_runs && g->cols_sorted && g->first_best && g->rstart && g->since_reset == 0 && g->arcs > 0 &&
          !g->serial;
 }
 
@@ -2320,7 +2335,7 @@ int launch_first(lpa_graph* g, int32_t* Lown) {
   const int64_t ntiles = (g->arcs + kRunTile - 1) / kRunTile;
   // after a lazy reset the L0 arc labels are in al0 (al is rebuilt by the refresh)
   hipLaunchKernelGGL(k_first_runs, dim3(cap_grid((ntiles + 3) / 4, 8192)), dim3(256), 0, s,
-                     g->al_pending ? g->al0 : g->al, g->crow, g->arcs, Lown, g->first_best);
+                     g->al_pending ? g->al0 : g->al, g->crow, g->rstart, g->arcs, Lown, g->first_best);
   LPA_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_first_final, dim3(cap_grid((g->slice + 255) / 256, 4096)), dim3(256), 0, s, g->rp,
                      g->slice, g->first_best, Lown, g->hub_lcnt);
@@ -2349,7 +2364,9 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // abits pass, on aux0 while the main stream re-tallies every hub unit and row (range
   // mode: their staged words are current again for the frontier supersteps); the bins
   // below the hubs then walk their unsettled rows' lists (fr_bins = gword[4])
-  const bool settle4 = g->since_reset == 3 && !exchanges(g) && g->abits != nullptr;
+  // (P > 1: each rank settles its owned rows from its own arc giant bits; G is the same
+  // on every rank, k_giant_pick reads the replicated vector)
+  const bool settle4 = g->since_reset == 3 && g->abits != nullptr;
   const int32_t* fr_bins = settle4 ? g->gword + 4 : fr_all;
   if (settle4) {
     if (!g->serial) {
@@ -2687,7 +2704,10 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   // one rank: its isolated slots (and the padding) never change; P > 1: the whole
   // replicated vector (other ranks' slots change through the exchange)
   const int64_t nd = !exchanges(g) ? g->bin_begin[BIN_ISO] : g->vpad;
-  if (dense_refresh(g)) {
+  // diff_done means, at P = 1, that the tally's per-stream diffs ran (count-only ones in
+  // a label-dense superstep); at P > 1, that the delta exchange queued every change
+  // already (nothing left to count or diff)
+  if (dense_refresh(g) && !(diff_done && exchanges(g))) {
     // counted changed slots (in the tally, or here) -> rebuild, or the full diff
     if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, false, par, 0, 0, 1));
     hipLaunchKernelGGL(k_dense_decide, dim3(1), dim3(64), 0, s, ctr, nd);
