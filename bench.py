@@ -545,22 +545,30 @@ def main():
     if world == 1 and not args.no_outlier:
         progress("outlier stage")
         lab = g.run(MAX_ITER)
-        for mode, key in (("L1", "outlier_l1_ms"), ("L2", "outlier_l2_ms")):
-            ts = []
-            for _ in range(3):
-                t0 = time.perf_counter()
-                res = g.outlier(lab, mode, sub_iter=5)
-                ts.append((time.perf_counter() - t0) * 1e3)
-                progress(f"outlier {mode}: {ts[-1]:.1f} ms")
-            out_json[key] = round(statistics.median(ts), 2)
-            if mode == "L1":   # the first call also builds the handle's distinct edge set
-                out_json["outlier_l1_first_ms"] = round(ts[0], 2)
+        dlab = torch.from_numpy(lab).to(f"cuda:{device}")
+        for mode, key in (("L1", "outlier_l1"), ("L2", "outlier_l2")):
+            # device form (labels and every output in HBM, as `value`'s inputs are), then
+            # the host-array form of the drop-in API (host labels in, numpy arrays out)
+            for form, labels_in in (("", dlab), ("_host", lab)):
+                ts = []
+                for _ in range(3):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    res = g.outlier(labels_in, mode, sub_iter=5)
+                    torch.cuda.synchronize()
+                    ts.append((time.perf_counter() - t0) * 1e3)
+                    progress(f"outlier {mode}{form}: {ts[-1]:.1f} ms")
+                out_json[f"{key}{form}_ms"] = round(statistics.median(ts), 2)
+                if form == "":
+                    out_json[f"{key}_first_ms"] = round(ts[0], 2)
             if mode == "L2":
                 out_json["outlier_l2_flagged"] = int(res["flags"].sum())
-        out_json["outlier_note"] = ("lpa_outlier on the maxIter=10 labels (host labels in, host arrays out), "
-                                    "median of 3 calls; L2 = second LPA of 5 supersteps on the intra-community "
-                                    "distinct edges; the handle's distinct directed edge set (topology) is built "
-                                    "by its first outlier call and kept (outlier_l1_first_ms includes it)")
+        out_json["outlier_note"] = ("lpa_outlier on the maxIter=10 labels, median of 3 calls; outlier_l*_ms: device "
+                                    "labels in, device arrays out (lpa_outlier_device); outlier_l*_host_ms: host "
+                                    "labels in, host numpy arrays out (lpa_outlier); L2 = second LPA of 5 supersteps "
+                                    "on the intra-community distinct edges.  The handle's distinct directed edge "
+                                    "set (and, for L2, its (d, s) order) is topology, built by the first call of "
+                                    "each kind and kept (outlier_l*_first_ms include it)")
     if keep_host and rank == 0:
         progress("CPU baseline")
         out_json["cpu_baseline"] = cpu_baseline(src_np, dst_np, V, g)

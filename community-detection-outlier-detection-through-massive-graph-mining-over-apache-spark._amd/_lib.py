@@ -61,6 +61,7 @@ class LpaGraphInfo(ctypes.Structure):
         ("hub_vertices", ctypes.c_int64), ("segments", ctypes.c_int64),
         ("device_bytes", ctypes.c_int64),
         ("exchanges_full", ctypes.c_int64), ("exchanges_delta", ctypes.c_int64),
+        ("id_order", ctypes.c_int64),
     ]
 
     def to_dict(self):
@@ -108,6 +109,8 @@ SIGNATURES = {
     "lpa_run": (ctypes.c_int, [_vp, ctypes.c_int32, _vp, ctypes.c_int32, ctypes.POINTER(LpaStats)]),
     "lpa_outlier": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                    _i64p, _i64p, _i32p, _u8p, ctypes.POINTER(LpaOutlierSummary)]),
+    "lpa_outlier_device": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp,
+                                          ctypes.POINTER(LpaOutlierSummary)]),
     "lpa_degrees": (ctypes.c_int, [_vp, _i32p]),
     "lpa_quality": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, _vp]),
     "lpa_loopback_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_vp)]),

@@ -132,6 +132,37 @@ __global__ void k_locality_keys(u64* __restrict__ keys, int64_t V, const int32_t
   }
 }
 
+// Input-id locality: the fraction of edges whose endpoints' ids differ by less than a
+// window (one block-reduced count).  Generators and crawls that number communities
+// contiguously (planted-partition SBM: block = id / block size) put most edges inside
+// the window; scrambled or hashed ids (R-MAT, SHA-1 domain ids) almost none.
+__global__ __launch_bounds__(256) void k_id_local(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                                  int64_t m, int32_t w, unsigned long long* __restrict__ cnt) {
+  __shared__ unsigned long long ws[4];
+  unsigned long long c = 0;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t a = src[e], b = dst[e];
+    c += (a > b ? a - b : b - a) < w ? 1ull : 0ull;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0 && (ws[0] | ws[1] | ws[2] | ws[3])) atomicAdd(cnt, ws[0] + ws[1] + ws[2] + ws[3]);
+}
+
+// id order inside the bins below the hubs (hubs by degree desc): keys (bin, hub degree
+// rank | 0) in the high word, generated in id order, so a stable sort on the high word
+// leaves ids ascending inside each bin -- the input's own locality (a community's
+// vertices in contiguous slots, so its rows' label gathers share lines)
+__global__ void k_id_order_keys(u64* __restrict__ keys, int64_t V, const int32_t* __restrict__ deg, int32_t maxdeg) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t d = deg[v];
+    const u32 bin = degree_bin(d);
+    const u32 a = bin == 0 ? (u32)(maxdeg - d) : 0u;
+    keys[v] = ((u64)((bin << 28) | a) << 32) | (u64)v;
+  }
+}
+
 __global__ void k_vertex_order(const u64* __restrict__ keys, int64_t V, int32_t P, int64_t S,
                                int32_t* __restrict__ new_of, int32_t* __restrict__ old_of) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < V;
@@ -317,6 +348,72 @@ __global__ void k_init_labels(const int32_t* __restrict__ old_of, int64_t n, int
   }
 }
 
+
+// ---- the outlier stage's L2 sub-graph (build_graph_l2) ----
+// intra-community marks over the parent's distinct edges in (s, d) order ...
+__global__ void k_l2_mark_out(const u64* __restrict__ ek, int64_t md, const int32_t* __restrict__ L,
+                              int32_t* __restrict__ mark) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < md; i += (int64_t)gridDim.x * blockDim.x) {
+    const u64 k = ek[i];
+    mark[i] = L[(int32_t)(k >> 32)] == L[(int32_t)(u32)k] ? 1 : 0;
+  }
+}
+// ... and in (d, s) order (de_t: d << 32 | index, de_ts: s)
+__global__ void k_l2_mark_in(const u64* __restrict__ et, const uint32_t* __restrict__ ets, int64_t md,
+                             const int32_t* __restrict__ L, int32_t* __restrict__ mark) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < md; j += (int64_t)gridDim.x * blockDim.x)
+    mark[j] = L[(int32_t)(et[j] >> 32)] == L[(int32_t)ets[j]] ? 1 : 0;
+}
+// degrees from segment lengths: v's intra out-edges are the marks of its run in the
+// (s, d) order, its in-edges those of its run in the (d, s) order
+__global__ void k_l2_degree(const int64_t* __restrict__ out_off, const int64_t* __restrict__ in_off,
+                            const int64_t* __restrict__ pos_out, const int64_t* __restrict__ pos_in, int64_t V,
+                            int32_t* __restrict__ deg, int32_t* __restrict__ dout) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t o = (int32_t)(pos_out[out_off[v + 1]] - pos_out[out_off[v]]);
+    const int32_t n = (int32_t)(pos_in[in_off[v + 1]] - pos_in[in_off[v]]);
+    dout[v] = o;
+    deg[v] = o + n;
+  }
+}
+// arcs of row s from its intra out-edges, in place: row s's first dout[s] positions
+__global__ void k_l2_emit_out(const u64* __restrict__ ek, int64_t md, const int32_t* __restrict__ mark,
+                              const int64_t* __restrict__ pos_out, const int64_t* __restrict__ out_off,
+                              const int32_t* __restrict__ new_of, const int64_t* __restrict__ rp,
+                              int32_t* __restrict__ col, int32_t* __restrict__ crow) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < md; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!mark[i]) continue;
+    const u64 k = ek[i];
+    const int32_t sv = (int32_t)(k >> 32), rs = new_of[sv];
+    const int64_t p = rp[rs] + (pos_out[i] - pos_out[out_off[sv]]);
+    col[p] = new_of[(int32_t)(u32)k];
+    crow[p] = rs;
+  }
+}
+// arcs of row d from its intra in-edges, after its out-edges; each edge's two arcs are
+// each other's CSC entry: column u's positions are the twins of row u's arcs, so the
+// CSC shares the row offsets (cptr = rp) and cpos[p] = q, cpos[q] = p
+__global__ void k_l2_emit_in(const u64* __restrict__ et, const uint32_t* __restrict__ ets, int64_t md,
+                             const int32_t* __restrict__ mark, const int64_t* __restrict__ pos_in,
+                             const int64_t* __restrict__ in_off, const int64_t* __restrict__ pos_out,
+                             const int64_t* __restrict__ out_off, const int32_t* __restrict__ dout,
+                             const int32_t* __restrict__ new_of, const int64_t* __restrict__ rp,
+                             int32_t* __restrict__ col, int32_t* __restrict__ crow, uint32_t* __restrict__ cpos) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < md; j += (int64_t)gridDim.x * blockDim.x) {
+    if (!mark[j]) continue;
+    const u64 k = et[j];
+    const int32_t dv = (int32_t)(k >> 32), sv = (int32_t)ets[j];
+    const int64_t i = (int64_t)(u32)k;
+    const int32_t rd = new_of[dv], rs = new_of[sv];
+    const int64_t q = rp[rd] + dout[dv] + (pos_in[j] - pos_in[in_off[dv]]);
+    const int64_t p = rp[rs] + (pos_out[i] - pos_out[out_off[sv]]);
+    col[q] = rs;
+    crow[q] = rd;
+    cpos[p] = (uint32_t)q;
+    cpos[q] = (uint32_t)p;
+  }
+}
+
 inline unsigned grid_for(int64_t n, int threads = 256) {
   int64_t b = (n + threads - 1) / threads;
   if (b < 1) b = 1;
@@ -351,57 +448,13 @@ int init_labels(lpa_graph* g) {
   return rebuild_arc_labels(g);
 }
 
-int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
-                uint32_t flags) {
+// Degree-ranked vertex order (degree desc, id asc; optionally the locality order inside
+// the bins below the hubs, which reads the kept edge list): new_of / old_of.  Needs
+// g->deg and g->max_degree; P ranks take the ranks round-robin (slot (k % P) S + k / P).
+int vertex_order(lpa_graph* g, int32_t V, int64_t m, bool locality) {
   hipStream_t s = g->stream;
-  const int32_t P = g->nranks, r = g->rank;
-  g->V = V;
-  g->m = m;
-  g->slice = ((int64_t)V + P - 1) / P;
-  g->slice = (g->slice + 63) / 64 * 64;  // vector-aligned slices (k_diff reads int4)
-  if (g->slice == 0) g->slice = 64;
-  g->vpad = g->slice * P;
-  g->own_begin = (int64_t)r * g->slice;
+  const int32_t P = g->nranks;
   const int64_t S = g->slice;
-
-  // ---- keep the edge list on the device (outlier stage needs it) ----
-  LPA_TRY(dev_alloc(g, (void**)&g->e_src, sizeof(int32_t) * (m > 0 ? m : 1)));
-  LPA_TRY(dev_alloc(g, (void**)&g->e_dst, sizeof(int32_t) * (m > 0 ? m : 1)));
-  if (m > 0) {
-    hipMemcpyKind kind = (flags & LPA_INPUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    LPA_HIP(hipMemcpyAsync(g->e_src, src, sizeof(int32_t) * m, kind, s));
-    LPA_HIP(hipMemcpyAsync(g->e_dst, dst, sizeof(int32_t) * m, kind, s));
-  }
-
-  // ---- 1. degrees ----
-  int32_t* d_err = nullptr;
-  int32_t* d_max = nullptr;
-  LPA_TRY(scratch_alloc(g, (void**)&d_err, 2 * sizeof(int32_t)));
-  d_max = d_err + 1;
-  LPA_HIP(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), s));
-  LPA_TRY(dev_alloc(g, (void**)&g->deg, sizeof(int32_t) * (V > 0 ? V : 1)));
-  LPA_HIP(hipMemsetAsync(g->deg, 0, sizeof(int32_t) * (V > 0 ? V : 1), s));
-  if (m > 0) {
-    hipLaunchKernelGGL(k_degree, dim3(cap_bh(grid_for(m))), dim3(256), 0, s, g->e_src, g->e_dst, m, V,
-                       g->deg, d_err);
-    LPA_HIP(hipGetLastError());
-  }
-  if (V > 0) {
-    hipLaunchKernelGGL(k_maxdeg, dim3(grid_for(V) < 1024u ? grid_for(V) : 1024u), dim3(256), 0, s, g->deg,
-                       (int64_t)V, d_max);
-    LPA_HIP(hipGetLastError());
-  }
-  int32_t h_err[2] = {0, 0};
-  LPA_HIP(hipMemcpyAsync(h_err, d_err, sizeof(h_err), hipMemcpyDeviceToHost, s));
-  LPA_HIP(hipStreamSynchronize(s));
-  scratch_free(g, d_err);
-  if (h_err[0]) {
-    set_error("edge endpoint outside [0, V=%d)", V);
-    return LPA_EINVAL;
-  }
-  g->max_degree = h_err[1];
-
-  // ---- 2. degree-ranked vertex order ----
   LPA_TRY(dev_alloc(g, (void**)&g->new_of, sizeof(int32_t) * (V > 0 ? V : 1)));
   LPA_TRY(dev_alloc(g, (void**)&g->old_of, sizeof(int32_t) * g->vpad));
   LPA_HIP(hipMemsetAsync(g->old_of, 0xFF, sizeof(int32_t) * g->vpad, s));
@@ -416,7 +469,30 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(vk, vk + V, V, shifts, ns, s));
-    if (g->locality > 0 && m > 0 && V < (1 << 28)) {
+    // the input ids' own locality first: more than half of the edges within a window of
+    // 16 K ids -> id order inside the bins (the neighbour-rank order below would scatter
+    // it); LPA_LOCALITY=3 / 4 skip the test
+    bool id_local = false;
+    if (locality && m > 0 && V < (1 << 28) && g->locality <= 2 && V > (1 << 16)) {
+      unsigned long long* d_cnt = nullptr;
+      LPA_TRY(scratch_alloc(g, (void**)&d_cnt, sizeof(unsigned long long)));
+      LPA_HIP(hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long), s));
+      hipLaunchKernelGGL(k_id_local, dim3(grid_for(m) < 2048u ? grid_for(m) : 2048u), dim3(256), 0, s, g->e_src,
+                         g->e_dst, m, 1 << 14, d_cnt);
+      LPA_HIP(hipGetLastError());
+      unsigned long long h_cnt = 0;
+      LPA_HIP(hipMemcpyAsync(&h_cnt, d_cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
+      LPA_HIP(hipStreamSynchronize(s));
+      scratch_free(g, d_cnt);
+      id_local = 2 * (int64_t)h_cnt > m;
+    }
+    g->id_order = id_local;
+    if (id_local) {
+      hipLaunchKernelGGL(k_id_order_keys, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, g->deg, g->max_degree);
+      LPA_HIP(hipGetLastError());
+      const int hi[4] = {32, 40, 48, 56};
+      LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
+    } else if (locality && m > 0 && V < (1 << 28)) {
       const int K = g->locality < 4 ? g->locality : 4;  // neighbour keys (LPA_LOCALITY)
       int32_t* rank_of = nullptr;
       LPA_TRY(scratch_alloc(g, (void**)&rank_of, sizeof(int32_t) * (1 + K) * (size_t)V));
@@ -442,110 +518,17 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     scratch_free(g, vk);
   }
 
-  // ---- owned degrees, row_ptr ----
-  int32_t* deg_own = nullptr;
-  LPA_TRY(scratch_alloc(g, (void**)&deg_own, sizeof(int32_t) * S));
-  hipLaunchKernelGGL(k_owned_degree, dim3(grid_for(S)), dim3(256), 0, s, g->old_of + g->own_begin,
-                     g->deg, S, deg_own);
-  LPA_HIP(hipGetLastError());
-  LPA_TRY(dev_alloc(g, (void**)&g->rp, sizeof(int64_t) * (S + 1)));
-  LPA_TRY(exclusive_scan_i32_i64(deg_own, g->rp, S, s));
-  int64_t arcs = 0;
-  LPA_HIP(hipMemcpyAsync(&arcs, g->rp + S, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  LPA_HIP(hipStreamSynchronize(s));
-  g->arcs = arcs;
+  return LPA_OK;
+}
 
-  // ---- 3. owned arcs, sorted ----
-  LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
-  if (arcs > 0) {
-    u64* keys = nullptr;
-    if (scratch_alloc(g, (void**)&keys, sizeof(u64) * 2 * arcs) != LPA_OK) {
-      set_error("out of device memory for %lld arc keys", (long long)(2 * arcs));
-      return LPA_ENOMEM;
-    }
-    if (P == 1) {
-      hipLaunchKernelGGL(k_emit_arcs_single, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
-                         g->e_dst, m, g->new_of, keys);
-    } else {
-      unsigned long long* cursor = nullptr;
-      LPA_TRY(scratch_alloc(g, (void**)&cursor, sizeof(unsigned long long)));
-      LPA_HIP(hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
-      hipLaunchKernelGGL(k_emit_arcs_owned, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
-                         g->e_dst, m, g->new_of, g->own_begin, g->own_begin + S, keys, cursor);
-      scratch_free(g, cursor);
-    }
-    LPA_HIP(hipGetLastError());
-    int shifts[16], ns = 0;
-    int blo = bits_for((uint64_t)(g->vpad - 1)), bhi = bits_for((uint64_t)(S - 1));
-    // columns sorted inside each row: the rebuild's gathers of a hub row coalesce.  No
-    // kernel needs the order (a mode is order-free), so a pooled internal graph (the
-    // outlier stage's 5-superstep L2 sub-graph) sorts by row only: half the passes.
-    g->cols_sorted = !g->pooled;
-    if (g->cols_sorted)
-      for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
-    for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
-    LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
-    LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t) * arcs));
-    hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col, g->crow);
-    LPA_HIP(hipGetLastError());
-    // CSC position index over this rank's arcs (for the replicated-label refresh)
-    if (arcs >= (int64_t)UINT32_MAX) {
-      set_error("%lld arcs on one rank exceed the 32-bit position index", (long long)arcs);
-      return LPA_EINVAL;
-    }
-    int32_t* colcnt = nullptr;
-    LPA_TRY(scratch_alloc(g, (void**)&colcnt, sizeof(int32_t) * g->vpad));
-    if (P == 1) {
-      // one rank: column u occurs once per arc of u, i.e. deg_own[u] times
-      LPA_HIP(hipMemcpyAsync(colcnt, deg_own, sizeof(int32_t) * g->vpad, hipMemcpyDeviceToDevice, s));
-      hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(arcs)), dim3(256), 0, s, g->col, arcs, keys, (int32_t*)nullptr);
-    } else {
-      LPA_HIP(hipMemsetAsync(colcnt, 0, sizeof(int32_t) * g->vpad, s));
-      hipLaunchKernelGGL(k_csc_keys, dim3(cap_bh(grid_for(arcs))), dim3(256), 0, s, g->col, arcs, keys, colcnt);
-    }
-    LPA_HIP(hipGetLastError());
-    int cs[8], ncs = 0;
-    for (int b = 0; b < bits_for((uint64_t)(g->vpad - 1)); b += 8) cs[ncs++] = 32 + b;
-    LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, cs, ncs, s));
-    LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
-    LPA_TRY(exclusive_scan_i32_i64(colcnt, g->cptr, g->vpad, s));
-    LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t) * arcs));
-    hipLaunchKernelGGL(k_keys_to_pos, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->cpos);
-    LPA_HIP(hipGetLastError());
-    // static scatter chunks (colcnt is reused for the per-column chunk counts)
-    hipLaunchKernelGGL(k_col_chunks, dim3(grid_for(g->vpad)), dim3(256), 0, s, colcnt, g->vpad, colcnt);
-    LPA_HIP(hipGetLastError());
-    LPA_TRY(dev_alloc(g, (void**)&g->cch, sizeof(int64_t) * (g->vpad + 1)));
-    LPA_TRY(exclusive_scan_i32_i64(colcnt, g->cch, g->vpad, s));
-    LPA_HIP(hipMemcpyAsync(&g->n_chunks, g->cch + g->vpad, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    LPA_HIP(hipStreamSynchronize(s));
-    LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t) * (g->n_chunks > 0 ? g->n_chunks : 1)));
-    {
-      // multi-chunk columns are the high-degree ones, i.e. the first slots at P = 1:
-      // the scatter scans the chunk flags only up to the last such column's chunks
-      unsigned long long* d_end = nullptr;
-      LPA_TRY(scratch_alloc(g, (void**)&d_end, sizeof(unsigned long long)));
-      LPA_HIP(hipMemsetAsync(d_end, 0, sizeof(unsigned long long), s));
-      hipLaunchKernelGGL(k_chunk_owner, dim3(grid_for(g->vpad)), dim3(256), 0, s, g->cch, g->vpad,
-                         g->cowner, d_end);
-      LPA_HIP(hipGetLastError());
-      unsigned long long h_end = 0;
-      LPA_HIP(hipMemcpyAsync(&h_end, d_end, sizeof(h_end), hipMemcpyDeviceToHost, s));
-      LPA_HIP(hipStreamSynchronize(s));
-      scratch_free(g, d_end);
-      g->n_chunk_scan = (int64_t)h_end;
-    }
-    scratch_free(g, colcnt);
-    scratch_free(g, keys);
-  } else {
-    LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
-    LPA_HIP(hipMemsetAsync(g->cptr, 0, sizeof(int64_t) * (g->vpad + 1), s));
-    LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t)));
-    LPA_TRY(dev_alloc(g, (void**)&g->cch, sizeof(int64_t) * (g->vpad + 1)));
-    LPA_HIP(hipMemsetAsync(g->cch, 0, sizeof(int64_t) * (g->vpad + 1), s));
-    LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t)));
-    g->n_chunks = 0;
-  }
+// Everything after the CSR and its CSC position index: the arc label arrays, the degree
+// bins, the hub units and combine tables, the frontier flags, the superstep-1 run
+// structures and the label vectors.  Frees deg_own (the owned degrees, scratch).
+int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
+  hipStream_t s = g->stream;
+  const int32_t P = g->nranks, r = g->rank;
+  const int64_t S = g->slice;
+  const int64_t arcs = g->arcs;
   LPA_TRY(dev_alloc(g, (void**)&g->al, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
   {
     const int64_t nfl = (g->n_chunks + 16) / 16 * 16;
@@ -675,6 +658,276 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     g->e_src = g->e_dst = nullptr;
   }
   return LPA_OK;
+}
+
+int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                uint32_t flags) {
+  hipStream_t s = g->stream;
+  const int32_t P = g->nranks, r = g->rank;
+  g->V = V;
+  g->m = m;
+  g->slice = ((int64_t)V + P - 1) / P;
+  g->slice = (g->slice + 63) / 64 * 64;  // vector-aligned slices (k_diff reads int4)
+  if (g->slice == 0) g->slice = 64;
+  g->vpad = g->slice * P;
+  g->own_begin = (int64_t)r * g->slice;
+  const int64_t S = g->slice;
+
+  // ---- keep the edge list on the device (outlier stage needs it) ----
+  LPA_TRY(dev_alloc(g, (void**)&g->e_src, sizeof(int32_t) * (m > 0 ? m : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->e_dst, sizeof(int32_t) * (m > 0 ? m : 1)));
+  if (m > 0) {
+    hipMemcpyKind kind = (flags & LPA_INPUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    LPA_HIP(hipMemcpyAsync(g->e_src, src, sizeof(int32_t) * m, kind, s));
+    LPA_HIP(hipMemcpyAsync(g->e_dst, dst, sizeof(int32_t) * m, kind, s));
+  }
+
+  // ---- 1. degrees ----
+  int32_t* d_err = nullptr;
+  int32_t* d_max = nullptr;
+  LPA_TRY(scratch_alloc(g, (void**)&d_err, 2 * sizeof(int32_t)));
+  d_max = d_err + 1;
+  LPA_HIP(hipMemsetAsync(d_err, 0, 2 * sizeof(int32_t), s));
+  LPA_TRY(dev_alloc(g, (void**)&g->deg, sizeof(int32_t) * (V > 0 ? V : 1)));
+  LPA_HIP(hipMemsetAsync(g->deg, 0, sizeof(int32_t) * (V > 0 ? V : 1), s));
+  if (m > 0) {
+    hipLaunchKernelGGL(k_degree, dim3(cap_bh(grid_for(m))), dim3(256), 0, s, g->e_src, g->e_dst, m, V,
+                       g->deg, d_err);
+    LPA_HIP(hipGetLastError());
+  }
+  if (V > 0) {
+    hipLaunchKernelGGL(k_maxdeg, dim3(grid_for(V) < 1024u ? grid_for(V) : 1024u), dim3(256), 0, s, g->deg,
+                       (int64_t)V, d_max);
+    LPA_HIP(hipGetLastError());
+  }
+  int32_t h_err[2] = {0, 0};
+  LPA_HIP(hipMemcpyAsync(h_err, d_err, sizeof(h_err), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  scratch_free(g, d_err);
+  if (h_err[0]) {
+    set_error("edge endpoint outside [0, V=%d)", V);
+    return LPA_EINVAL;
+  }
+  g->max_degree = h_err[1];
+
+  // ---- 2. degree-ranked vertex order ----
+  LPA_TRY(vertex_order(g, V, m, g->locality > 0));
+
+  // ---- owned degrees, row_ptr ----
+  int32_t* deg_own = nullptr;
+  LPA_TRY(scratch_alloc(g, (void**)&deg_own, sizeof(int32_t) * S));
+  hipLaunchKernelGGL(k_owned_degree, dim3(grid_for(S)), dim3(256), 0, s, g->old_of + g->own_begin,
+                     g->deg, S, deg_own);
+  LPA_HIP(hipGetLastError());
+  LPA_TRY(dev_alloc(g, (void**)&g->rp, sizeof(int64_t) * (S + 1)));
+  LPA_TRY(exclusive_scan_i32_i64(deg_own, g->rp, S, s));
+  int64_t arcs = 0;
+  LPA_HIP(hipMemcpyAsync(&arcs, g->rp + S, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  g->arcs = arcs;
+
+  // ---- 3. owned arcs, sorted ----
+  LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
+  if (arcs > 0) {
+    u64* keys = nullptr;
+    if (scratch_alloc(g, (void**)&keys, sizeof(u64) * 2 * arcs) != LPA_OK) {
+      set_error("out of device memory for %lld arc keys", (long long)(2 * arcs));
+      return LPA_ENOMEM;
+    }
+    if (P == 1) {
+      hipLaunchKernelGGL(k_emit_arcs_single, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
+                         g->e_dst, m, g->new_of, keys);
+    } else {
+      unsigned long long* cursor = nullptr;
+      LPA_TRY(scratch_alloc(g, (void**)&cursor, sizeof(unsigned long long)));
+      LPA_HIP(hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
+      hipLaunchKernelGGL(k_emit_arcs_owned, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
+                         g->e_dst, m, g->new_of, g->own_begin, g->own_begin + S, keys, cursor);
+      scratch_free(g, cursor);
+    }
+    LPA_HIP(hipGetLastError());
+    int shifts[16], ns = 0;
+    int blo = bits_for((uint64_t)(g->vpad - 1)), bhi = bits_for((uint64_t)(S - 1));
+    // columns sorted inside each row: the rebuild's gathers of a hub row coalesce.  No
+    // kernel needs the order (a mode is order-free), so a pooled internal graph (the
+    // outlier stage's 5-superstep L2 sub-graph) sorts by row only: half the passes.
+    g->cols_sorted = !g->pooled;
+    if (g->cols_sorted)
+      for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
+    for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
+    LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
+    LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t) * arcs));
+    hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col, g->crow);
+    LPA_HIP(hipGetLastError());
+    // CSC position index over this rank's arcs (for the replicated-label refresh)
+    if (arcs >= (int64_t)UINT32_MAX) {
+      set_error("%lld arcs on one rank exceed the 32-bit position index", (long long)arcs);
+      return LPA_EINVAL;
+    }
+    int32_t* colcnt = nullptr;
+    LPA_TRY(scratch_alloc(g, (void**)&colcnt, sizeof(int32_t) * g->vpad));
+    if (P == 1) {
+      // one rank: column u occurs once per arc of u, i.e. deg_own[u] times
+      LPA_HIP(hipMemcpyAsync(colcnt, deg_own, sizeof(int32_t) * g->vpad, hipMemcpyDeviceToDevice, s));
+      hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(arcs)), dim3(256), 0, s, g->col, arcs, keys, (int32_t*)nullptr);
+    } else {
+      LPA_HIP(hipMemsetAsync(colcnt, 0, sizeof(int32_t) * g->vpad, s));
+      hipLaunchKernelGGL(k_csc_keys, dim3(cap_bh(grid_for(arcs))), dim3(256), 0, s, g->col, arcs, keys, colcnt);
+    }
+    LPA_HIP(hipGetLastError());
+    int cs[8], ncs = 0;
+    for (int b = 0; b < bits_for((uint64_t)(g->vpad - 1)); b += 8) cs[ncs++] = 32 + b;
+    LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, cs, ncs, s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
+    LPA_TRY(exclusive_scan_i32_i64(colcnt, g->cptr, g->vpad, s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t) * arcs));
+    hipLaunchKernelGGL(k_keys_to_pos, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->cpos);
+    LPA_HIP(hipGetLastError());
+    // static scatter chunks (colcnt is reused for the per-column chunk counts)
+    hipLaunchKernelGGL(k_col_chunks, dim3(grid_for(g->vpad)), dim3(256), 0, s, colcnt, g->vpad, colcnt);
+    LPA_HIP(hipGetLastError());
+    LPA_TRY(dev_alloc(g, (void**)&g->cch, sizeof(int64_t) * (g->vpad + 1)));
+    LPA_TRY(exclusive_scan_i32_i64(colcnt, g->cch, g->vpad, s));
+    LPA_HIP(hipMemcpyAsync(&g->n_chunks, g->cch + g->vpad, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t) * (g->n_chunks > 0 ? g->n_chunks : 1)));
+    {
+      // multi-chunk columns are the high-degree ones, i.e. the first slots at P = 1:
+      // the scatter scans the chunk flags only up to the last such column's chunks
+      unsigned long long* d_end = nullptr;
+      LPA_TRY(scratch_alloc(g, (void**)&d_end, sizeof(unsigned long long)));
+      LPA_HIP(hipMemsetAsync(d_end, 0, sizeof(unsigned long long), s));
+      hipLaunchKernelGGL(k_chunk_owner, dim3(grid_for(g->vpad)), dim3(256), 0, s, g->cch, g->vpad,
+                         g->cowner, d_end);
+      LPA_HIP(hipGetLastError());
+      unsigned long long h_end = 0;
+      LPA_HIP(hipMemcpyAsync(&h_end, d_end, sizeof(h_end), hipMemcpyDeviceToHost, s));
+      LPA_HIP(hipStreamSynchronize(s));
+      scratch_free(g, d_end);
+      g->n_chunk_scan = (int64_t)h_end;
+    }
+    scratch_free(g, colcnt);
+    scratch_free(g, keys);
+  } else {
+    LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
+    LPA_HIP(hipMemsetAsync(g->cptr, 0, sizeof(int64_t) * (g->vpad + 1), s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t)));
+    LPA_TRY(dev_alloc(g, (void**)&g->cch, sizeof(int64_t) * (g->vpad + 1)));
+    LPA_HIP(hipMemsetAsync(g->cch, 0, sizeof(int64_t) * (g->vpad + 1), s));
+    LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t)));
+    g->n_chunks = 0;
+  }
+  return finish_build(g, deg_own, m);
+}
+
+
+// The outlier stage's L2 sub-graph (E' = the distinct (s, d) with
+// L[s] == L[d], Graphframes.py:121-128) built without sorting arcs: the parent's distinct
+// edges are kept in (s, d) order (de_keys) and in (d, s) order (de_t), so a row's intra
+// arcs are a filter of its two runs -- marks, two exclusive scans, the degrees as
+// segment-length differences (no per-vertex atomics), the degree-ranked slot order (a
+// sort of V keys), then every arc written at its final position, with its CSC twin.
+// Rows keep their columns in run order (cols_sorted = false: no column-run superstep).
+int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L) {
+  hipStream_t s = g->stream;
+  const int32_t V = (int32_t)parent->V;
+  const int64_t md = parent->de_n;
+  g->V = V;
+  g->slice = ((int64_t)V + 63) / 64 * 64;
+  if (g->slice == 0) g->slice = 64;
+  g->vpad = g->slice;
+  g->own_begin = 0;
+  g->cols_sorted = false;
+  const int64_t S = g->slice;
+  int32_t *mo = nullptr, *mi = nullptr, *dout = nullptr, *d_max = nullptr;
+  int64_t *pos_out = nullptr, *pos_in = nullptr;
+  LPA_TRY(scratch_alloc(g, (void**)&mo, sizeof(int32_t) * (md > 0 ? md : 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&mi, sizeof(int32_t) * (md > 0 ? md : 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&pos_out, sizeof(int64_t) * (md + 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&pos_in, sizeof(int64_t) * (md + 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&dout, sizeof(int32_t) * (V > 0 ? V : 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&d_max, sizeof(int32_t)));
+  LPA_TRY(dev_alloc(g, (void**)&g->deg, sizeof(int32_t) * (V > 0 ? V : 1)));
+  if (md > 0) {
+    hipLaunchKernelGGL(k_l2_mark_out, dim3(grid_for(md)), dim3(256), 0, s, parent->de_keys, md, L, mo);
+    hipLaunchKernelGGL(k_l2_mark_in, dim3(grid_for(md)), dim3(256), 0, s, parent->de_t, parent->de_ts, md, L, mi);
+    LPA_HIP(hipGetLastError());
+  }
+  LPA_TRY(exclusive_scan_i32_i64(mo, pos_out, md, s));
+  LPA_TRY(exclusive_scan_i32_i64(mi, pos_in, md, s));
+  LPA_HIP(hipMemsetAsync(d_max, 0, sizeof(int32_t), s));
+  if (V > 0) {
+    hipLaunchKernelGGL(k_l2_degree, dim3(grid_for(V)), dim3(256), 0, s, parent->de_out_off, parent->de_in_off,
+                       pos_out, pos_in, (int64_t)V, g->deg, dout);
+    hipLaunchKernelGGL(k_maxdeg, dim3(grid_for(V) < 1024u ? grid_for(V) : 1024u), dim3(256), 0, s, g->deg,
+                       (int64_t)V, d_max);
+    LPA_HIP(hipGetLastError());
+  }
+  int64_t m2 = 0;
+  LPA_HIP(hipMemcpyAsync(&m2, pos_out + md, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipMemcpyAsync(&g->max_degree, d_max, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  g->m = m2;
+  scratch_free(g, d_max);
+
+  // ---- degree-ranked slots, row offsets ----
+  LPA_TRY(vertex_order(g, V, m2, false));
+  int32_t* deg_own = nullptr;
+  LPA_TRY(scratch_alloc(g, (void**)&deg_own, sizeof(int32_t) * S));
+  hipLaunchKernelGGL(k_owned_degree, dim3(grid_for(S)), dim3(256), 0, s, g->old_of, g->deg, S, deg_own);
+  LPA_HIP(hipGetLastError());
+  LPA_TRY(dev_alloc(g, (void**)&g->rp, sizeof(int64_t) * (S + 1)));
+  LPA_TRY(exclusive_scan_i32_i64(deg_own, g->rp, S, s));
+  const int64_t arcs = 2 * m2;
+  g->arcs = arcs;
+  if (arcs >= (int64_t)UINT32_MAX) {
+    set_error("%lld arcs in the L2 sub-graph exceed the 32-bit position index", (long long)arcs);
+    return LPA_EINVAL;
+  }
+
+  // ---- arcs at their final positions, the CSC as their twins ----
+  LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t) * (arcs > 0 ? arcs : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
+  LPA_HIP(hipMemcpyAsync(g->cptr, g->rp, sizeof(int64_t) * (S + 1), hipMemcpyDeviceToDevice, s));
+  if (md > 0) {
+    hipLaunchKernelGGL(k_l2_emit_out, dim3(grid_for(md)), dim3(256), 0, s, parent->de_keys, md, mo, pos_out,
+                       parent->de_out_off, g->new_of, g->rp, g->col, g->crow);
+    hipLaunchKernelGGL(k_l2_emit_in, dim3(grid_for(md)), dim3(256), 0, s, parent->de_t, parent->de_ts, md, mi,
+                       pos_in, parent->de_in_off, pos_out, parent->de_out_off, dout, g->new_of, g->rp, g->col,
+                       g->crow, g->cpos);
+    LPA_HIP(hipGetLastError());
+  }
+  scratch_free(g, mo);
+  scratch_free(g, mi);
+  scratch_free(g, pos_out);
+  scratch_free(g, pos_in);
+  scratch_free(g, dout);
+  // static scatter chunks of every column (its count is its degree: P = 1, symmetric)
+  int32_t* nch = nullptr;
+  LPA_TRY(scratch_alloc(g, (void**)&nch, sizeof(int32_t) * S));
+  hipLaunchKernelGGL(k_col_chunks, dim3(grid_for(S)), dim3(256), 0, s, deg_own, S, nch);
+  LPA_HIP(hipGetLastError());
+  LPA_TRY(dev_alloc(g, (void**)&g->cch, sizeof(int64_t) * (g->vpad + 1)));
+  LPA_TRY(exclusive_scan_i32_i64(nch, g->cch, g->vpad, s));
+  LPA_HIP(hipMemcpyAsync(&g->n_chunks, g->cch + g->vpad, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  scratch_free(g, nch);
+  LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t) * (g->n_chunks > 0 ? g->n_chunks : 1)));
+  {
+    unsigned long long* d_end = nullptr;
+    LPA_TRY(scratch_alloc(g, (void**)&d_end, sizeof(unsigned long long)));
+    LPA_HIP(hipMemsetAsync(d_end, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_chunk_owner, dim3(grid_for(g->vpad)), dim3(256), 0, s, g->cch, g->vpad, g->cowner, d_end);
+    LPA_HIP(hipGetLastError());
+    unsigned long long h_end = 0;
+    LPA_HIP(hipMemcpyAsync(&h_end, d_end, sizeof(h_end), hipMemcpyDeviceToHost, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    scratch_free(g, d_end);
+    g->n_chunk_scan = (int64_t)h_end;
+  }
+  return finish_build(g, deg_own, m2);
 }
 
 }  // namespace lpa

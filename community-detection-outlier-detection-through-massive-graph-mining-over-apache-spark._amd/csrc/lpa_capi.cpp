@@ -81,7 +81,7 @@ void destroy(lpa_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   void* bufs[] = {g->rp,   g->col,   g->new_of, g->old_of, g->deg,   g->lab[0], g->lab[1],
-                  g->segs, g->e_src,  g->e_dst, g->de_keys, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
+                  g->segs, g->e_src,  g->e_dst, g->de_keys, g->de_t, g->de_ts, g->de_out_off, g->de_in_off, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
                   g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
@@ -140,7 +140,8 @@ static int check_edges(const int32_t* src, const int32_t* dst, int64_t m, int32_
 int create_common(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
                   int64_t m, int32_t V, uint32_t flags, int32_t rank, int32_t nranks,
                   const uint8_t* comm_id, Loopback* loop, lpa_graph** out,
-                  const lpa_graph* borrow = nullptr) {
+                  const lpa_graph* borrow = nullptr, const lpa_graph* l2_parent = nullptr,
+                  const int32_t* l2_labels = nullptr) {
   if (!out) {
     set_error("out must be non-null");
     return LPA_EINVAL;
@@ -224,7 +225,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
       return LPA_ERCCL;
     }
   }
-  int rc = build_graph(g, src, dst, m, V, flags);
+  int rc = l2_parent ? build_graph_l2(g, l2_parent, l2_labels) : build_graph(g, src, dst, m, V, flags);
   if (rc == LPA_OK) rc = exchange_alloc(g);
   if (rc != LPA_OK) {
     destroy(g);
@@ -234,9 +235,11 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   return LPA_OK;
 }
 
-int create_local(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
-                 int64_t m, int32_t V, uint32_t flags, lpa_graph** out, const lpa_graph* borrow) {
-  return create_common(device, stream, src, dst, m, V, flags, 0, 1, nullptr, nullptr, out, borrow);
+// the outlier stage's L2 sub-graph of `parent` under the community labels L (device,
+// dense ids): pooled, on the parent's stream, borrowing its aux streams
+int create_l2(const lpa_graph* parent, const int32_t* L, lpa_graph** out) {
+  return create_common(parent->device, parent->stream, nullptr, nullptr, 0, (int32_t)parent->V,
+                       kFlagNoLocality | kFlagPooled, 0, 1, nullptr, nullptr, out, parent, parent, L);
 }
 
 }  // namespace lpa
@@ -493,7 +496,21 @@ int lpa_outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, i
   }
   LPA_HIP(hipSetDevice(g->device));
   return outlier(g, labels, labels_on_device, mode, sub_iter, size_hist, incident, sub_labels, flags,
-                 summary);
+                 summary, 0);
+}
+
+int lpa_outlier_device(lpa_graph* g, const int32_t* labels, int32_t mode, int32_t sub_iter, int64_t* size_hist,
+                       int64_t* incident, int32_t* sub_labels, uint8_t* flags, lpa_outlier_summary* summary) {
+  if (!g || (!labels && g->V > 0)) {
+    set_error("null handle or labels");
+    return LPA_EINVAL;
+  }
+  if (g->nranks > 1) {
+    set_error("lpa_outlier runs on a single-GPU handle");
+    return LPA_EINVAL;
+  }
+  LPA_HIP(hipSetDevice(g->device));
+  return outlier(g, labels, 1, mode, sub_iter, size_hist, incident, sub_labels, flags, summary, 1);
 }
 
 int lpa_quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, lpa_quality_summary* out) {
@@ -534,6 +551,7 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->own_begin = g->own_begin;
   info->rank = g->rank;
   info->nranks = g->nranks;
+  info->id_order = g->id_order ? 1 : 0;
   info->device = g->device;
   info->max_degree = g->max_degree;
   for (int b = 0; b < LPA_NBINS; ++b) {

@@ -227,6 +227,7 @@ struct lpa_graph {
   // (superstep, cur, par)
   hipGraphExec_t gexec[16] = {};
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
+  bool id_order = false;                    // the input ids carry locality: id order inside the bins
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
@@ -248,6 +249,13 @@ struct lpa_graph {
   // and kept (label-independent topology, as GraphFrames' cachedTopologyGraphX)
   lpa::u64* de_keys = nullptr;
   int64_t de_n = -1;                        // -1: not built yet
+  // ... and, for the L2 sub-graph build (first L2 call, kept): the same edges in (d, s)
+  // order as (d << 32 | index into de_keys), their s, and the first index of every
+  // vertex's run in either order ([V + 1] each)
+  lpa::u64* de_t = nullptr;
+  uint32_t* de_ts = nullptr;
+  int64_t* de_out_off = nullptr;
+  int64_t* de_in_off = nullptr;
   void* host_pin = nullptr;                 // outlier stage: pinned staging of host labels in /
   size_t host_pin_bytes = 0;                //   arrays out (kept with the handle)
 
@@ -287,6 +295,10 @@ int bits_for(uint64_t maxval);  // bits needed to represent maxval (0 -> 0)
 int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
                 uint32_t flags);
 int init_labels(lpa_graph* g);
+// the outlier stage's L2 sub-graph (P = 1, pooled handle g, V vertices) straight from the
+// parent's sorted distinct edge orders: E' = distinct (s, d) with L[s] == L[d], no sort
+// of arcs (lpa_build.hip)
+int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L);
 int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
 // join = false: the forked bucket path's end is recorded in ev_join2[0] and the caller
 // joins it (main-stream work can be queued behind the mid tiers first)
@@ -329,7 +341,7 @@ int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool 
 // outlier (lpa_outlier.hip)
 int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
             int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
-            uint8_t* flags, lpa_outlier_summary* summary);
+            uint8_t* flags, lpa_outlier_summary* summary, int32_t out_on_device);
 int quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, lpa_quality_summary* out);
 
 }  // namespace lpa

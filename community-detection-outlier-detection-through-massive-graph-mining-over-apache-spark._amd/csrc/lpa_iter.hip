@@ -2071,10 +2071,16 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
   if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(s_cnt, (u32)cnt);
   __syncthreads();
   const bool bits = 2 * (int64_t)*s_cnt >= nhb && nhb > 0;  // uniform: the same data in every block
+  // hybrid (P = 1): G on >= 1/8 of the bit-range slots but not on half -- the hot
+  // slots' LABELS in LDS, a cold column's bit from gbits, its label gathered only when
+  // the bit is clear (Chung-Lu C5 superstep 2: G on ~40 % of the arcs, ~30 % of the cold
+  // gathers become L2 / Infinity-Cache hits on the 5 MB bit array)
+  const bool hyb = !kRanked && !bits && 8 * (int64_t)*s_cnt >= nhb && nhb > 0;
   const int32_t G = gword[0];
-  // bits mode also writes the arc giant bits (abits: bit i = al[i] == G, one ballot per
-  // 64 arcs), which the next superstep's full tally settles rows from (k_settle_*)
-  if (blockIdx.x == 0 && threadIdx.x == 0) gword[2] = bits ? 1 : 0;
+  // bits / hybrid modes also write the arc giant bits (abits: bit i = al[i] == G, one
+  // ballot per 64 arcs), which the next superstep's full tally settles rows from
+  // (k_settle_*)
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[2] = (bits || hyb) ? 1 : 0;
   if (!bits) {
     __syncthreads();
     for (int i = threadIdx.x; i < nhot; i += 1024)
@@ -2106,13 +2112,15 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
   } else {
     auto p1 = [&](int c) -> u32 {
       if (bits) return (u32)c < (u32)nhb ? hot[(u32)c >> 5] : gbits[(u32)c >> 5];
+      if (hyb) return (u32)c < nh ? hot[c] : gbits[(u32)c >> 5];
       return (u32)c < nh ? hot[c] : 0u;
     };
     auto p2 = [&](int c, u32 w) -> int32_t {
       if (bits) return ((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c];
+      if (hyb) return (u32)c < nh ? (int32_t)w : (((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c]);
       return (u32)c < nh ? (int32_t)w : Ln[c];
     };
-    rebuild_pipe(p1, p2, G, bits, col, arcs, al, abits);
+    rebuild_pipe(p1, p2, G, bits || hyb, col, arcs, al, abits);
   }
 }
 

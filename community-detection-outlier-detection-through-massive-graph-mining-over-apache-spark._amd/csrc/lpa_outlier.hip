@@ -25,8 +25,7 @@
 
 namespace lpa {
 
-int create_local(int32_t device, hipStream_t stream, const int32_t* src, const int32_t* dst,
-                 int64_t m, int32_t V, uint32_t flags, lpa_graph** out, const lpa_graph* borrow);
+int create_l2(const lpa_graph* parent, const int32_t* L, lpa_graph** out);
 void destroy(lpa_graph* g);
 
 namespace {
@@ -122,18 +121,26 @@ __global__ __launch_bounds__(256) void k_incident(const u64* __restrict__ ek, in
   bh.flush(inc);
 }
 
-// E' edges: distinct edges whose endpoints share a label
-__global__ void k_mark_intra(const u64* __restrict__ ek, int64_t n, const int32_t* __restrict__ L,
-                             int32_t* __restrict__ mark) {
-  GRID_STRIDE(i, n) mark[i] = (L[(int32_t)(ek[i] >> 32)] == L[(int32_t)(u32)ek[i]]) ? 1 : 0;
+// the distinct edges in (d, s) order: keys (d << 32 | i) generated in de_keys order,
+// where i ascends with s for a fixed d, so a stable sort on the d bits alone gives (d, s)
+__global__ void k_t_keys(const u64* __restrict__ ek, int64_t n, u64* __restrict__ t) {
+  GRID_STRIDE(i, n) t[i] = ((u64)(u32)ek[i] << 32) | (u64)i;
 }
-
-__global__ void k_split_marked(const u64* __restrict__ ek, const int32_t* __restrict__ mark,
-                               const int64_t* __restrict__ pos, int64_t n, int32_t* __restrict__ s,
-                               int32_t* __restrict__ d) {
-  GRID_STRIDE(i, n) if (mark[i]) {
-    s[pos[i]] = (int32_t)(ek[i] >> 32);
-    d[pos[i]] = (int32_t)(u32)ek[i];
+__global__ void k_t_src(const u64* __restrict__ ek, const u64* __restrict__ t, int64_t n, uint32_t* __restrict__ ts) {
+  GRID_STRIDE(j, n) ts[j] = (uint32_t)(ek[(u32)t[j]] >> 32);
+}
+// first index of every vertex's run in keys sorted by their high 32 bits ([V + 1])
+__global__ void k_run_offsets(const u64* __restrict__ k, int64_t n, int64_t V, int64_t* __restrict__ off) {
+  if (n == 0) {
+    GRID_STRIDE(v, V + 1) off[v] = 0;
+    return;
+  }
+  GRID_STRIDE(i, n) {
+    const int64_t cur = (int64_t)(k[i] >> 32);
+    const int64_t prev = i == 0 ? -1 : (int64_t)(k[i - 1] >> 32);
+    for (int64_t v = prev + 1; v <= cur; ++v) off[v] = i;
+    if (i == n - 1)
+      for (int64_t v = cur + 1; v <= V; ++v) off[v] = n;
   }
 }
 
@@ -282,6 +289,38 @@ int distinct_edges(lpa_graph* g) {
   LPA_HIP(hipGetLastError());
   LPA_HIP(hipStreamSynchronize(s));   // the scratch is freed on return
   g->de_n = n;
+  return LPA_OK;
+}
+
+// The distinct edges in (d, s) order (de_t, de_ts) and both orders' per-vertex run
+// offsets: what the L2 sub-graph build filters (build_graph_l2).  Built by the first L2
+// call and kept with the handle (topology, like de_keys).
+int transposed_edges(lpa_graph* g) {
+  if (g->de_t) return LPA_OK;
+  hipStream_t s = g->stream;
+  const int64_t md = g->de_n, V = g->V;
+  LPA_TRY(dev_alloc(g, (void**)&g->de_out_off, sizeof(int64_t) * (V + 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->de_in_off, sizeof(int64_t) * (V + 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->de_ts, sizeof(uint32_t) * (md > 0 ? md : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->de_t, sizeof(u64) * (md > 0 ? md : 1)));
+  if (md > 0) {
+    Scratch sc(s);
+    u64* tmp = nullptr;
+    LPA_TRY(sc.get(&tmp, md));
+    hipLaunchKernelGGL(k_t_keys, dim3(grid_for(md)), dim3(256), 0, s, g->de_keys, md, g->de_t);
+    LPA_HIP(hipGetLastError());
+    int shifts[8], ns = 0;
+    for (int b = 0; b < bits_for((uint64_t)(V > 0 ? V - 1 : 0)); b += 8) shifts[ns++] = 32 + b;
+    LPA_TRY(radix_sort_u64(g->de_t, tmp, md, shifts, ns, s));
+    hipLaunchKernelGGL(k_t_src, dim3(grid_for(md)), dim3(256), 0, s, g->de_keys, g->de_t, md, g->de_ts);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipStreamSynchronize(s));   // the scratch is freed on return
+  }
+  hipLaunchKernelGGL(k_run_offsets, dim3(grid_for(md > V ? md : V + 1)), dim3(256), 0, s, g->de_keys, md, V,
+                     g->de_out_off);
+  hipLaunchKernelGGL(k_run_offsets, dim3(grid_for(md > V ? md : V + 1)), dim3(256), 0, s, g->de_t, md, V,
+                     g->de_in_off);
+  LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
 
@@ -471,7 +510,7 @@ int quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, lpa_q
 // which the second LPA's graph build needs).
 int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
             int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
-            uint8_t* flags, lpa_outlier_summary* summary) {
+            uint8_t* flags, lpa_outlier_summary* summary, int32_t out_on_device) {
   if (mode != 1 && mode != 2) {
     set_error("outlier mode must be 1 (L1) or 2 (L2), got %d", mode);
     return LPA_EINVAL;
@@ -502,8 +541,9 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     if (summary) *summary = sum;
     return LPA_OK;
   }
-  // pinned staging: [labels 4V | size 8V | incident 8V | sub-labels 4V | flags V]
-  LPA_TRY(ensure_pin(g, (size_t)25 * (size_t)V));
+  // pinned staging: [labels 4V | size 8V | incident 8V | sub-labels 4V | flags V] (host
+  // labels in or host arrays out only)
+  if (!labels_on_device || !out_on_device) LPA_TRY(ensure_pin(g, (size_t)25 * (size_t)V));
   char* pin = (char*)g->host_pin;
   int32_t* pin_lab = (int32_t*)pin;
   int64_t* pin_size = (int64_t*)(pin + 4 * V);
@@ -553,35 +593,19 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     sum.n_communities_flagged = sum.n_flagged > 0 ? 1 : 0;
     sum.distinct_edges = md;
   } else {
-    // E' = distinct intra-community edges (compacted: the second LPA builds on it)
-    int32_t* mark = nullptr;
-    int64_t* pos = nullptr;
-    int32_t *s2 = nullptr, *d2 = nullptr, *sub = nullptr, *subsize = nullptr;
-    LPA_TRY(sc.get(&mark, md));
-    LPA_TRY(sc.get(&pos, md + 1));
-    if (md > 0) {
-      hipLaunchKernelGGL(k_mark_intra, dim3(grid_for(md)), dim3(256), 0, s, ek, md, L, mark);
-      LPA_HIP(hipGetLastError());
-    }
-    LPA_TRY(exclusive_scan_i32_i64(mark, pos, md, s));
-    int64_t m2 = 0;
+    // E' = the distinct intra-community edges: the sub-graph is built straight from the
+    // handle's two sorted distinct-edge orders (build_graph_l2, no arc sort)
+    int32_t *sub = nullptr, *subsize = nullptr;
     unsigned long long nbad = 0;
-    LPA_HIP(hipMemcpyAsync(&m2, pos + md, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     LPA_HIP(hipMemcpyAsync(&nbad, cnt + 3, sizeof(nbad), hipMemcpyDeviceToHost, s));
-    LPA_HIP(hipStreamSynchronize(s));   // the one round trip: E' size for the build
+    LPA_HIP(hipStreamSynchronize(s));
     if (nbad) return bad_labels(nbad, V);
-    LPA_TRY(sc.get(&s2, m2));
-    LPA_TRY(sc.get(&d2, m2));
     LPA_TRY(sc.get(&sub, V));
     LPA_TRY(sc.get(&subsize, V));
-    if (md > 0) {
-      hipLaunchKernelGGL(k_split_marked, dim3(grid_for(md)), dim3(256), 0, s, ek, mark, pos, md, s2, d2);
-      LPA_HIP(hipGetLastError());
-    }
+    LPA_TRY(transposed_edges(g));
     // second LPA on the induced simple subgraph (same device, same stream)
     lpa_graph* h = nullptr;
-    LPA_TRY(create_local(g->device, s, s2, d2, m2, (int32_t)V, LPA_INPUT_DEVICE | kFlagNoLocality | kFlagPooled, &h,
-                               g));
+    LPA_TRY(create_l2(g, L, &h));
     int rc = run_supersteps(h, sub_iter, nullptr);
     if (rc == LPA_OK) rc = gather_labels(h, sub);
     if (rc == LPA_OK && hipStreamSynchronize(s) != hipSuccess) rc = LPA_EHIP;
@@ -599,7 +623,9 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     LPA_HIP(hipGetLastError());
     unsigned long long h_cnt[8];
     LPA_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
-    if (sub_labels) LPA_HIP(hipMemcpyAsync(pin_sub, sub, sizeof(int32_t) * V, hipMemcpyDeviceToHost, s));
+    if (sub_labels)
+      LPA_HIP(hipMemcpyAsync(out_on_device ? (void*)sub_labels : (void*)pin_sub, sub, sizeof(int32_t) * V,
+                             out_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
     sum.n_groups = (int64_t)h_cnt[4];
     sum.k = -1;
@@ -612,6 +638,16 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
 
   // every output into the pinned area in stream order (`wide` is reused: each copy is
   // ordered before the next widening), one sync, then the threaded host copies
+  if (out_on_device) {
+    // device outputs: widened / copied in place, one sync for the stream's work
+    if (size_hist) hipLaunchKernelGGL(k_widen, dim3(grid_for(V)), dim3(256), 0, s, size, V, size_hist);
+    if (incident) hipLaunchKernelGGL(k_widen, dim3(grid_for(V)), dim3(256), 0, s, inc, V, incident);
+    LPA_HIP(hipGetLastError());
+    if (flags) LPA_HIP(hipMemcpyAsync(flags, fl, V, hipMemcpyDeviceToDevice, s));
+    LPA_HIP(hipStreamSynchronize(s));
+    if (summary) *summary = sum;
+    return LPA_OK;
+  }
   if (size_hist) {
     hipLaunchKernelGGL(k_widen, dim3(grid_for(V)), dim3(256), 0, s, size, V, wide);
     LPA_HIP(hipGetLastError());

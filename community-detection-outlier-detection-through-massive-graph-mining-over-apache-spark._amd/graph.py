@@ -189,11 +189,16 @@ class Graph:
 
     # -- outlier stage --------------------------------------------------------
     def outlier(self, labels, mode="L1", sub_iter: int = 5):
-        """Appendix B outlier stage.  Returns dict(size, incident, sub_labels, flags, summary)."""
+        """Appendix B outlier stage.  Returns dict(size, incident, sub_labels, flags, summary):
+        host numpy arrays for host labels; for a device label tensor (int32, this
+        handle's device) every output is a device tensor of this device and nothing is
+        staged through the host (lpa_outlier_device)."""
         if mode not in OUTLIER_MODES:
             raise ValueError(f"mode must be 'L1' or 'L2', got {mode!r}")
         md = OUTLIER_MODES[mode]
         V = self.num_vertices
+        if _is_device_tensor(labels):
+            return self._outlier_device(labels, md, sub_iter)
         lab = np.ascontiguousarray(labels, dtype=np.int32)
         if lab.shape != (V,):
             raise ValueError(f"labels must have shape ({V},)")
@@ -211,6 +216,29 @@ class Graph:
         return dict(size=size, incident=inc, sub_labels=sub, flags=flags.astype(bool),
                     summary=summ.to_dict())
 
+
+    def _outlier_device(self, labels, md: int, sub_iter: int):
+        import torch
+
+        V = self.num_vertices
+        if labels.dtype != torch.int32:
+            raise ValueError(f"device labels must be int32, got {labels.dtype}")
+        if labels.device.index != self.device:
+            raise ValueError(f"device labels must be on cuda:{self.device}, got {labels.device}")
+        if labels.numel() != V:
+            raise ValueError(f"labels must hold {V} entries")
+        lab = labels.contiguous()
+        dev = lab.device
+        size = torch.empty(V, dtype=torch.int64, device=dev)
+        inc = torch.empty(V, dtype=torch.int64, device=dev)
+        sub = torch.empty(V, dtype=torch.int32, device=dev) if md == 2 else None
+        flags = torch.empty(V, dtype=torch.uint8, device=dev)
+        torch.cuda.current_stream(dev).synchronize()   # the library works on its own stream
+        summ = _lib.LpaOutlierSummary()
+        _lib.check(self._lib.lpa_outlier_device(
+            self._handle(), lab.data_ptr(), md, int(sub_iter), size.data_ptr(), inc.data_ptr(),
+            sub.data_ptr() if sub is not None else None, flags.data_ptr(), ctypes.byref(summ)))
+        return dict(size=size, incident=inc, sub_labels=sub, flags=flags.bool(), summary=summ.to_dict())
 
     def quality(self, labels) -> dict:
         """Community count and modularity of a labelling (host array or device tensor of

@@ -78,6 +78,8 @@ typedef struct lpa_graph_info {
   int64_t device_bytes; /* device memory held by the handle                   */
   int64_t exchanges_full;  /* P > 1: label exchanges done as a full allgather   */
   int64_t exchanges_delta; /* P > 1: label exchanges done as changed-label deltas */
+  int64_t id_order;        /* 1: the input ids carry locality (most edges within 16 K ids),
+                              so the slots inside each degree bin keep the id order */
 } lpa_graph_info;
 
 /* Outlier summary. */
@@ -210,6 +212,14 @@ int lpa_run(lpa_graph* g, int32_t max_iter, int32_t* labels_out, int32_t out_is_
 int lpa_outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32_t mode,
                 int32_t sub_iter, int64_t* size_hist, int64_t* incident, int32_t* sub_labels,
                 uint8_t* flags, lpa_outlier_summary* summary);
+
+/* The same stage with every array on the device (`device` of the handle): labels in,
+ * size_hist / incident (int64[V]), sub_labels (int32[V], L2) and flags (uint8[V]) out,
+ * each output nullable; no host staging (the pipeline form: labels straight from
+ * lpa_run(..., out_is_device = 1), results consumed on the GPU). */
+int lpa_outlier_device(lpa_graph* g, const int32_t* labels, int32_t mode, int32_t sub_iter,
+                       int64_t* size_hist, int64_t* incident, int32_t* sub_labels, uint8_t* flags,
+                       lpa_outlier_summary* summary);
 
 /* Partition quality of a labelling (dense ids, values in [0, V)) on the handle's
  * symmetrised multigraph, the graph labelPropagation votes on (A = 2m arcs: every

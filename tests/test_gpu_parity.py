@@ -294,6 +294,35 @@ def test_chunglu_heavy_hub_every_superstep(gfa, oracle):
         assert np.array_equal(got[t], hist[t]), f"Chung-Lu superstep {t + 1}"
 
 
+def test_sbm_id_order_every_superstep(gfa, oracle):
+    """An SBM with block-contiguous ids (200 K vertices, 100 blocks): the build detects
+    the input-id locality and keeps the id order inside the degree bins; every superstep
+    bit-exact, on one GPU and over a P = 2 loopback group; R-MAT's scrambled ids do not
+    trigger it."""
+    V = 200_000
+    s, d = gfa.gen_sbm(V, 100, 4_000_000, seed=5)
+    sn, dn = s.cpu().numpy(), d.cpu().numpy()
+    _, hist, _ = oracle.lpa(V, sn, dn, 8, per_iter=True)
+    with gfa.Graph(s, d, V) as g:
+        assert g.info()["id_order"] == 1
+        for t in range(8):
+            g.step(1)
+            assert np.array_equal(g.labels(), hist[t]), f"superstep {t + 1}"
+    lb = gfa.Loopback(2)
+    ranks = [gfa.Graph(sn, dn, V, rank=r, loopback=lb) for r in range(2)]
+    try:
+        assert all(g.info()["id_order"] == 1 for g in ranks)
+        runs = gfa.run_ranks(ranks, lambda r, g: g.run(8))
+        assert all(np.array_equal(x, hist[7]) for x in runs)
+    finally:
+        for g in ranks:
+            g.close()
+        lb.close()
+    ts, td = gfa.gen_rmat(17, 16, seed=1)
+    with gfa.Graph(ts, td, 1 << 17) as g:
+        assert g.info()["id_order"] == 0
+
+
 def test_sbm_bit_exact(gfa, oracle):
     s, d = gfa.gen_sbm(20000, 20, 400000)
     with gfa.Graph(s, d, 20000) as g:
@@ -415,6 +444,55 @@ def test_outlier_vs_oracle(gfa, oracle, seed):
         sub, flags2, summ2 = oracle.outlier_l2(V, s, d, lab, 4)
         assert np.array_equal(o2["sub_labels"], sub) and np.array_equal(o2["flags"], flags2)
         assert o2["summary"]["n_flagged"] == summ2["n_flagged"]
+
+
+@pytest.mark.parametrize("case", ["mix_run", "mix_random_labels", "reciprocal_loops", "rmat_coarse"])
+def test_outlier_l2_subgraph_and_device(gfa, oracle, case):
+    """The L2 sub-graph built straight from the distinct-edge orders (no arc sort):
+    reciprocal pairs (u, v) + (v, u) (two arcs of the same column in a row), self-loops,
+    duplicates, isolated vertices, arbitrary (non-LPA) community labels; L1 / L2 vs the
+    oracle, and the device-array form (lpa_outlier_device) equal to the host form."""
+    import torch
+
+    rng = np.random.default_rng(11)
+    if case.startswith("mix"):
+        V, s, d = degree_mix(7, hubs=(900, 2500), n_low=2500, extra=9000)
+    elif case == "reciprocal_loops":
+        V = 3000
+        a = rng.integers(0, V - 200, size=6000)
+        b = rng.integers(0, V - 200, size=6000)
+        loops = rng.integers(0, V - 200, size=300)
+        s = np.concatenate([a, b, loops, a[:500]]).astype(np.int32)     # (a, b), (b, a), loops, dups
+        d = np.concatenate([b, a, loops, b[:500]]).astype(np.int32)
+    else:
+        ts, td = gfa.gen_rmat(15, 16, seed=4)
+        V, s, d = 1 << 15, ts.cpu().numpy(), td.cpu().numpy()
+    with gfa.Graph(s, d, V) as g:
+        if case == "mix_random_labels":
+            lab = rng.integers(0, 40, size=V).astype(np.int32)        # 40 arbitrary communities
+        elif case == "rmat_coarse":
+            lab = (g.run(2) % 97).astype(np.int32)
+        else:
+            lab = g.run(3)
+        o1 = g.outlier(lab, "L1")
+        o2 = g.outlier(lab, "L2", sub_iter=4)
+        dl = torch.from_numpy(lab).cuda()
+        d1 = g.outlier(dl, "L1")
+        d2 = g.outlier(dl, "L2", sub_iter=4)
+    size, inc, flags, summ = oracle.outlier_l1(V, s, d, lab)
+    assert np.array_equal(o1["size"], size) and np.array_equal(o1["incident"], inc)
+    assert np.array_equal(o1["flags"], flags) and o1["summary"]["threshold"] == summ["thr"]
+    sub, flags2, summ2 = oracle.outlier_l2(V, s, d, lab, 4)
+    assert np.array_equal(o2["sub_labels"], sub), int((o2["sub_labels"] != sub).sum())
+    assert np.array_equal(o2["flags"], flags2)
+    assert o2["summary"]["n_groups"] == summ2["n_subgroups"]
+    assert o2["summary"]["n_communities_flagged"] == summ2["n_communities_flagged"]
+    for h, dv in ((o1, d1), (o2, d2)):
+        assert dv["summary"] == h["summary"]
+        assert np.array_equal(dv["size"].cpu().numpy(), h["size"])
+        assert np.array_equal(dv["incident"].cpu().numpy(), h["incident"])
+        assert np.array_equal(dv["flags"].cpu().numpy(), h["flags"])
+    assert np.array_equal(d2["sub_labels"].cpu().numpy(), o2["sub_labels"])
 
 
 def test_dropin_graphframe_r9(gfa, golden):

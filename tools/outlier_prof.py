@@ -21,9 +21,14 @@ print(f"build {1e3 * (time.perf_counter() - t0):.1f} ms", flush=True)
 del src, dst
 torch.cuda.empty_cache()
 lab = g.run(10)
-for mode in ("L1", "L1", "L2", "L2"):
+dlab = torch.from_numpy(lab).cuda()
+for mode, labels_in, form in (("L1", lab, "host"), ("L1", lab, "host"), ("L1", dlab, "device"),
+                              ("L1", dlab, "device"), ("L2", lab, "host"), ("L2", lab, "host"),
+                              ("L2", dlab, "device"), ("L2", dlab, "device")):
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r = g.outlier(lab, mode, sub_iter=5)
-    print(f"{mode} {1e3 * (time.perf_counter() - t0):.1f} ms flagged {int(r['flags'].sum())} "
+    r = g.outlier(labels_in, mode, sub_iter=5)
+    torch.cuda.synchronize()
+    print(f"{mode} {form} {1e3 * (time.perf_counter() - t0):.1f} ms flagged {int(r['flags'].sum())} "
           f"groups {r['summary']['n_groups']}", flush=True)
 g.close()
