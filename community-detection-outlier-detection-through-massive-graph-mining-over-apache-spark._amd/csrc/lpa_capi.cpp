@@ -81,7 +81,7 @@ void destroy(lpa_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   void* bufs[] = {g->rp,   g->col,   g->new_of, g->old_of, g->deg,   g->lab[0], g->lab[1],
-                  g->segs, g->e_src,  g->e_dst, g->de_keys, g->de_t, g->de_ts, g->de_out_off, g->de_in_off, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
+                  g->segs, g->e_src,  g->e_dst, g->gsend, g->gbm, g->xpair, g->gcounts, g->dsend, g->drecv, g->dcount, g->de_keys, g->de_t, g->de_ts, g->de_out_off, g->de_in_off, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
                   g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
@@ -563,6 +563,7 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->device_bytes = g->device_bytes;
   info->exchanges_full = g->n_exch_full;
   info->exchanges_delta = g->n_exch_delta;
+  info->exchanges_giant = g->n_exch_giant;
   return LPA_OK;
 }
 

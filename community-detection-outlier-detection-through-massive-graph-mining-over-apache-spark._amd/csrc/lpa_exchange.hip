@@ -11,7 +11,17 @@
 //          superstep 4+), so the exchange shrinks by ~2 orders of magnitude.
 //          Chosen when the largest delta is <= slice / 4 (its bytes <= 1/2 of the
 //          full slice).
-// Both give the identical full label vector, so the mode never affects labels.
+//   giant  (round 4) the giant label G (k_giant_pick of the current vector, the same on
+//          every rank) carries most of the new labels once LPA collapses: each rank
+//          sends the bitmap (label == G) of its slice (1/32 of the slice's bytes) and
+//          its CHANGED non-G labels as (slot, label) entries; a receiver writes G where
+//          the bit is set, keeps its current label elsewhere, then applies the entries.
+//          R-MAT (oracle, scale 22): superstep 2 1.7 B per vertex instead of 4 (full),
+//          superstep 3 0.16 instead of 1.6 (delta); Chung-Lu superstep 3 0.4 instead of 4.
+// Each superstep after the first allgathers one (delta, giant) count pair per rank and
+// the host takes the form of fewest bytes among those that fit (delta and giant entries
+// <= slice / 4 per rank).  All give the identical full label vector, so the mode never
+// affects labels.
 //
 // Completing the next-label buffer Ln after a delta exchange.  Ln (the ping-pong
 // partner of the current vector Lc = L_t) still holds L_{t-1} outside the own
@@ -20,6 +30,9 @@
 // the vector; otherwise the other slices are first copied from Lc.  The gathered
 // E_{t+1} is also the list of changed vertices, so the al[] refresh takes its
 // position chunks from it instead of diffing the whole vector.
+#include <algorithm>
+#include <climits>
+
 #include "lpa_internal.h"
 
 namespace lpa {
@@ -59,6 +72,87 @@ __global__ __launch_bounds__(256) void k_delta_compact(const int32_t* __restrict
       dsend[pos] = ((u64)(uint32_t)i << 32) | (u64)(uint32_t)nv;
     }
     __syncthreads();  // wsum / base_s reused by the next tile
+  }
+}
+
+// this rank's changed owned slots -> dsend (slot << 32 | label), count xpair[0]; the
+// changed ones whose new label is not G -> gsend, count xpair[1]; bit i of the slice's
+// bitmap = (new label == G).  One pass, block-aggregated counts (one atomic per block
+// and list).  The slice is a multiple of 64 slots: a wave owns whole bitmap words.
+__global__ __launch_bounds__(256) void k_exch_compact(const int32_t* __restrict__ Lc_own,
+                                                      const int32_t* __restrict__ Ln_own, int64_t slice,
+                                                      const int32_t* __restrict__ gword,
+                                                      u64* __restrict__ dsend, u64* __restrict__ gsend,
+                                                      unsigned long long* __restrict__ xpair,
+                                                      unsigned long long* __restrict__ bm_own) {
+  __shared__ int wsum[2][4];
+  __shared__ unsigned long long base_s[2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int32_t G = gword[0];
+  for (int64_t i0 = (int64_t)blockIdx.x * 256; i0 < slice; i0 += (int64_t)gridDim.x * 256) {
+    const int64_t i = i0 + threadIdx.x;
+    int32_t nv = 0;
+    bool chg = false, isg = false;
+    if (i < slice) {
+      nv = Ln_own[i];
+      chg = nv != Lc_own[i];
+      isg = nv == G;
+    }
+    const bool ng = chg && !isg;
+    const u64 m = __ballot(chg), mg = __ballot(ng), mb = __ballot(isg);
+    if (lane == 0) {
+      wsum[0][w] = __popcll(m);
+      wsum[1][w] = __popcll(mg);
+      if (i < slice) bm_own[i >> 6] = mb;
+    }
+    __syncthreads();
+    int before = 0, tot = 0, gbefore = 0, gtot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k < w) before += wsum[0][k], gbefore += wsum[1][k];
+      tot += wsum[0][k];
+      gtot += wsum[1][k];
+    }
+    if (threadIdx.x == 0) {
+      if (tot) base_s[0] = atomicAdd(&xpair[0], (unsigned long long)tot);
+      if (gtot) base_s[1] = atomicAdd(&xpair[1], (unsigned long long)gtot);
+    }
+    __syncthreads();
+    const u64 e = ((u64)(uint32_t)i << 32) | (u64)(uint32_t)nv;
+    const u64 lt = (1ull << lane) - 1ull;
+    if (chg) dsend[base_s[0] + before + __popcll(m & lt)] = e;
+    if (ng) gsend[base_s[1] + gbefore + __popcll(mg & lt)] = e;
+    __syncthreads();  // wsum / base_s reused by the next tile
+  }
+}
+
+// the gathered (delta, giant) count pairs -> the delta protocol's per-rank counts (its
+// receive buffer) and the giant counts
+__global__ void k_split_counts(const unsigned long long* __restrict__ pairs, int P,
+                               unsigned long long* __restrict__ dcounts, unsigned long long* __restrict__ gcounts) {
+  const int r = threadIdx.x;
+  if (r < P) {
+    dcounts[r] = pairs[2 * r];
+    gcounts[r] = pairs[2 * r + 1];
+  }
+}
+
+// Ln outside the own slice after a giant exchange: G where the sender's bit is set, the
+// current label elsewhere (the changed non-G entries are applied next); one bitmap word
+// per 64 slots, int4 stores
+__global__ void k_giant_apply(const int4* __restrict__ Lc, int4* __restrict__ Ln,
+                              const unsigned long long* __restrict__ bm, int64_t n4, int64_t own4_begin,
+                              int64_t own4_end, const int32_t* __restrict__ gword) {
+  const int32_t G = gword[0];
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    if (q >= own4_begin && q < own4_end) continue;
+    const u32 b = (u32)(bm[q >> 4] >> ((q & 15) * 4)) & 0xFu;
+    int4 v = Lc[q];
+    if (b & 1u) v.x = G;
+    if (b & 2u) v.y = G;
+    if (b & 4u) v.z = G;
+    if (b & 8u) v.w = G;
+    Ln[q] = v;
   }
 }
 
@@ -147,7 +241,11 @@ int exchange_alloc(lpa_graph* g) {
   LPA_TRY(dev_alloc(g, (void**)&g->dsend, sizeof(u64) * g->slice));
   LPA_TRY(dev_alloc(g, (void**)&g->drecv, sizeof(u64) * g->dcap * P * 2));
   LPA_TRY(dev_alloc(g, (void**)&g->dcount, sizeof(unsigned long long) * (1 + 2 * P)));
-  LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * P, hipHostMallocDefault));
+  LPA_TRY(dev_alloc(g, (void**)&g->gsend, sizeof(u64) * g->slice));
+  LPA_TRY(dev_alloc(g, (void**)&g->gbm, sizeof(unsigned long long) * (g->slice / 64) * P));
+  LPA_TRY(dev_alloc(g, (void**)&g->xpair, sizeof(unsigned long long) * (2 + 2 * P)));
+  LPA_TRY(dev_alloc(g, (void**)&g->gcounts, sizeof(unsigned long long) * P));
+  LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * 2 * P, hipHostMallocDefault));
   g->dbuf = 0;
   g->prev_delta_ok = false;
   return LPA_OK;
@@ -209,30 +307,62 @@ int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t 
 // In-library exchange of one superstep (P > 1, RCCL communicator or loopback group):
 // Lown = Ln + own_begin holds the new owned labels; on return Ln holds the full new
 // label vector.  *changes_listed: the refresh's position chunks were queued from the delta.
-int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed) {
+// first: the superstep right after L0 (every label changes: full, no count round trip).
+int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first, bool* changes_listed) {
   hipStream_t s = g->stream;
   int32_t* Lown = Ln + g->own_begin;
+  const int P = g->nranks;
+  const int64_t S = g->slice, wpr = S / 64;   // bitmap words per rank
   *changes_listed = false;
-  if (!dense) {
-    LPA_TRY(exchange_compact(g, Lc, Ln));
-    unsigned long long* counts = exchange_recv_counts(g);
-    LPA_TRY(coll_allgather(g, g->dcount, counts, 1, 8, s));
-    LPA_HIP(hipMemcpyAsync(g->h_dcounts, counts, sizeof(unsigned long long) * g->nranks,
-                           hipMemcpyDeviceToHost, s));
+  if (!first) {
+    LPA_HIP(hipMemsetAsync(g->xpair, 0, 2 * sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_exch_compact, dim3(grid_of(S, 4096)), dim3(256), 0, s, Lc + g->own_begin, Lown, S,
+                       g->gword, g->dsend, g->gsend, g->xpair, g->gbm + (int64_t)g->rank * wpr);
+    LPA_HIP(hipGetLastError());
+    LPA_TRY(coll_allgather(g, g->xpair, g->xpair + 2, 2, 8, s));
+    hipLaunchKernelGGL(k_split_counts, dim3(1), dim3(64 * ((P + 63) / 64)), 0, s, g->xpair + 2, P,
+                       exchange_recv_counts(g), g->gcounts);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipMemcpyAsync(g->h_dcounts, g->xpair + 2, sizeof(unsigned long long) * 2 * P, hipMemcpyDeviceToHost, s));
     LPA_HIP(hipStreamSynchronize(s));
-    int64_t cap = 0;
-    for (int k = 0; k < g->nranks; ++k)
-      if ((int64_t)g->h_dcounts[k] > cap) cap = (int64_t)g->h_dcounts[k];
-    if (cap <= g->dcap) {
-      if (cap > 0) LPA_TRY(coll_allgather(g, g->dsend, exchange_recv_buf(g), (size_t)cap, 8, s));
-      g->last_exchange_delta = cap;
+    int64_t capd = 0, capg = 0;
+    for (int k = 0; k < P; ++k) {
+      capd = std::max(capd, (int64_t)g->h_dcounts[2 * k]);
+      capg = std::max(capg, (int64_t)g->h_dcounts[2 * k + 1]);
+    }
+    // bytes every rank receives per form (the full slice otherwise)
+    const int64_t full_b = 4 * S;
+    const int64_t delta_b = capd <= g->dcap ? 8 * capd : INT64_MAX;
+    const int64_t giant_b = capg <= g->dcap ? 8 * wpr + 8 * capg : INT64_MAX;
+    if (delta_b <= giant_b && delta_b < full_b) {
+      if (capd > 0) LPA_TRY(coll_allgather(g, g->dsend, exchange_recv_buf(g), (size_t)capd, 8, s));
+      g->last_exchange_delta = capd;
       ++g->n_exch_delta;
       *changes_listed = true;
-      return exchange_finish_delta(g, Lc, Ln, cap, g->par);
+      return exchange_finish_delta(g, Lc, Ln, capd, g->par);
+    }
+    if (giant_b < full_b) {
+      // in place: rank r's bitmap words at gbm + r * wpr
+      LPA_TRY(coll_allgather(g, g->gbm + (int64_t)g->rank * wpr, g->gbm, (size_t)wpr, 8, s));
+      u64* ent = exchange_recv_buf(g);
+      if (capg > 0) LPA_TRY(coll_allgather(g, g->gsend, ent, (size_t)capg, 8, s));
+      const int64_t n4 = g->vpad / 4;
+      hipLaunchKernelGGL(k_giant_apply, dim3(grid_of(n4, 8192)), dim3(256), 0, s, (const int4*)Lc, (int4*)Ln,
+                         g->gbm, n4, g->own_begin / 4, (g->own_begin + S) / 4, g->gword);
+      LPA_HIP(hipGetLastError());
+      if (capg > 0) {
+        hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(capg * P, 8192)), dim3(256), 0, s, ent, g->gcounts, capg,
+                           P, g->rank, S, Ln);
+        LPA_HIP(hipGetLastError());
+      }
+      g->last_exchange_delta = -2;
+      ++g->n_exch_giant;
+      g->prev_delta_ok = false;   // Ln is the full new vector; no delta chain to continue
+      return LPA_OK;
     }
   }
   // full: in-place allgather of the owned slices (rank r's slice at Ln + r * slice)
-  LPA_TRY(coll_allgather(g, Lown, Ln, (size_t)g->slice, 4, s));
+  LPA_TRY(coll_allgather(g, Lown, Ln, (size_t)S, 4, s));
   g->last_exchange_delta = -1;
   ++g->n_exch_full;
   g->prev_delta_ok = false;

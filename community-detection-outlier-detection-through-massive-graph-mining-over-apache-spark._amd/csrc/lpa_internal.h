@@ -234,7 +234,14 @@ struct lpa_graph {
   lpa::u64* dsend = nullptr;                 // [slice] this rank's (slot << 32 | label)
   lpa::u64* drecv = nullptr;                 // [2][nranks * dcap] gathered deltas
   unsigned long long* dcount = nullptr;      // [1 + 2 nranks] own count, then every rank's (x2)
-  unsigned long long* h_dcounts = nullptr;   // [nranks] pinned host copy
+  unsigned long long* h_dcounts = nullptr;   // [2 nranks] pinned host copy of the count pairs
+  // giant-compressed exchange (lpa_exchange.hip): the giant-label bitmap of every slice
+  // ([nranks][slice / 64] words, own slice in place) and the changed non-G entries
+  lpa::u64* gsend = nullptr;                 // [slice] this rank's changed non-G (slot << 32 | label)
+  unsigned long long* gbm = nullptr;         // [nranks * slice / 64] bit = (label == G)
+  unsigned long long* xpair = nullptr;       // [2 + 2 nranks] own (delta, giant) counts, then every rank's
+  unsigned long long* gcounts = nullptr;     // [nranks] every rank's giant-entry count
+  int64_t n_exch_giant = 0;                  // exchanges done in the giant-compressed form
   int64_t dcap = 0;                          // delta entries per rank (slice / 4)
   int64_t last_exchange_delta = -1;          // entries per rank of the last exchange (-1 full)
   int dbuf = 0;                              // receive buffer of the next delta (ping-pong)
@@ -335,7 +342,7 @@ int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln);
 lpa::u64* exchange_recv_buf(lpa_graph* g);
 unsigned long long* exchange_recv_counts(lpa_graph* g);
 int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par);
-int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool dense, bool* changes_listed);
+int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first, bool* changes_listed);
 int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par);
 
 // outlier (lpa_outlier.hip)

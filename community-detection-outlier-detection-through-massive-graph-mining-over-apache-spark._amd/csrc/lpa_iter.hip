@@ -2878,7 +2878,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv], s));
     bool changes_listed = false;
     if (exchanges(g) && has_collective(g))
-      LPA_TRY(exchange_collective(g, Lc, Ln, g->since_reset < kDenseSupersteps, &changes_listed));
+      LPA_TRY(exchange_collective(g, Lc, Ln, g->since_reset == 0, &changes_listed));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 1], s));
     // P > 1 without a communicator: the caller completes the superstep with
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta

@@ -102,8 +102,11 @@ def _partitioned_every_superstep(gfa, cfg, P, what):
             for t in range(MAX_ITER):
                 assert bad[r][t] == 0, f"{what} P={P} rank {r} superstep {t + 1}: {bad[r][t]} labels differ"
         infos = [g.info() for g in ranks]
-        # label-dense supersteps exchange full slices, converging ones changed-label deltas
-        assert all(i["exchanges_full"] >= 2 and i["exchanges_delta"] >= 2 for i in infos), infos
+        # full slices after L0, giant-compressed (bitmap + changed non-giant labels) once
+        # G dominates, changed-label deltas when converged: one exchange per superstep
+        assert all(i["exchanges_full"] >= 1 and i["exchanges_delta"] >= 2 and i["exchanges_giant"] >= 1
+                   for i in infos), infos
+        assert all(i["exchanges_full"] + i["exchanges_delta"] + i["exchanges_giant"] == MAX_ITER for i in infos)
         runs = gfa.run_ranks(ranks, lambda r, g: int((g.run(MAX_ITER) != cfg.hist[MAX_ITER - 1]).sum()))
         assert runs == [0] * P, f"{what} P={P} lpa_run(10) mismatches per rank: {runs}"
     finally:

@@ -3,9 +3,10 @@
 Two RCCL ranks cannot share one device, so the distributed path is driven as a
 ONE-rank job: lpa_comm_unique_id -> lpa_graph_create_dist(nranks=1, comm_id) runs
 ncclCommInitRank, and every superstep goes through exchange_collective exactly as
-at P > 1 (full ncclAllGather in place in the label-dense supersteps, then the delta
-protocol: counts allgathered and read on the host, the entries allgathered, the
-refresh queued from the gathered change list).  Bit-exact against the oracle per
+at P > 1 (full ncclAllGather in place after L0, then per superstep the (delta, giant)
+count pairs allgathered and read on the host and the smaller form sent: the delta
+entries, whose gathered change list queues the refresh, or the giant-label bitmap
+plus the changed non-giant entries).  Bit-exact against the oracle per
 superstep (reference: Graphframes.py:81 labelPropagation, the Spark shuffle
 behind aggregateMessages replaced by the allgather).
 """
@@ -51,8 +52,13 @@ def test_rccl_one_rank_every_superstep(gfa, oracle, graph):
             bad = int((g.labels() != hist[t]).sum())
             assert bad == 0, f"{graph} superstep {t + 1}: {bad} labels differ"
         info = g.info()
-        # both transport branches ran: in-place full allgathers after L0, then deltas
-        assert info["exchanges_full"] >= 2 and info["exchanges_delta"] >= 2, info
+        # every transport branch ran: the in-place full allgather after L0, then deltas,
+        # and (R-MAT, once its giant label dominates) the giant-compressed form with its
+        # bitmap allgather; one exchange per superstep
+        assert info["exchanges_full"] >= 1 and info["exchanges_delta"] >= 2, info
+        assert info["exchanges_full"] + info["exchanges_delta"] + info["exchanges_giant"] == 10, info
+        if graph == "rmat16":
+            assert info["exchanges_giant"] >= 1, info
         # lpa_run from reset (captured tally graphs replayed) twice: the same answer
         for _ in range(2):
             assert np.array_equal(g.run(10), hist[9])
