@@ -352,7 +352,7 @@ __global__ void k_init_labels(const int32_t* __restrict__ old_of, int64_t n, int
 // ---- the outlier stage's L2 sub-graph (build_graph_l2) ----
 // intra-community marks over the parent's distinct edges in (s, d) order ...
 __global__ void k_l2_mark_out(const u64* __restrict__ ek, int64_t md, const int32_t* __restrict__ L,
-                              int32_t* __restrict__ mark) {
+                              uint8_t* __restrict__ mark) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < md; i += (int64_t)gridDim.x * blockDim.x) {
     const u64 k = ek[i];
     mark[i] = L[(int32_t)(k >> 32)] == L[(int32_t)(u32)k] ? 1 : 0;
@@ -360,14 +360,14 @@ __global__ void k_l2_mark_out(const u64* __restrict__ ek, int64_t md, const int3
 }
 // ... and in (d, s) order (de_t: d << 32 | index, de_ts: s)
 __global__ void k_l2_mark_in(const u64* __restrict__ et, const uint32_t* __restrict__ ets, int64_t md,
-                             const int32_t* __restrict__ L, int32_t* __restrict__ mark) {
+                             const int32_t* __restrict__ L, uint8_t* __restrict__ mark) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < md; j += (int64_t)gridDim.x * blockDim.x)
     mark[j] = L[(int32_t)(et[j] >> 32)] == L[(int32_t)ets[j]] ? 1 : 0;
 }
 // degrees from segment lengths: v's intra out-edges are the marks of its run in the
 // (s, d) order, its in-edges those of its run in the (d, s) order
 __global__ void k_l2_degree(const int64_t* __restrict__ out_off, const int64_t* __restrict__ in_off,
-                            const int64_t* __restrict__ pos_out, const int64_t* __restrict__ pos_in, int64_t V,
+                            const uint32_t* __restrict__ pos_out, const uint32_t* __restrict__ pos_in, int64_t V,
                             int32_t* __restrict__ deg, int32_t* __restrict__ dout) {
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += (int64_t)gridDim.x * blockDim.x) {
     const int32_t o = (int32_t)(pos_out[out_off[v + 1]] - pos_out[out_off[v]]);
@@ -377,40 +377,43 @@ __global__ void k_l2_degree(const int64_t* __restrict__ out_off, const int64_t* 
   }
 }
 // arcs of row s from its intra out-edges, in place: row s's first dout[s] positions
-__global__ void k_l2_emit_out(const u64* __restrict__ ek, int64_t md, const int32_t* __restrict__ mark,
-                              const int64_t* __restrict__ pos_out, const int64_t* __restrict__ out_off,
+// (rows are the runs of the (s, d) order, so the per-row terms are cached loads); the
+// arc's row and position are kept per edge (pinfo) for its twin in k_l2_emit_in
+__global__ void k_l2_emit_out(const u64* __restrict__ ek, int64_t md, const uint8_t* __restrict__ mark,
+                              const uint32_t* __restrict__ pos_out, const int64_t* __restrict__ out_off,
                               const int32_t* __restrict__ new_of, const int64_t* __restrict__ rp,
-                              int32_t* __restrict__ col, int32_t* __restrict__ crow) {
+                              int32_t* __restrict__ col, int32_t* __restrict__ crow, u64* __restrict__ pinfo) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < md; i += (int64_t)gridDim.x * blockDim.x) {
     if (!mark[i]) continue;
     const u64 k = ek[i];
     const int32_t sv = (int32_t)(k >> 32), rs = new_of[sv];
-    const int64_t p = rp[rs] + (pos_out[i] - pos_out[out_off[sv]]);
+    const int64_t p = rp[rs] + (int64_t)(pos_out[i] - pos_out[out_off[sv]]);
     col[p] = new_of[(int32_t)(u32)k];
     crow[p] = rs;
+    pinfo[i] = ((u64)(u32)rs << 32) | (u64)(u32)p;
   }
 }
 // arcs of row d from its intra in-edges, after its out-edges; each edge's two arcs are
 // each other's CSC entry: column u's positions are the twins of row u's arcs, so the
-// CSC shares the row offsets (cptr = rp) and cpos[p] = q, cpos[q] = p
-__global__ void k_l2_emit_in(const u64* __restrict__ et, const uint32_t* __restrict__ ets, int64_t md,
-                             const int32_t* __restrict__ mark, const int64_t* __restrict__ pos_in,
-                             const int64_t* __restrict__ in_off, const int64_t* __restrict__ pos_out,
-                             const int64_t* __restrict__ out_off, const int32_t* __restrict__ dout,
-                             const int32_t* __restrict__ new_of, const int64_t* __restrict__ rp,
+// CSC shares the row offsets (cptr = rp) and cpos[p] = q, cpos[q] = p.  Per edge one
+// random 8-B read (the out-arc's row and position) and one random 4-B write (cpos[p]).
+__global__ void k_l2_emit_in(const u64* __restrict__ et, int64_t md, const uint8_t* __restrict__ mark,
+                             const uint32_t* __restrict__ pos_in, const int64_t* __restrict__ in_off,
+                             const int32_t* __restrict__ dout, const int32_t* __restrict__ new_of,
+                             const int64_t* __restrict__ rp, const u64* __restrict__ pinfo,
                              int32_t* __restrict__ col, int32_t* __restrict__ crow, uint32_t* __restrict__ cpos) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < md; j += (int64_t)gridDim.x * blockDim.x) {
     if (!mark[j]) continue;
     const u64 k = et[j];
-    const int32_t dv = (int32_t)(k >> 32), sv = (int32_t)ets[j];
-    const int64_t i = (int64_t)(u32)k;
-    const int32_t rd = new_of[dv], rs = new_of[sv];
-    const int64_t q = rp[rd] + dout[dv] + (pos_in[j] - pos_in[in_off[dv]]);
-    const int64_t p = rp[rs] + (pos_out[i] - pos_out[out_off[sv]]);
+    const int32_t dv = (int32_t)(k >> 32);
+    const u64 pi = pinfo[(u32)k];
+    const int32_t rd = new_of[dv], rs = (int32_t)(pi >> 32);
+    const uint32_t p = (uint32_t)pi;
+    const int64_t q = rp[rd] + dout[dv] + (int64_t)(pos_in[j] - pos_in[in_off[dv]]);
     col[q] = rs;
     crow[q] = rd;
     cpos[p] = (uint32_t)q;
-    cpos[q] = (uint32_t)p;
+    cpos[q] = p;
   }
 }
 
@@ -473,7 +476,7 @@ int vertex_order(lpa_graph* g, int32_t V, int64_t m, bool locality) {
     // 16 K ids -> id order inside the bins (the neighbour-rank order below would scatter
     // it); LPA_LOCALITY=3 / 4 skip the test
     bool id_local = false;
-    if (locality && m > 0 && V < (1 << 28) && g->locality <= 2 && V > (1 << 16)) {
+    if (locality && g->id_order_test && m > 0 && V < (1 << 28) && g->locality <= 2 && V > (1 << 16)) {
       unsigned long long* d_cnt = nullptr;
       LPA_TRY(scratch_alloc(g, (void**)&d_cnt, sizeof(unsigned long long)));
       LPA_HIP(hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long), s));
@@ -828,7 +831,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
 // segment-length differences (no per-vertex atomics), the degree-ranked slot order (a
 // sort of V keys), then every arc written at its final position, with its CSC twin.
 // Rows keep their columns in run order (cols_sorted = false: no column-run superstep).
-int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L) {
+int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L, const uint8_t* mo_pre) {
   hipStream_t s = g->stream;
   const int32_t V = (int32_t)parent->V;
   const int64_t md = parent->de_n;
@@ -839,22 +842,24 @@ int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L) {
   g->own_begin = 0;
   g->cols_sorted = false;
   const int64_t S = g->slice;
-  int32_t *mo = nullptr, *mi = nullptr, *dout = nullptr, *d_max = nullptr;
-  int64_t *pos_out = nullptr, *pos_in = nullptr;
-  LPA_TRY(scratch_alloc(g, (void**)&mo, sizeof(int32_t) * (md > 0 ? md : 1)));
-  LPA_TRY(scratch_alloc(g, (void**)&mi, sizeof(int32_t) * (md > 0 ? md : 1)));
-  LPA_TRY(scratch_alloc(g, (void**)&pos_out, sizeof(int64_t) * (md + 1)));
-  LPA_TRY(scratch_alloc(g, (void**)&pos_in, sizeof(int64_t) * (md + 1)));
+  uint8_t *mo = nullptr, *mi = nullptr;
+  int32_t *dout = nullptr, *d_max = nullptr;
+  uint32_t *pos_out = nullptr, *pos_in = nullptr;
+  if (!mo_pre) LPA_TRY(scratch_alloc(g, (void**)&mo, md > 0 ? md : 1));
+  LPA_TRY(scratch_alloc(g, (void**)&mi, md > 0 ? md : 1));
+  LPA_TRY(scratch_alloc(g, (void**)&pos_out, sizeof(uint32_t) * (md + 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&pos_in, sizeof(uint32_t) * (md + 1)));
   LPA_TRY(scratch_alloc(g, (void**)&dout, sizeof(int32_t) * (V > 0 ? V : 1)));
   LPA_TRY(scratch_alloc(g, (void**)&d_max, sizeof(int32_t)));
   LPA_TRY(dev_alloc(g, (void**)&g->deg, sizeof(int32_t) * (V > 0 ? V : 1)));
+  const uint8_t* mo_c = mo_pre ? mo_pre : mo;
   if (md > 0) {
-    hipLaunchKernelGGL(k_l2_mark_out, dim3(grid_for(md)), dim3(256), 0, s, parent->de_keys, md, L, mo);
+    if (!mo_pre) hipLaunchKernelGGL(k_l2_mark_out, dim3(grid_for(md)), dim3(256), 0, s, parent->de_keys, md, L, mo);
     hipLaunchKernelGGL(k_l2_mark_in, dim3(grid_for(md)), dim3(256), 0, s, parent->de_t, parent->de_ts, md, L, mi);
     LPA_HIP(hipGetLastError());
   }
-  LPA_TRY(exclusive_scan_i32_i64(mo, pos_out, md, s));
-  LPA_TRY(exclusive_scan_i32_i64(mi, pos_in, md, s));
+  LPA_TRY(exclusive_scan_u8_u32(mo_c, pos_out, md, s));
+  LPA_TRY(exclusive_scan_u8_u32(mi, pos_in, md, s));
   LPA_HIP(hipMemsetAsync(d_max, 0, sizeof(int32_t), s));
   if (V > 0) {
     hipLaunchKernelGGL(k_l2_degree, dim3(grid_for(V)), dim3(256), 0, s, parent->de_out_off, parent->de_in_off,
@@ -863,10 +868,11 @@ int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L) {
                        (int64_t)V, d_max);
     LPA_HIP(hipGetLastError());
   }
-  int64_t m2 = 0;
-  LPA_HIP(hipMemcpyAsync(&m2, pos_out + md, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  uint32_t m2u = 0;
+  LPA_HIP(hipMemcpyAsync(&m2u, pos_out + md, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   LPA_HIP(hipMemcpyAsync(&g->max_degree, d_max, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   LPA_HIP(hipStreamSynchronize(s));
+  const int64_t m2 = (int64_t)m2u;
   g->m = m2;
   scratch_free(g, d_max);
 
@@ -892,14 +898,16 @@ int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L) {
   LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
   LPA_HIP(hipMemcpyAsync(g->cptr, g->rp, sizeof(int64_t) * (S + 1), hipMemcpyDeviceToDevice, s));
   if (md > 0) {
-    hipLaunchKernelGGL(k_l2_emit_out, dim3(grid_for(md)), dim3(256), 0, s, parent->de_keys, md, mo, pos_out,
-                       parent->de_out_off, g->new_of, g->rp, g->col, g->crow);
-    hipLaunchKernelGGL(k_l2_emit_in, dim3(grid_for(md)), dim3(256), 0, s, parent->de_t, parent->de_ts, md, mi,
-                       pos_in, parent->de_in_off, pos_out, parent->de_out_off, dout, g->new_of, g->rp, g->col,
-                       g->crow, g->cpos);
+    u64* pinfo = nullptr;
+    LPA_TRY(scratch_alloc(g, (void**)&pinfo, sizeof(u64) * md));
+    hipLaunchKernelGGL(k_l2_emit_out, dim3(grid_for(md)), dim3(256), 0, s, parent->de_keys, md, mo_c, pos_out,
+                       parent->de_out_off, g->new_of, g->rp, g->col, g->crow, pinfo);
+    hipLaunchKernelGGL(k_l2_emit_in, dim3(grid_for(md)), dim3(256), 0, s, parent->de_t, md, mi, pos_in,
+                       parent->de_in_off, dout, g->new_of, g->rp, pinfo, g->col, g->crow, g->cpos);
     LPA_HIP(hipGetLastError());
+    scratch_free(g, pinfo);
   }
-  scratch_free(g, mo);
+  if (mo) scratch_free(g, mo);
   scratch_free(g, mi);
   scratch_free(g, pos_out);
   scratch_free(g, pos_in);

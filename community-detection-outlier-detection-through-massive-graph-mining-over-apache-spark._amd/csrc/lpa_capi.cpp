@@ -141,7 +141,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
                   int64_t m, int32_t V, uint32_t flags, int32_t rank, int32_t nranks,
                   const uint8_t* comm_id, Loopback* loop, lpa_graph** out,
                   const lpa_graph* borrow = nullptr, const lpa_graph* l2_parent = nullptr,
-                  const int32_t* l2_labels = nullptr) {
+                  const int32_t* l2_labels = nullptr, const uint8_t* l2_marks = nullptr) {
   if (!out) {
     set_error("out must be non-null");
     return LPA_EINVAL;
@@ -163,6 +163,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
   if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
   if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
+  if (const char* f = getenv("LPA_ID_ORDER")) g->id_order_test = atoi(f);
+  if (const char* f = getenv("LPA_REBUILD_HYBRID")) g->rebuild_hybrid = atoi(f);
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
@@ -225,7 +227,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
       return LPA_ERCCL;
     }
   }
-  int rc = l2_parent ? build_graph_l2(g, l2_parent, l2_labels) : build_graph(g, src, dst, m, V, flags);
+  int rc = l2_parent ? build_graph_l2(g, l2_parent, l2_labels, l2_marks) : build_graph(g, src, dst, m, V, flags);
   if (rc == LPA_OK) rc = exchange_alloc(g);
   if (rc != LPA_OK) {
     destroy(g);
@@ -237,9 +239,9 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
 
 // the outlier stage's L2 sub-graph of `parent` under the community labels L (device,
 // dense ids): pooled, on the parent's stream, borrowing its aux streams
-int create_l2(const lpa_graph* parent, const int32_t* L, lpa_graph** out) {
+int create_l2(const lpa_graph* parent, const int32_t* L, const uint8_t* marks, lpa_graph** out) {
   return create_common(parent->device, parent->stream, nullptr, nullptr, 0, (int32_t)parent->V,
-                       kFlagNoLocality | kFlagPooled, 0, 1, nullptr, nullptr, out, parent, parent, L);
+                       kFlagNoLocality | kFlagPooled, 0, 1, nullptr, nullptr, out, parent, parent, L, marks);
 }
 
 }  // namespace lpa

@@ -221,6 +221,7 @@ struct lpa_graph {
   int64_t n_chunk_scan = 0;     // chunks below this belong to every multi-chunk column
   int32_t* chlist = nullptr;    // [vpad] changed one-chunk columns (count: counters[par][0])
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
+  int rebuild_hybrid = 1;                   // its hybrid labels + bits mode (LPA_REBUILD_HYBRID=0: A/B)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per
@@ -228,6 +229,7 @@ struct lpa_graph {
   hipGraphExec_t gexec[16] = {};
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
   bool id_order = false;                    // the input ids carry locality: id order inside the bins
+  int id_order_test = 1;                    // LPA_ID_ORDER=0: never take the id order (A/B)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
@@ -296,6 +298,8 @@ int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshift
 // exclusive scan of int32 input into int64 output (n + 1 entries: out[n] = total)
 int exclusive_scan_i32_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s);
 int exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
+// exclusive scan of 0/1 bytes into uint32 positions (n + 1 entries; the total < 2^32)
+int exclusive_scan_u8_u32(const uint8_t* in, uint32_t* out, int64_t n, hipStream_t s);
 int bits_for(uint64_t maxval);  // bits needed to represent maxval (0 -> 0)
 
 // build (lpa_build.hip)
@@ -305,7 +309,9 @@ int init_labels(lpa_graph* g);
 // the outlier stage's L2 sub-graph (P = 1, pooled handle g, V vertices) straight from the
 // parent's sorted distinct edge orders: E' = distinct (s, d) with L[s] == L[d], no sort
 // of arcs (lpa_build.hip)
-int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L);
+// mo (nullable): the intra marks of the parent's (s, d)-ordered distinct edges, when the
+// caller's incident-edge pass already computed them (k_incident<true>)
+int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L, const uint8_t* mo);
 int build_hub_tables(lpa_graph* g, const int32_t* deg_own);  // lpa_hub.hip
 // join = false: the forked bucket path's end is recorded in ev_join2[0] and the caller
 // joins it (main-stream work can be queued behind the mid tiers first)

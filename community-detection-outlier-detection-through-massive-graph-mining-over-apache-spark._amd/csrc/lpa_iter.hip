@@ -2050,7 +2050,7 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
                                                          int slice_lg, int hot_lg, int hb_lg,
                                                          const uint32_t* __restrict__ gbits, int64_t nbits,
                                                          int32_t* __restrict__ gword,
-                                                         unsigned long long* __restrict__ abits) {
+                                                         unsigned long long* __restrict__ abits, int allow_hyb) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   __shared__ u32 hot[kHotLabelsSingle];
   u32* s_cnt = &hot[kHotLabelsSingle - 1];   // beyond the bit words; labels mode refills it
@@ -2075,7 +2075,7 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
   // slots' LABELS in LDS, a cold column's bit from gbits, its label gathered only when
   // the bit is clear (Chung-Lu C5 superstep 2: G on ~40 % of the arcs, ~30 % of the cold
   // gathers become L2 / Infinity-Cache hits on the 5 MB bit array)
-  const bool hyb = !kRanked && !bits && 8 * (int64_t)*s_cnt >= nhb && nhb > 0;
+  const bool hyb = !kRanked && allow_hyb && !bits && 8 * (int64_t)*s_cnt >= nhb && nhb > 0;
   const int32_t G = gword[0];
   // bits / hybrid modes also write the arc giant bits (abits: bit i = al[i] == G, one
   // ballot per 64 arcs), which the next superstep's full tally settles rows from
@@ -2659,7 +2659,8 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     const int64_t nbits = (ranked && hb_lg == 0) ? 0 : g->vpad;
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
-                     g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits)
+                     g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \
+                     g->rebuild_hybrid)
     if (if_wanted) {
       if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
     } else {

@@ -25,7 +25,7 @@
 
 namespace lpa {
 
-int create_l2(const lpa_graph* parent, const int32_t* L, lpa_graph** out);
+int create_l2(const lpa_graph* parent, const int32_t* L, const uint8_t* marks, lpa_graph** out);
 void destroy(lpa_graph* g);
 
 namespace {
@@ -96,10 +96,12 @@ __global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ l
 
 // incident distinct edges per community, over the sorted edge keys (distinct =
 // first occurrences): +1 for L[s], +1 for L[d] when it differs
-// (ek: the distinct directed edges)
+// (ek: the distinct directed edges); kMark (L2): also the edge's intra-community mark,
+// the E' filter of the sub-graph build (the same two label reads)
+template <bool kMark>
 __global__ __launch_bounds__(256) void k_incident(const u64* __restrict__ ek, int64_t n,
                                                   const int32_t* __restrict__ L, int64_t nv,
-                                                  int32_t* __restrict__ inc) {
+                                                  int32_t* __restrict__ inc, uint8_t* __restrict__ mark) {
   __shared__ u32 bk[dev::kBhSlots];
   __shared__ int32_t bv[dev::kBhSlots];
   __shared__ int bsat;
@@ -115,6 +117,7 @@ __global__ __launch_bounds__(256) void k_incident(const u64* __restrict__ ek, in
       ld = (u32)L[(int32_t)(u32)k];
     }
     const u32 V = (u32)nv;   // out-of-range labels (reported by k_histogram) are skipped
+    if (kMark && a) mark[i] = ls == ld ? 1 : 0;
     bh.add1(inc, a && ls < V, ls, lane);
     bh.add1(inc, a && ld != ls && ld < V, ld, lane);
   }
@@ -569,8 +572,14 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
   LPA_TRY(distinct_edges(g));
   const u64* ek = g->de_keys;
   const int64_t md = g->de_n;   // distinct directed edges
+  uint8_t* intra = nullptr;     // L2: the E' marks of the distinct edges
+  if (mode == 2) LPA_TRY(sc.get(&intra, md));
   if (md > 0) {
-    hipLaunchKernelGGL(k_incident, dim3(grid_bh(md)), dim3(256), 0, s, ek, md, L, V, inc);
+    if (mode == 2)
+      hipLaunchKernelGGL(k_incident<true>, dim3(grid_bh(md)), dim3(256), 0, s, ek, md, L, V, inc, intra);
+    else
+      hipLaunchKernelGGL(k_incident<false>, dim3(grid_bh(md)), dim3(256), 0, s, ek, md, L, V, inc,
+                         (uint8_t*)nullptr);
     LPA_HIP(hipGetLastError());
   }
 
@@ -605,7 +614,7 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     LPA_TRY(transposed_edges(g));
     // second LPA on the induced simple subgraph (same device, same stream)
     lpa_graph* h = nullptr;
-    LPA_TRY(create_l2(g, L, &h));
+    LPA_TRY(create_l2(g, L, intra, &h));
     int rc = run_supersteps(h, sub_iter, nullptr);
     if (rc == LPA_OK) rc = gather_labels(h, sub);
     if (rc == LPA_OK && hipStreamSynchronize(s) != hipSuccess) rc = LPA_EHIP;

@@ -275,6 +275,10 @@ int exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s
   return scan_impl<int64_t, int64_t>(in, out, n, s);
 }
 
+int exclusive_scan_u8_u32(const uint8_t* in, uint32_t* out, int64_t n, hipStream_t s) {
+  return scan_impl<uint8_t, u32>(in, out, n, s);
+}
+
 int radix_sort_u64(u64* keys, u64* tmp, int64_t n, const int* shifts, int nshifts,
                    hipStream_t s) {
   if (n <= 1 || nshifts == 0) return LPA_OK;
