@@ -222,6 +222,7 @@ struct lpa_graph {
   int32_t* chlist = nullptr;    // [vpad] changed one-chunk columns (count: counters[par][0])
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int rebuild_hybrid = 1;                   // its hybrid labels + bits mode (LPA_REBUILD_HYBRID=0: A/B)
+  int rebuild_sc1 = 0;                      // its al[] stores sc1 instead of non-temporal (LPA_REBUILD_SC1)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per

@@ -1885,13 +1885,21 @@ __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __
   }
 }
 
+// al[] store of the rebuild: non-temporal (the line stays in the XCD's L2), or sc1 (the
+// line leaves L2: the 4 B/arc store stream then evicts none of the label lines the
+// gathers hit; MI355X_MICROARCH.md, store flavours)
+__device__ __forceinline__ void st_arc(int32_t* p, int32_t v, bool sc1) {
+  if (sc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __builtin_nontemporal_store(v, p);
+}
+
 // al[i] = lab(col[i]) over every arc by the calling grid (one wave per 512-arc batch,
 // grid-stride); bits: also the arc giant bits (abits: bit i = al[i] == G, one ballot
 // per 64 arcs), which the next superstep's full tally settles rows from (k_settle_*).
 template <typename Lab>
 __device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, const int32_t* __restrict__ col,
                                                int64_t arcs, int32_t* __restrict__ al,
-                                               unsigned long long* __restrict__ abits) {
+                                               unsigned long long* __restrict__ abits, bool sc1) {
   // lane-consecutive arcs: one gather instruction covers 64 consecutive arcs of
   // a row, whose sorted columns often share lines (hub rows) -> fewer L2 requests.
   // Full 512-arc batches are software-pipelined: the next batch's column loads are in
@@ -1916,7 +1924,7 @@ __device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, co
 #pragma unroll
     for (int k = 0; k < 8; ++k) r[k] = lab(c[k]);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
+    for (int k = 0; k < 8; ++k) st_arc(al + base + k * 64 + lane, r[k], sc1);
     if (bits) {
       unsigned long long mine = 0ull;
 #pragma unroll
@@ -1952,7 +1960,7 @@ __device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, co
 template <typename P1, typename P2>
 __device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits, const int32_t* __restrict__ col,
                                              int64_t arcs, int32_t* __restrict__ al,
-                                             unsigned long long* __restrict__ abits) {
+                                             unsigned long long* __restrict__ abits, bool sc1) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t step = nw * 512;
@@ -1978,7 +1986,7 @@ __device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits,
   };
   auto S = [&](const int32_t (&r)[8], int64_t b) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + b + k * 64 + lane);
+    for (int k = 0; k < 8; ++k) st_arc(al + b + k * 64 + lane, r[k], sc1);
     if (bits) {
       unsigned long long mine = 0ull;
 #pragma unroll
@@ -2050,7 +2058,8 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
                                                          int slice_lg, int hot_lg, int hb_lg,
                                                          const uint32_t* __restrict__ gbits, int64_t nbits,
                                                          int32_t* __restrict__ gword,
-                                                         unsigned long long* __restrict__ abits, int allow_hyb) {
+                                                         unsigned long long* __restrict__ abits, int allow_hyb,
+                                                         int store_sc1) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   __shared__ u32 hot[kHotLabelsSingle];
   u32* s_cnt = &hot[kHotLabelsSingle - 1];   // beyond the bit words; labels mode refills it
@@ -2108,7 +2117,7 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
     }
   };
   if constexpr (kRanked) {
-    rebuild_stream(lab, G, bits, col, arcs, al, abits);
+    rebuild_stream(lab, G, bits, col, arcs, al, abits, store_sc1 != 0);
   } else {
     auto p1 = [&](int c) -> u32 {
       if (bits) return (u32)c < (u32)nhb ? hot[(u32)c >> 5] : gbits[(u32)c >> 5];
@@ -2120,7 +2129,7 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
       if (hyb) return (u32)c < nh ? (int32_t)w : (((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c]);
       return (u32)c < nh ? (int32_t)w : Ln[c];
     };
-    rebuild_pipe(p1, p2, G, bits || hyb, col, arcs, al, abits);
+    rebuild_pipe(p1, p2, G, bits || hyb, col, arcs, al, abits, store_sc1 != 0);
   }
 }
 
@@ -2149,7 +2158,7 @@ __global__ __launch_bounds__(256) void k_al_rebuild_small(const unsigned long lo
     if ((gbits[(u32)c >> 5] >> ((u32)c & 31u)) & 1u) return G;
     return Ln[c];
   };
-  rebuild_stream(lab, G, true, col, arcs, al, abits);
+  rebuild_stream(lab, G, true, col, arcs, al, abits, false);
 }
 
 __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __restrict__ new_of,
@@ -2660,7 +2669,7 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
                      g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \
-                     g->rebuild_hybrid)
+                     g->rebuild_hybrid, g->rebuild_sc1)
     if (if_wanted) {
       if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
     } else {
