@@ -61,7 +61,7 @@ class LpaGraphInfo(ctypes.Structure):
         ("hub_vertices", ctypes.c_int64), ("segments", ctypes.c_int64),
         ("device_bytes", ctypes.c_int64),
         ("exchanges_full", ctypes.c_int64), ("exchanges_delta", ctypes.c_int64),
-        ("exchanges_giant", ctypes.c_int64), ("id_order", ctypes.c_int64),
+        ("exchanges_giant", ctypes.c_int64),
     ]
 
     def to_dict(self):

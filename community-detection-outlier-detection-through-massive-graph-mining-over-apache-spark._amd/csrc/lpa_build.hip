@@ -132,37 +132,6 @@ __global__ void k_locality_keys(u64* __restrict__ keys, int64_t V, const int32_t
   }
 }
 
-// Input-id locality: the fraction of edges whose endpoints' ids differ by less than a
-// window (one block-reduced count).  Generators and crawls that number communities
-// contiguously (planted-partition SBM: block = id / block size) put most edges inside
-// the window; scrambled or hashed ids (R-MAT, SHA-1 domain ids) almost none.
-__global__ __launch_bounds__(256) void k_id_local(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
-                                                  int64_t m, int32_t w, unsigned long long* __restrict__ cnt) {
-  __shared__ unsigned long long ws[4];
-  unsigned long long c = 0;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t a = src[e], b = dst[e];
-    c += (a > b ? a - b : b - a) < w ? 1ull : 0ull;
-  }
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0 && (ws[0] | ws[1] | ws[2] | ws[3])) atomicAdd(cnt, ws[0] + ws[1] + ws[2] + ws[3]);
-}
-
-// id order inside the bins below the hubs (hubs by degree desc): keys (bin, hub degree
-// rank | 0) in the high word, generated in id order, so a stable sort on the high word
-// leaves ids ascending inside each bin -- the input's own locality (a community's
-// vertices in contiguous slots, so its rows' label gathers share lines)
-__global__ void k_id_order_keys(u64* __restrict__ keys, int64_t V, const int32_t* __restrict__ deg, int32_t maxdeg) {
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t d = deg[v];
-    const u32 bin = degree_bin(d);
-    const u32 a = bin == 0 ? (u32)(maxdeg - d) : 0u;
-    keys[v] = ((u64)((bin << 28) | a) << 32) | (u64)v;
-  }
-}
-
 __global__ void k_vertex_order(const u64* __restrict__ keys, int64_t V, int32_t P, int64_t S,
                                int32_t* __restrict__ new_of, int32_t* __restrict__ old_of) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < V;
@@ -377,43 +346,32 @@ __global__ void k_l2_degree(const int64_t* __restrict__ out_off, const int64_t* 
   }
 }
 // arcs of row s from its intra out-edges, in place: row s's first dout[s] positions
-// (rows are the runs of the (s, d) order, so the per-row terms are cached loads); the
-// arc's row and position are kept per edge (pinfo) for its twin in k_l2_emit_in
+// (rows are the runs of the (s, d) order, so the per-row terms are cached loads; the
+// column's slot is one gather from new_of, 4 B per vertex, cache-resident)
 __global__ void k_l2_emit_out(const u64* __restrict__ ek, int64_t md, const uint8_t* __restrict__ mark,
                               const uint32_t* __restrict__ pos_out, const int64_t* __restrict__ out_off,
                               const int32_t* __restrict__ new_of, const int64_t* __restrict__ rp,
-                              int32_t* __restrict__ col, int32_t* __restrict__ crow, u64* __restrict__ pinfo) {
+                              int32_t* __restrict__ col) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < md; i += (int64_t)gridDim.x * blockDim.x) {
     if (!mark[i]) continue;
     const u64 k = ek[i];
-    const int32_t sv = (int32_t)(k >> 32), rs = new_of[sv];
-    const int64_t p = rp[rs] + (int64_t)(pos_out[i] - pos_out[out_off[sv]]);
+    const int32_t sv = (int32_t)(k >> 32);
+    const int64_t p = rp[new_of[sv]] + (int64_t)(pos_out[i] - pos_out[out_off[sv]]);
     col[p] = new_of[(int32_t)(u32)k];
-    crow[p] = rs;
-    pinfo[i] = ((u64)(u32)rs << 32) | (u64)(u32)p;
   }
 }
-// arcs of row d from its intra in-edges, after its out-edges; each edge's two arcs are
-// each other's CSC entry: column u's positions are the twins of row u's arcs, so the
-// CSC shares the row offsets (cptr = rp) and cpos[p] = q, cpos[q] = p.  Per edge one
-// random 8-B read (the out-arc's row and position) and one random 4-B write (cpos[p]).
-__global__ void k_l2_emit_in(const u64* __restrict__ et, int64_t md, const uint8_t* __restrict__ mark,
-                             const uint32_t* __restrict__ pos_in, const int64_t* __restrict__ in_off,
-                             const int32_t* __restrict__ dout, const int32_t* __restrict__ new_of,
-                             const int64_t* __restrict__ rp, const u64* __restrict__ pinfo,
-                             int32_t* __restrict__ col, int32_t* __restrict__ crow, uint32_t* __restrict__ cpos) {
+// arcs of row d from its intra in-edges, after its out-edges (de_t: d << 32 | index into
+// the (s, d) order, de_ts: s)
+__global__ void k_l2_emit_in(const u64* __restrict__ et, const uint32_t* __restrict__ ets, int64_t md,
+                             const uint8_t* __restrict__ mark, const uint32_t* __restrict__ pos_in,
+                             const int64_t* __restrict__ in_off, const int32_t* __restrict__ dout,
+                             const int32_t* __restrict__ new_of, const int64_t* __restrict__ rp,
+                             int32_t* __restrict__ col) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < md; j += (int64_t)gridDim.x * blockDim.x) {
     if (!mark[j]) continue;
-    const u64 k = et[j];
-    const int32_t dv = (int32_t)(k >> 32);
-    const u64 pi = pinfo[(u32)k];
-    const int32_t rd = new_of[dv], rs = (int32_t)(pi >> 32);
-    const uint32_t p = (uint32_t)pi;
-    const int64_t q = rp[rd] + dout[dv] + (int64_t)(pos_in[j] - pos_in[in_off[dv]]);
-    col[q] = rs;
-    crow[q] = rd;
-    cpos[p] = (uint32_t)q;
-    cpos[q] = p;
+    const int32_t dv = (int32_t)(et[j] >> 32);
+    const int64_t q = rp[new_of[dv]] + dout[dv] + (int64_t)(pos_in[j] - pos_in[in_off[dv]]);
+    col[q] = new_of[(int32_t)ets[j]];
   }
 }
 
@@ -472,30 +430,7 @@ int vertex_order(lpa_graph* g, int32_t V, int64_t m, bool locality) {
     for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(vk, vk + V, V, shifts, ns, s));
-    // the input ids' own locality first: more than half of the edges within a window of
-    // 16 K ids -> id order inside the bins (the neighbour-rank order below would scatter
-    // it); LPA_LOCALITY=3 / 4 skip the test
-    bool id_local = false;
-    if (locality && g->id_order_test && m > 0 && V < (1 << 28) && g->locality <= 2 && V > (1 << 16)) {
-      unsigned long long* d_cnt = nullptr;
-      LPA_TRY(scratch_alloc(g, (void**)&d_cnt, sizeof(unsigned long long)));
-      LPA_HIP(hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long), s));
-      hipLaunchKernelGGL(k_id_local, dim3(grid_for(m) < 2048u ? grid_for(m) : 2048u), dim3(256), 0, s, g->e_src,
-                         g->e_dst, m, 1 << 14, d_cnt);
-      LPA_HIP(hipGetLastError());
-      unsigned long long h_cnt = 0;
-      LPA_HIP(hipMemcpyAsync(&h_cnt, d_cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, s));
-      LPA_HIP(hipStreamSynchronize(s));
-      scratch_free(g, d_cnt);
-      id_local = 2 * (int64_t)h_cnt > m;
-    }
-    g->id_order = id_local;
-    if (id_local) {
-      hipLaunchKernelGGL(k_id_order_keys, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, g->deg, g->max_degree);
-      LPA_HIP(hipGetLastError());
-      const int hi[4] = {32, 40, 48, 56};
-      LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
-    } else if (locality && m > 0 && V < (1 << 28)) {
+    if (locality && m > 0 && V < (1 << 28)) {
       const int K = g->locality < 4 ? g->locality : 4;  // neighbour keys (LPA_LOCALITY)
       int32_t* rank_of = nullptr;
       LPA_TRY(scratch_alloc(g, (void**)&rank_of, sizeof(int32_t) * (1 + K) * (size_t)V));
@@ -891,50 +826,34 @@ int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L, cons
     return LPA_EINVAL;
   }
 
-  // ---- arcs at their final positions, the CSC as their twins ----
+  // ---- arcs at their final positions ----
+  // No CSC position index: the sub-graph runs 5 supersteps, the first two label-dense,
+  // and every refresh rebuilds al[] (no_scatter).  Its twins (cpos) would cost one random
+  // read and one random write per edge into GB-sized arrays (16.8 ms at C3, more than
+  // the rebuilds they save); the frontier is off with it (every refresh is a rebuild).
+  g->no_scatter = true;
   LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
-  LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
-  LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t) * (arcs > 0 ? arcs : 1)));
   LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
   LPA_HIP(hipMemcpyAsync(g->cptr, g->rp, sizeof(int64_t) * (S + 1), hipMemcpyDeviceToDevice, s));
   if (md > 0) {
-    u64* pinfo = nullptr;
-    LPA_TRY(scratch_alloc(g, (void**)&pinfo, sizeof(u64) * md));
     hipLaunchKernelGGL(k_l2_emit_out, dim3(grid_for(md)), dim3(256), 0, s, parent->de_keys, md, mo_c, pos_out,
-                       parent->de_out_off, g->new_of, g->rp, g->col, g->crow, pinfo);
-    hipLaunchKernelGGL(k_l2_emit_in, dim3(grid_for(md)), dim3(256), 0, s, parent->de_t, md, mi, pos_in,
-                       parent->de_in_off, dout, g->new_of, g->rp, pinfo, g->col, g->crow, g->cpos);
+                       parent->de_out_off, g->new_of, g->rp, g->col);
+    hipLaunchKernelGGL(k_l2_emit_in, dim3(grid_for(md)), dim3(256), 0, s, parent->de_t, parent->de_ts, md, mi,
+                       pos_in, parent->de_in_off, dout, g->new_of, g->rp, g->col);
     LPA_HIP(hipGetLastError());
-    scratch_free(g, pinfo);
   }
   if (mo) scratch_free(g, mo);
   scratch_free(g, mi);
   scratch_free(g, pos_out);
   scratch_free(g, pos_in);
   scratch_free(g, dout);
-  // static scatter chunks of every column (its count is its degree: P = 1, symmetric)
-  int32_t* nch = nullptr;
-  LPA_TRY(scratch_alloc(g, (void**)&nch, sizeof(int32_t) * S));
-  hipLaunchKernelGGL(k_col_chunks, dim3(grid_for(S)), dim3(256), 0, s, deg_own, S, nch);
-  LPA_HIP(hipGetLastError());
+  // empty scatter-chunk tables (no column has a chunk: the diff queues nothing)
+  LPA_TRY(dev_alloc(g, (void**)&g->cpos, sizeof(uint32_t)));
   LPA_TRY(dev_alloc(g, (void**)&g->cch, sizeof(int64_t) * (g->vpad + 1)));
-  LPA_TRY(exclusive_scan_i32_i64(nch, g->cch, g->vpad, s));
-  LPA_HIP(hipMemcpyAsync(&g->n_chunks, g->cch + g->vpad, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  LPA_HIP(hipStreamSynchronize(s));
-  scratch_free(g, nch);
-  LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t) * (g->n_chunks > 0 ? g->n_chunks : 1)));
-  {
-    unsigned long long* d_end = nullptr;
-    LPA_TRY(scratch_alloc(g, (void**)&d_end, sizeof(unsigned long long)));
-    LPA_HIP(hipMemsetAsync(d_end, 0, sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(k_chunk_owner, dim3(grid_for(g->vpad)), dim3(256), 0, s, g->cch, g->vpad, g->cowner, d_end);
-    LPA_HIP(hipGetLastError());
-    unsigned long long h_end = 0;
-    LPA_HIP(hipMemcpyAsync(&h_end, d_end, sizeof(h_end), hipMemcpyDeviceToHost, s));
-    LPA_HIP(hipStreamSynchronize(s));
-    scratch_free(g, d_end);
-    g->n_chunk_scan = (int64_t)h_end;
-  }
+  LPA_HIP(hipMemsetAsync(g->cch, 0, sizeof(int64_t) * (g->vpad + 1), s));
+  LPA_TRY(dev_alloc(g, (void**)&g->cowner, sizeof(int32_t)));
+  g->n_chunks = 0;
+  g->n_chunk_scan = 0;
   return finish_build(g, deg_own, m2);
 }
 

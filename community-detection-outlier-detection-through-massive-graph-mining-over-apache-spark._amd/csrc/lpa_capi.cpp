@@ -163,9 +163,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
   if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
   if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
-  if (const char* f = getenv("LPA_ID_ORDER")) g->id_order_test = atoi(f);
   if (const char* f = getenv("LPA_REBUILD_HYBRID")) g->rebuild_hybrid = atoi(f);
-  if (const char* f = getenv("LPA_REBUILD_SC1")) g->rebuild_sc1 = atoi(f);
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
@@ -554,7 +552,6 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->own_begin = g->own_begin;
   info->rank = g->rank;
   info->nranks = g->nranks;
-  info->id_order = g->id_order ? 1 : 0;
   info->device = g->device;
   info->max_degree = g->max_degree;
   for (int b = 0; b < LPA_NBINS; ++b) {

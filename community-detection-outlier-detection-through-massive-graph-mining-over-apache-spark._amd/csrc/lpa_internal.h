@@ -222,15 +222,12 @@ struct lpa_graph {
   int32_t* chlist = nullptr;    // [vpad] changed one-chunk columns (count: counters[par][0])
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
   int rebuild_hybrid = 1;                   // its hybrid labels + bits mode (LPA_REBUILD_HYBRID=0: A/B)
-  int rebuild_sc1 = 0;                      // its al[] stores sc1 instead of non-temporal (LPA_REBUILD_SC1)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per
   // (superstep, cur, par)
   hipGraphExec_t gexec[16] = {};
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
-  bool id_order = false;                    // the input ids carry locality: id order inside the bins
-  int id_order_test = 1;                    // LPA_ID_ORDER=0: never take the id order (A/B)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
@@ -271,6 +268,8 @@ struct lpa_graph {
 
   int64_t device_bytes = 0;
   bool pooled = false;                      // kFlagPooled: arrays from the stream-ordered pool
+  bool no_scatter = false;                  // no CSC position index: every refresh rebuilds al[]
+                                            //   (the outlier stage's 5-superstep L2 sub-graph)
   bool borrowed = false;                    // aux streams / fork-join events belong to a parent handle
   hipEvent_t ev[2 * LPA_STATS_MAX_ITERS + 2] = {};
   hipEvent_t bin_ev[LPA_STATS_MAX_ITERS * lpa::kBinEvents] = {};

@@ -1885,21 +1885,13 @@ __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __
   }
 }
 
-// al[] store of the rebuild: non-temporal (the line stays in the XCD's L2), or sc1 (the
-// line leaves L2: the 4 B/arc store stream then evicts none of the label lines the
-// gathers hit; MI355X_MICROARCH.md, store flavours)
-__device__ __forceinline__ void st_arc(int32_t* p, int32_t v, bool sc1) {
-  if (sc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else __builtin_nontemporal_store(v, p);
-}
-
 // al[i] = lab(col[i]) over every arc by the calling grid (one wave per 512-arc batch,
 // grid-stride); bits: also the arc giant bits (abits: bit i = al[i] == G, one ballot
 // per 64 arcs), which the next superstep's full tally settles rows from (k_settle_*).
 template <typename Lab>
 __device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, const int32_t* __restrict__ col,
                                                int64_t arcs, int32_t* __restrict__ al,
-                                               unsigned long long* __restrict__ abits, bool sc1) {
+                                               unsigned long long* __restrict__ abits) {
   // lane-consecutive arcs: one gather instruction covers 64 consecutive arcs of
   // a row, whose sorted columns often share lines (hub rows) -> fewer L2 requests.
   // Full 512-arc batches are software-pipelined: the next batch's column loads are in
@@ -1924,7 +1916,7 @@ __device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, co
 #pragma unroll
     for (int k = 0; k < 8; ++k) r[k] = lab(c[k]);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) st_arc(al + base + k * 64 + lane, r[k], sc1);
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
     if (bits) {
       unsigned long long mine = 0ull;
 #pragma unroll
@@ -1960,7 +1952,7 @@ __device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, co
 template <typename P1, typename P2>
 __device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits, const int32_t* __restrict__ col,
                                              int64_t arcs, int32_t* __restrict__ al,
-                                             unsigned long long* __restrict__ abits, bool sc1) {
+                                             unsigned long long* __restrict__ abits) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t step = nw * 512;
@@ -1986,7 +1978,7 @@ __device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits,
   };
   auto S = [&](const int32_t (&r)[8], int64_t b) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) st_arc(al + b + k * 64 + lane, r[k], sc1);
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + b + k * 64 + lane);
     if (bits) {
       unsigned long long mine = 0ull;
 #pragma unroll
@@ -2058,8 +2050,7 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
                                                          int slice_lg, int hot_lg, int hb_lg,
                                                          const uint32_t* __restrict__ gbits, int64_t nbits,
                                                          int32_t* __restrict__ gword,
-                                                         unsigned long long* __restrict__ abits, int allow_hyb,
-                                                         int store_sc1) {
+                                                         unsigned long long* __restrict__ abits, int allow_hyb) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   __shared__ u32 hot[kHotLabelsSingle];
   u32* s_cnt = &hot[kHotLabelsSingle - 1];   // beyond the bit words; labels mode refills it
@@ -2085,6 +2076,9 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
   // the bit is clear (Chung-Lu C5 superstep 2: G on ~40 % of the arcs, ~30 % of the cold
   // gathers become L2 / Infinity-Cache hits on the 5 MB bit array)
   const bool hyb = !kRanked && allow_hyb && !bits && 8 * (int64_t)*s_cnt >= nhb && nhb > 0;
+  // allow_hyb 2: labels-mode gathers, only the arc giant bits written (the next superstep's
+  // settle); 1: cold columns also take G from their bit
+  const bool hyb_bits = hyb && allow_hyb == 1;
   const int32_t G = gword[0];
   // bits / hybrid modes also write the arc giant bits (abits: bit i = al[i] == G, one
   // ballot per 64 arcs), which the next superstep's full tally settles rows from
@@ -2117,19 +2111,19 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
     }
   };
   if constexpr (kRanked) {
-    rebuild_stream(lab, G, bits, col, arcs, al, abits, store_sc1 != 0);
+    rebuild_stream(lab, G, bits, col, arcs, al, abits);
   } else {
     auto p1 = [&](int c) -> u32 {
       if (bits) return (u32)c < (u32)nhb ? hot[(u32)c >> 5] : gbits[(u32)c >> 5];
-      if (hyb) return (u32)c < nh ? hot[c] : gbits[(u32)c >> 5];
+      if (hyb_bits) return (u32)c < nh ? hot[c] : gbits[(u32)c >> 5];
       return (u32)c < nh ? hot[c] : 0u;
     };
     auto p2 = [&](int c, u32 w) -> int32_t {
       if (bits) return ((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c];
-      if (hyb) return (u32)c < nh ? (int32_t)w : (((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c]);
+      if (hyb_bits) return (u32)c < nh ? (int32_t)w : (((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c]);
       return (u32)c < nh ? (int32_t)w : Ln[c];
     };
-    rebuild_pipe(p1, p2, G, bits || hyb, col, arcs, al, abits, store_sc1 != 0);
+    rebuild_pipe(p1, p2, G, bits || hyb, col, arcs, al, abits);
   }
 }
 
@@ -2158,7 +2152,7 @@ __global__ __launch_bounds__(256) void k_al_rebuild_small(const unsigned long lo
     if ((gbits[(u32)c >> 5] >> ((u32)c & 31u)) & 1u) return G;
     return Ln[c];
   };
-  rebuild_stream(lab, G, true, col, arcs, al, abits, false);
+  rebuild_stream(lab, G, true, col, arcs, al, abits);
 }
 
 __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __restrict__ new_of,
@@ -2669,7 +2663,7 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
                      g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \
-                     g->rebuild_hybrid, g->rebuild_sc1)
+                     g->rebuild_hybrid)
     if (if_wanted) {
       if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
     } else {
@@ -2735,7 +2729,8 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
     LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, true, par));
   }
   LPA_TRACE_POINT("diff");
-  const int64_t thr = (int64_t)(kRebuildFrac * (double)g->arcs);
+  // (a handle without the CSC position index rebuilds every time: counters[1] >= 0 > -1)
+  const int64_t thr = g->no_scatter ? -1 : (int64_t)(kRebuildFrac * (double)g->arcs);
   FrontierMarks fm;
   fm.crow = g->crow;
   fm.rp = g->rp;

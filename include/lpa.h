@@ -80,8 +80,6 @@ typedef struct lpa_graph_info {
   int64_t exchanges_delta; /* P > 1: label exchanges done as changed-label deltas */
   int64_t exchanges_giant; /* P > 1: label exchanges done giant-compressed (bitmap of the
                               giant label + changed non-giant labels) */
-  int64_t id_order;        /* 1: the input ids carry locality (most edges within 16 K ids),
-                              so the slots inside each degree bin keep the id order */
 } lpa_graph_info;
 
 /* Outlier summary. */

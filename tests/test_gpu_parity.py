@@ -294,35 +294,6 @@ def test_chunglu_heavy_hub_every_superstep(gfa, oracle):
         assert np.array_equal(got[t], hist[t]), f"Chung-Lu superstep {t + 1}"
 
 
-def test_sbm_id_order_every_superstep(gfa, oracle):
-    """An SBM with block-contiguous ids (200 K vertices, 100 blocks): the build detects
-    the input-id locality and keeps the id order inside the degree bins; every superstep
-    bit-exact, on one GPU and over a P = 2 loopback group; R-MAT's scrambled ids do not
-    trigger it."""
-    V = 200_000
-    s, d = gfa.gen_sbm(V, 100, 4_000_000, seed=5)
-    sn, dn = s.cpu().numpy(), d.cpu().numpy()
-    _, hist, _ = oracle.lpa(V, sn, dn, 8, per_iter=True)
-    with gfa.Graph(s, d, V) as g:
-        assert g.info()["id_order"] == 1
-        for t in range(8):
-            g.step(1)
-            assert np.array_equal(g.labels(), hist[t]), f"superstep {t + 1}"
-    lb = gfa.Loopback(2)
-    ranks = [gfa.Graph(sn, dn, V, rank=r, loopback=lb) for r in range(2)]
-    try:
-        assert all(g.info()["id_order"] == 1 for g in ranks)
-        runs = gfa.run_ranks(ranks, lambda r, g: g.run(8))
-        assert all(np.array_equal(x, hist[7]) for x in runs)
-    finally:
-        for g in ranks:
-            g.close()
-        lb.close()
-    ts, td = gfa.gen_rmat(17, 16, seed=1)
-    with gfa.Graph(ts, td, 1 << 17) as g:
-        assert g.info()["id_order"] == 0
-
-
 def test_sbm_bit_exact(gfa, oracle):
     s, d = gfa.gen_sbm(20000, 20, 400000)
     with gfa.Graph(s, d, 20000) as g:
