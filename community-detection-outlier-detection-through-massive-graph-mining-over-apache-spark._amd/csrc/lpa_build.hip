@@ -832,6 +832,9 @@ int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L, cons
   // read and one random write per edge into GB-sized arrays (16.8 ms at C3, more than
   // the rebuilds they save); the frontier is off with it (every refresh is a rebuild).
   g->no_scatter = true;
+  // no captured superstep graphs: a handle that lives for 5 supersteps pays their capture,
+  // instantiation and destruction (~8 ms of host time at C3) for ~1 ms of launches
+  g->use_graphs = 0;
   LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
   LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
   LPA_HIP(hipMemcpyAsync(g->cptr, g->rp, sizeof(int64_t) * (S + 1), hipMemcpyDeviceToDevice, s));

@@ -221,7 +221,9 @@ struct lpa_graph {
   int64_t n_chunk_scan = 0;     // chunks below this belong to every multi-chunk column
   int32_t* chlist = nullptr;    // [vpad] changed one-chunk columns (count: counters[par][0])
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
-  int rebuild_hybrid = 1;                   // its hybrid labels + bits mode (LPA_REBUILD_HYBRID=0: A/B)
+  int rebuild_hybrid = 2;                   // G on 1/8..1/2 of the bit-range slots: 2 labels-mode
+                                            //   gathers + the arc giant bits, 1 also G from the bits
+                                            //   of cold columns, 0 neither (LPA_REBUILD_HYBRID, A/B)
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per
@@ -325,7 +327,9 @@ int ensure_al(lpa_graph* g);           // al valid (copies al0 after a lazy rese
 int frontier_all(lpa_graph* g, int par);  // next tally of parity `par` takes every row
 
 // iteration (lpa_iter.hip)
-int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st);
+// last_refresh = false: the last superstep leaves al[] stale (a handle whose labels are
+// read and which is then destroyed: the outlier stage's L2 sub-graph)
+int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh = true);
 int gather_labels(lpa_graph* g, int32_t* out_dense_dev);
 
 // collective backend (lpa_comm.cpp): allgather of `count` elements of `elem` bytes

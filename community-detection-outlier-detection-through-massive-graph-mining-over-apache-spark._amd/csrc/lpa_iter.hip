@@ -2787,7 +2787,7 @@ int capture_graph(lpa_graph* g, hipGraphExec_t* out, Body body) {
   return LPA_OK;
 }
 
-int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
+int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
   hipStream_t s = g->stream;
   const bool timed = st != nullptr;
   const int nt = n < LPA_STATS_MAX_ITERS ? n : LPA_STATS_MAX_ITERS;
@@ -2889,7 +2889,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st) {
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
     // (changes + refresh); a refresh here would see a partial vector
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));  // stays if there is no refresh
-    if ((!exchanges(g) || has_collective(g)) && !early_graph)
+    if ((!exchanges(g) || has_collective(g)) && !early_graph && (last_refresh || t + 1 < n))
       LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par,
                              bev ? bev[kTallyEv + 2] : nullptr));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 3], s));

@@ -615,7 +615,8 @@ int outlier(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, int32
     // second LPA on the induced simple subgraph (same device, same stream)
     lpa_graph* h = nullptr;
     LPA_TRY(create_l2(g, L, intra, &h));
-    int rc = run_supersteps(h, sub_iter, nullptr);
+    // no refresh after the last superstep: only the labels are read, then h is destroyed
+    int rc = run_supersteps(h, sub_iter, nullptr, false);
     if (rc == LPA_OK) rc = gather_labels(h, sub);
     if (rc == LPA_OK && hipStreamSynchronize(s) != hipSuccess) rc = LPA_EHIP;
     destroy(h);

@@ -76,4 +76,10 @@ if ab:
     na = A - info["bin_arcs"]["seg"]
     res["k_abits_pass"] = entry("k_abits_pass", ab, 4 * na + na // 8,
                                 "al 4 B/arc read + 1 bit/arc written over the rows below the hubs; superstep 4")
+fr = in_call(lf, "k_first_runs", 1)
+if fr:
+    S = info["slice"]
+    res["k_first_runs"] = entry("k_first_runs", fr, 4 * A + A // 8 + 4 * S,
+                                "al0 4 B/arc + row-start bits 1/8 B/arc + the label of every row (4 B); "
+                                "superstep 1 (round 4: the 1-bit row-start map replaced crow, 4 B/arc)")
 print(json.dumps(res, indent=1))
