@@ -62,6 +62,8 @@ class LpaGraphInfo(ctypes.Structure):
         ("device_bytes", ctypes.c_int64),
         ("exchanges_full", ctypes.c_int64), ("exchanges_delta", ctypes.c_int64),
         ("exchanges_giant", ctypes.c_int64),
+        ("blocked_rows", ctypes.c_int64),
+        ("blocked_pieces", ctypes.c_int64),
     ]
 
     def to_dict(self):

@@ -154,14 +154,74 @@ __global__ void k_owned_degree(const int32_t* __restrict__ old_of_own,
 }
 
 // P == 1: every edge gives two arcs at fixed positions (no atomics)
+// rows below H (the class-blocked rows) sort their columns by (class, column): the
+// class sits above the column's blo bits of the key
 __global__ void k_emit_arcs_single(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                    int64_t m, const int32_t* __restrict__ new_of,
-                                   u64* __restrict__ keys) {
+                                   u64* __restrict__ keys, int64_t H, int blo) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
        e += (int64_t)gridDim.x * blockDim.x) {
     u64 s = (u32)new_of[src[e]], d = (u32)new_of[dst[e]];
-    keys[2 * e] = (s << 32) | d;
-    keys[2 * e + 1] = (d << 32) | s;
+    const u64 cd = (int64_t)s < H ? (u64)col_class((int32_t)d) << blo : 0ull;
+    const u64 cs = (int64_t)d < H ? (u64)col_class((int32_t)s) << blo : 0ull;
+    keys[2 * e] = (s << 32) | cd | d;
+    keys[2 * e + 1] = (d << 32) | cs | s;
+  }
+}
+
+// H = the number of rows of degree > T: with the degree-binned slot order (bins are
+// contiguous, highest degrees first) they are the first H rows
+__global__ void k_count_hub_rows(const int32_t* __restrict__ deg_own, int64_t S, int32_t T,
+                                 int64_t* __restrict__ H) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < S; r += (int64_t)gridDim.x * blockDim.x)
+    if (deg_own[r] > T && (r + 1 == S || deg_own[r + 1] <= T)) *H = r + 1;
+}
+
+// class segments of the blocked rows (index x H + h, class-major): the first position
+// of row h with class >= x by binary search (the row is in (class, column) order), and
+// the segment's piece count (<= 64 arcs each)
+__global__ void k_class_segments(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t H,
+                                 uint32_t* __restrict__ seg_start, int32_t* __restrict__ npieces) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 8 * H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = i / H, h = i - x * H;
+    const int64_t b = rp[h], e = rp[h + 1];
+    auto first_ge = [&](uint32_t cls) {
+      int64_t lo = b, hi = e;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (col_class(col[mid]) < cls) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo;
+    };
+    const int64_t s0 = first_ge((uint32_t)x), s1 = x == 7 ? e : first_ge((uint32_t)x + 1);
+    seg_start[i] = (uint32_t)s0;
+    npieces[i] = (int32_t)((s1 - s0 + 63) / 64);
+  }
+}
+
+__global__ void k_emit_pieces(const int64_t* __restrict__ rp, const uint32_t* __restrict__ seg_start,
+                              const int64_t* __restrict__ poff, int64_t H, const int64_t* __restrict__ base,
+                              u64* __restrict__ pieces) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 8 * H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = i / H, h = i - x * H;
+    const int64_t s0 = seg_start[i];
+    const int64_t s1 = x == 7 ? rp[h + 1] : (int64_t)seg_start[i + H];
+    int64_t q = base[x] + (poff[i] - poff[x * H]);
+    for (int64_t p = s0; p < s1; p += 64, ++q)
+      pieces[q] = ((u64)(s1 - p < 64 ? s1 - p : 64) << 32) | (u64)p;
+  }
+}
+
+// the positions [a, a0) between the last blocked row and the aligned start of the
+// plain stream: pieces at the end of class 7's list
+__global__ void k_tail_pieces(int64_t a, int64_t a0, int64_t q0, u64* __restrict__ pieces) {
+  const int64_t n = (a0 - a + 63) / 64;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = a + 64 * j;
+    pieces[q0 + j] = ((u64)(a0 - p < 64 ? a0 - p : 64) << 32) | (u64)p;
   }
 }
 
@@ -192,11 +252,11 @@ __global__ void k_emit_arcs_owned(const int32_t* __restrict__ src, const int32_t
 // sorted (row << 32 | col) keys -> col[] and the row of every arc position (crow[],
 // read by the al[] scatter to mark the rows its writes make dirty)
 __global__ void k_keys_to_col(const u64* __restrict__ keys, int64_t n, int32_t* __restrict__ col,
-                              int32_t* __restrict__ crow) {
+                              int32_t* __restrict__ crow, u32 cmask) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += (int64_t)gridDim.x * blockDim.x) {
     const u64 k = keys[j];
-    col[j] = (int32_t)(u32)k;
+    col[j] = (int32_t)((u32)k & cmask);
     crow[j] = (int32_t)(k >> 32);
   }
 }
@@ -598,6 +658,59 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
   return LPA_OK;
 }
 
+// The class-blocked rebuild's piece lists (lpa_iter.hip rebuild_pieces) over the first
+// H rows (in (class, column) order): per class, every row's class segment in <= 64-arc
+// pieces, row after row, then padding to a multiple of 8 pieces; class 7 also lists
+// the positions up to blk_a0, the 512-aligned start of the plain stream.
+int build_pieces(lpa_graph* g, int64_t H) {
+  hipStream_t s = g->stream;
+  int64_t aH = 0;
+  LPA_HIP(hipMemcpyAsync(&aH, g->rp + H, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  uint32_t* seg = nullptr;
+  int32_t* np = nullptr;
+  int64_t* poff = nullptr;
+  int64_t* d_base = nullptr;
+  LPA_TRY(scratch_alloc(g, (void**)&seg, sizeof(uint32_t) * 8 * H));
+  LPA_TRY(scratch_alloc(g, (void**)&np, sizeof(int32_t) * 8 * H));
+  LPA_TRY(scratch_alloc(g, (void**)&poff, sizeof(int64_t) * (8 * H + 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&d_base, sizeof(int64_t) * 8));
+  hipLaunchKernelGGL(k_class_segments, dim3(grid_for(8 * H)), dim3(256), 0, s, g->rp, g->col, H, seg, np);
+  LPA_HIP(hipGetLastError());
+  LPA_TRY(exclusive_scan_i32_i64(np, poff, 8 * H, s));
+  int64_t cum[9];
+  for (int x = 0; x <= 8; ++x)
+    LPA_HIP(hipMemcpyAsync(&cum[x], poff + x * H, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  int64_t a0 = (aH + 511) / 512 * 512;
+  if (a0 > g->arcs) a0 = g->arcs;
+  const int64_t ntail = (a0 - aH + 63) / 64;
+  int64_t base[8];
+  g->blk_off[0] = 0;
+  for (int x = 0; x < 8; ++x) {
+    base[x] = g->blk_off[x];
+    const int64_t n = cum[x + 1] - cum[x] + (x == 7 ? ntail : 0);
+    g->blk_off[x + 1] = g->blk_off[x] + (n + 7) / 8 * 8;
+  }
+  LPA_TRY(dev_alloc(g, (void**)&g->blk_pieces, sizeof(u64) * (g->blk_off[8] > 0 ? g->blk_off[8] : 1)));
+  LPA_HIP(hipMemsetAsync(g->blk_pieces, 0, sizeof(u64) * (g->blk_off[8] > 0 ? g->blk_off[8] : 1), s));
+  LPA_HIP(hipMemcpyAsync(d_base, base, sizeof(base), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_emit_pieces, dim3(grid_for(8 * H)), dim3(256), 0, s, g->rp, seg, poff, H, d_base,
+                     g->blk_pieces);
+  LPA_HIP(hipGetLastError());
+  if (ntail > 0) {
+    hipLaunchKernelGGL(k_tail_pieces, dim3(grid_for(ntail)), dim3(256), 0, s, aH, a0,
+                       base[7] + (cum[8] - cum[7]), g->blk_pieces);
+    LPA_HIP(hipGetLastError());
+  }
+  LPA_HIP(hipStreamSynchronize(s));
+  g->blk_a0 = a0;
+  scratch_free(g, d_base);
+  scratch_free(g, poff);
+  scratch_free(g, np);
+  scratch_free(g, seg);
+  return LPA_OK;
+}
+
 int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
                 uint32_t flags) {
   hipStream_t s = g->stream;
@@ -672,9 +785,27 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
       set_error("out of device memory for %lld arc keys", (long long)(2 * arcs));
       return LPA_ENOMEM;
     }
+    int blo = bits_for((uint64_t)(g->vpad - 1)), bhi = bits_for((uint64_t)(S - 1));
+    // class-blocked rows (P = 1 hot-set rebuild sizes; the class needs 3 key bits)
+    g->cols_sorted = !g->pooled;
+    int64_t H = 0;
+    if (P == 1 && g->cols_sorted && g->block_deg > 0 && g->vpad >= kHotMinSlots && blo + 3 <= 32) {
+      int64_t* d_h = nullptr;
+      LPA_TRY(scratch_alloc(g, (void**)&d_h, sizeof(int64_t)));
+      LPA_HIP(hipMemsetAsync(d_h, 0, sizeof(int64_t), s));
+      // a power of two: the degree bins of the locality order are (2^(j-1), 2^j]
+      int32_t T = 1;
+      while (2 * T <= g->block_deg && T < (1 << 30)) T *= 2;
+      hipLaunchKernelGGL(k_count_hub_rows, dim3(grid_for(S)), dim3(256), 0, s, deg_own, S, T, d_h);
+      LPA_HIP(hipGetLastError());
+      LPA_HIP(hipMemcpyAsync(&H, d_h, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      LPA_HIP(hipStreamSynchronize(s));
+      scratch_free(g, d_h);
+    }
+    g->blk_rows = H;
     if (P == 1) {
       hipLaunchKernelGGL(k_emit_arcs_single, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
-                         g->e_dst, m, g->new_of, keys);
+                         g->e_dst, m, g->new_of, keys, H, blo);
     } else {
       unsigned long long* cursor = nullptr;
       LPA_TRY(scratch_alloc(g, (void**)&cursor, sizeof(unsigned long long)));
@@ -685,18 +816,19 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     }
     LPA_HIP(hipGetLastError());
     int shifts[16], ns = 0;
-    int blo = bits_for((uint64_t)(g->vpad - 1)), bhi = bits_for((uint64_t)(S - 1));
-    // columns sorted inside each row: the rebuild's gathers of a hub row coalesce.  No
-    // kernel needs the order (a mode is order-free), so a pooled internal graph (the
-    // outlier stage's 5-superstep L2 sub-graph) sorts by row only: half the passes.
-    g->cols_sorted = !g->pooled;
+    // columns sorted inside each row (blocked rows: by class, then column): the
+    // rebuild's gathers of a hub row coalesce, and superstep 1 counts runs of equal
+    // columns.  No tally needs the order (a mode is order-free), so a pooled internal
+    // graph (the outlier stage's 5-superstep L2 sub-graph) sorts by row only.
     if (g->cols_sorted)
-      for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
+      for (int b = 0; b < blo + (H > 0 ? 3 : 0); b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
     LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t) * arcs));
-    hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col, g->crow);
+    hipLaunchKernelGGL(k_keys_to_col, dim3(grid_for(arcs)), dim3(256), 0, s, keys, arcs, g->col, g->crow,
+                       H > 0 ? (u32)((1ull << blo) - 1ull) : ~0u);
     LPA_HIP(hipGetLastError());
+    if (H > 0) LPA_TRY(build_pieces(g, H));
     // CSC position index over this rank's arcs (for the replicated-label refresh)
     if (arcs >= (int64_t)UINT32_MAX) {
       set_error("%lld arcs on one rank exceed the 32-bit position index", (long long)arcs);

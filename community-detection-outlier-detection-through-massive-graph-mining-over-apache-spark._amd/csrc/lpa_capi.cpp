@@ -86,7 +86,7 @@ void destroy(lpa_graph* g) {
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
                   g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best, g->rstart,
-                  g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword, g->al0, g->abits,
+                  g->blk_pieces, g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword, g->al0, g->abits,
                   g->glist};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
@@ -164,6 +164,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
   if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
   if (const char* f = getenv("LPA_REBUILD_HYBRID")) g->rebuild_hybrid = atoi(f);
+  if (const char* f = getenv("LPA_BLOCK_DEG")) g->block_deg = atoi(f);
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
@@ -564,6 +565,8 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->exchanges_full = g->n_exch_full;
   info->exchanges_delta = g->n_exch_delta;
   info->exchanges_giant = g->n_exch_giant;
+  info->blocked_rows = g->blk_pieces ? g->blk_rows : 0;
+  info->blocked_pieces = g->blk_pieces ? g->blk_off[8] : 0;
   return LPA_OK;
 }
 

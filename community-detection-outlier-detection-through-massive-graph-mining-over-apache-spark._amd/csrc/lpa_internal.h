@@ -56,6 +56,12 @@ constexpr double kRebuildFrac = 0.25;
 // the al[] scatter marks dirty rows while <= this fraction of the arcs changed; above
 // it the next superstep tallies every row
 constexpr double kFrontierFrac = 0.005;
+// P = 1 label vectors of at least this many slots take the LDS hot-set rebuild
+// (k_al_rebuild_hot); smaller ones stay in L2 / the Infinity Cache (k_al_rebuild_small)
+constexpr int64_t kHotMinSlots = 4ll << 20;
+// column class of the class-blocked rebuild: the 128-B line (32 slots) of the column's
+// label, mod 8
+__host__ __device__ inline uint32_t col_class(int32_t c) { return ((uint32_t)c >> 5) & 7u; }
 
 struct Segment {   // one unit of a seg-bin row
   int64_t begin;  // first arc (local CSR index)
@@ -224,6 +230,15 @@ struct lpa_graph {
   int rebuild_hybrid = 2;                   // G on 1/8..1/2 of the bit-range slots: 2 labels-mode
                                             //   gathers + the arc giant bits, 1 also G from the bits
                                             //   of cold columns, 0 neither (LPA_REBUILD_HYBRID, A/B)
+  // class-blocked labels-mode rebuild (P = 1, lpa_iter.hip rebuild_pieces): rows of
+  // degree > block_deg keep their columns in (class, column) order, class = column line
+  // (32 slots) mod 8; the class segments cut into <= 64-arc pieces, listed per class
+  // (padded to multiples of 8) so that one block group (one XCD) gathers one class
+  int block_deg = 64;                       // LPA_BLOCK_DEG (0: off; a power of two)
+  lpa::u64* blk_pieces = nullptr;           // [n] (len << 32 | first position)
+  int64_t blk_off[9] = {};                  // class x: pieces [blk_off[x], blk_off[x + 1])
+  int64_t blk_a0 = 0;                       // arcs [0, blk_a0) are listed (a multiple of 512)
+  int64_t blk_rows = 0;                     // rows in (class, column) order
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per

@@ -1854,12 +1854,17 @@ __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__
   }
 }
 
+// (abits / nzero: the class-blocked rebuild that follows ORs the arc giant bits of its
+// pieces into abits[0, nzero): zeroed here, one launch ahead)
 template <bool kIfWanted>
 __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __restrict__ counters, int64_t thr,
                                                     const int32_t* __restrict__ L, int64_t n,
                                                     int32_t* __restrict__ gword,
-                                                    unsigned long long* __restrict__ bits) {
+                                                    unsigned long long* __restrict__ bits,
+                                                    unsigned long long* __restrict__ abits, int64_t nzero) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += (int64_t)gridDim.x * blockDim.x)
+    abits[i] = 0ull;
   const int32_t G = gword[0];
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -2029,6 +2034,93 @@ __device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits,
   }
 }
 
+// The class-blocked part of a labels-mode rebuild (P = 1).  A labels-mode rebuild is
+// bound by its L2-missing gathers (C3 superstep 1: 3.6x the algorithmic bytes); a block
+// group (blocks b = x mod 8, one XCD under the observed round-robin placement, speed
+// only) streams the pieces of column class x -- the class segments of the rows of degree
+// > block_deg, which keep their columns in (class, column) order -- so an XCD's gathers
+// touch 1/8 of the label lines and its L2 holds far more of them (C3, simulated: 0.18
+// -> 0.02 missing gathers per arc).  8 pieces (<= 64 arcs, lane-consecutive) per batch
+// and wave, in rebuild_pipe's three-stage pipeline; a piece's descriptor is re-read
+// (scalar, cached) where its positions are needed; a dead lane carries column -1.
+// bits: the arc giant bits, ORed into abits (a piece need not start a word; the words
+// were zeroed by k_giant_bits).
+struct BlkInfo {
+  int64_t off[9];  // class x: pieces [off[x], off[x + 1]), multiples of 8
+  int64_t a0;      // listed arcs [0, a0) (0: no blocked part)
+};
+template <typename P1, typename P2>
+__device__ __forceinline__ void rebuild_pieces(P1 p1, P2 p2, int32_t G, bool bits, const u64* __restrict__ pieces,
+                                               int64_t q0, int64_t q1, int64_t wi, int64_t nwv,
+                                               const int32_t* __restrict__ col, int32_t* __restrict__ al,
+                                               unsigned long long* __restrict__ abits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t step = nwv * 8;
+  int64_t q = q0 + wi * 8;
+  auto L = [&](int32_t (&c)[8], int64_t qq) {
+    if (qq < q1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const u64 d = pieces[qq + k];
+        c[k] = lane < (int)(d >> 32) ? __builtin_nontemporal_load(col + (u32)d + lane) : -1;
+      }
+    }
+  };
+  auto Q1 = [&](const int32_t (&c)[8], u32 (&w)[8], int64_t qq) {
+    if (qq < q1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w[k] = c[k] >= 0 ? p1(c[k]) : 0u;
+    }
+  };
+  auto Q2 = [&](const int32_t (&c)[8], const u32 (&w)[8], int32_t (&r)[8], int64_t qq) {
+    if (qq < q1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = c[k] >= 0 ? p2(c[k], w[k]) : 0;
+    }
+  };
+  auto S = [&](const int32_t (&r)[8], int64_t qq) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u64 d = pieces[qq + k];
+      const int ln = (int)(d >> 32);
+      const u32 st = (u32)d;
+      if (lane < ln) __builtin_nontemporal_store(r[k], al + st + lane);
+      if (bits) {
+        const unsigned long long m = __ballot(lane < ln && r[k] == G);
+        const u32 wd = st >> 6, off = st & 63u;
+        if (m && lane == 0) atomicOr(&abits[wd], m << off);
+        if (m && lane == 1 && off && (m >> (64u - off))) atomicOr(&abits[wd + 1], m >> (64u - off));
+      }
+    }
+  };
+  int32_t c0[8], c1[8], c2[8], r0[8], r1[8];
+  u32 w0[8], w1[8];
+  if (q < q1) {
+    L(c0, q);
+    L(c1, q + step);
+    L(c2, q + 2 * step);
+    Q1(c0, w0, q);
+    Q1(c1, w1, q + step);
+    Q2(c0, w0, r0, q);
+#define LPA_PIECE_STEP(CA, CB, CC, WA, WB, RA, RB) \
+    L(CA, q + 3 * step);                           \
+    Q1(CC, WA, q + 2 * step);                      \
+    Q2(CB, WB, RB, q + step);                      \
+    S(RA, q);                                      \
+    q += step;                                     \
+    if (q >= q1) break;
+    while (true) {
+      LPA_PIECE_STEP(c0, c1, c2, w0, w1, r0, r1)
+      LPA_PIECE_STEP(c1, c2, c0, w1, w0, r1, r0)
+      LPA_PIECE_STEP(c2, c0, c1, w0, w1, r0, r1)
+      LPA_PIECE_STEP(c0, c1, c2, w1, w0, r1, r0)
+      LPA_PIECE_STEP(c1, c2, c0, w0, w1, r0, r1)
+      LPA_PIECE_STEP(c2, c0, c1, w1, w0, r1, r0)
+    }
+#undef LPA_PIECE_STEP
+  }
+}
+
 // al[] rebuild with an LDS hot set (the slots of the highest-degree vertices: at P = 1
 // the first slots, 30-40 % of all arc targets on R-MAT).  The rebuild is bound by the
 // line traffic of its L2-missing 4-B gathers, and every gather served from LDS is one
@@ -2050,7 +2142,8 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
                                                          int slice_lg, int hot_lg, int hb_lg,
                                                          const uint32_t* __restrict__ gbits, int64_t nbits,
                                                          int32_t* __restrict__ gword,
-                                                         unsigned long long* __restrict__ abits, int allow_hyb) {
+                                                         unsigned long long* __restrict__ abits, int allow_hyb,
+                                                         const u64* __restrict__ pieces, BlkInfo blk) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   __shared__ u32 hot[kHotLabelsSingle];
   u32* s_cnt = &hot[kHotLabelsSingle - 1];   // beyond the bit words; labels mode refills it
@@ -2123,7 +2216,16 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
       if (hyb_bits) return (u32)c < nh ? (int32_t)w : (((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c]);
       return (u32)c < nh ? (int32_t)w : Ln[c];
     };
-    rebuild_pipe(p1, p2, G, bits || hyb, col, arcs, al, abits);
+    if (!bits && pieces) {  // uniform: labels / hybrid mode of a blocked handle
+      const int grp = blockIdx.x & 7;
+      const int64_t nwv = (int64_t)(gridDim.x >> 3) * (blockDim.x >> 6);
+      const int64_t wi = (int64_t)(blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+      rebuild_pieces(p1, p2, G, hyb, pieces, blk.off[grp], blk.off[grp + 1], wi, nwv, col, al, abits);
+      // then every block: the plain stream over the rows below block_deg
+      rebuild_pipe(p1, p2, G, hyb, col + blk.a0, arcs - blk.a0, al + blk.a0, abits + blk.a0 / 64);
+    } else {
+      rebuild_pipe(p1, p2, G, bits || hyb, col, arcs, al, abits);
+    }
   }
 }
 
@@ -2131,7 +2233,6 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
 // the Infinity Cache, so an LDS hot set saves no misses while every block's 160 KB fill
 // costs as much as the arcs' stream at C2 scale): the same bits / labels modes, the
 // bits-mode test from k_giant_bits' count of the hot slots' set bits (gword[3]).
-constexpr int64_t kHotMinSlots = 4ll << 20;
 template <bool kIfWanted>
 __global__ __launch_bounds__(256) void k_al_rebuild_small(const unsigned long long* __restrict__ counters,
                                                           int64_t thr, const int32_t* __restrict__ col, int64_t arcs,
@@ -2168,10 +2269,9 @@ __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __r
 // are sorted: its vote counts are the lengths of its runs of equal columns
 // (duplicate edges, a self-loop's two arcs).  The mode -- longest run, ties to the
 // smallest label -- is a segmented max over the arc stream, with no hash table.
-// A wave takes 512-arc tiles (8 chunks of 64 lanes): run lengths from a ballot of
-// the run starts, a per-row segmented max scan by shuffles, carries from chunk to
-// chunk; a row inside the tile is written directly, a row crossing a tile boundary
-// folds each piece into first_best[row] and k_first_final writes it.
+// A wave takes 512-arc tiles (8 positions per lane); a row inside the tile is
+// written directly, a row crossing a tile boundary folds each piece into
+// first_best[row] and k_first_final writes it.
 // ---------------------------------------------------------------------------
 constexpr int kRunTile = 512;
 
@@ -2189,91 +2289,155 @@ __device__ __forceinline__ void seg_max_step(u64& w, int32_t r) {
   if (ro == r && wo > w) w = wo;
 }
 
-// Row ids come from the row-start bitmap (1 bit per arc; crow is read once per tile):
-// the row of position i is crow[t0] + the number of row starts in (t0, i].  Rows are
-// degree-sorted, so every row between two rows with arcs has arcs too.
+// Inclusive wave scans in DPP: row_shr 1/2/4/8 inside each 16-lane row, then the
+// row broadcasts of lanes 15 and 31 (lanes without a source combine the identity).
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, kCtrl, kRowMask, 0xF, false);
+}
+__device__ __forceinline__ int wave_incl_add(int v) {
+  v += dpp_i<0x111>(0, v);
+  v += dpp_i<0x112>(0, v);
+  v += dpp_i<0x114>(0, v);
+  v += dpp_i<0x118>(0, v);
+  v += dpp_i<0x142, 0xA>(0, v);
+  v += dpp_i<0x143, 0xC>(0, v);
+  return v;
+}
+__device__ __forceinline__ int wave_incl_max(int v) {
+  constexpr int kMin = (int)0x80000000;
+  v = max(v, dpp_i<0x111>(kMin, v));
+  v = max(v, dpp_i<0x112>(kMin, v));
+  v = max(v, dpp_i<0x114>(kMin, v));
+  v = max(v, dpp_i<0x118>(kMin, v));
+  v = max(v, dpp_i<0x142, 0xA>(kMin, v));
+  v = max(v, dpp_i<0x143, 0xC>(kMin, v));
+  return v;
+}
+
+// Lane-sequential layout: lane l of a wave owns positions t0 + 8 l .. t0 + 8 l + 7 of
+// its 512-arc tile (two 16-B loads), walks them in registers (run lengths, the row's
+// running maximum, rows that start and end inside the lane written at once), and
+// only the lane-crossing parts go through cross-lane scans -- three per tile instead
+// of a segmented scan per 64 arcs (the per-arc-lane form was VALU-bound: ~190
+// instructions per 64 arcs, 1.34 ms at C3 against 0.27 ms of al[] stream).
+//   row ids   crow[t0] + the row starts in (t0, p] (a prefix sum of the lanes' start
+//             counts from the row-start bitmap; crow is read once per tile)
+//   runs      a run starts at a row start or a label change; the run in progress at
+//             a lane's first position started at the last run start of the lanes
+//             before (a max scan), or ck positions before the tile
+//   rows      a row ending inside the lane after starting in it is complete; the
+//             lane's first and last segments combine with their neighbours through a
+//             segmented (by row) max scan of the lanes' last segments
+// Positions at or past arcs count as row starts (so the last row ends at arcs - 1) and
+// hold no votes: their empty segments write nothing.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ al,
                                                     const int32_t* __restrict__ crow,
                                                     const u64* __restrict__ rstart, int64_t arcs,
                                                     int32_t* __restrict__ Ln, u64* __restrict__ best) {
+  constexpr int kP = kRunTile / 64;  // positions per lane
+  static_assert(kP == 8, "one bitmap byte per lane");
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   for (int64_t t0 = ((int64_t)blockIdx.x * 4 + wv) * kRunTile; t0 < arcs; t0 += nw * kRunTile) {
     const int64_t t1 = t0 + kRunTile < arcs ? t0 + kRunTile : arcs;
-    constexpr int kC = kRunTile / 64;
-    // the tile's labels first (every load in flight before the first chunk's scan)
-    u32 aa[kC];
+    const int64_t p0 = t0 + kP * lane;
+    u32 a[kP];
+    if (p0 + kP <= t1) {
+      const v4i_t* q = reinterpret_cast<const v4i_t*>(al + p0);  // 32-B aligned: t0 % 512 == 0
+      const v4i_t x = __builtin_nontemporal_load(q), y = __builtin_nontemporal_load(q + 1);
+      a[0] = (u32)x.x; a[1] = (u32)x.y; a[2] = (u32)x.z; a[3] = (u32)x.w;
+      a[4] = (u32)y.x; a[5] = (u32)y.y; a[6] = (u32)y.z; a[7] = (u32)y.w;
+    } else {
 #pragma unroll
-    for (int c = 0; c < kC; ++c) {
-      const int64_t i = t0 + c * 64 + lane;
-      aa[c] = i < t1 ? (u32)__builtin_nontemporal_load(al + i) : kNone;
+      for (int j = 0; j < kP; ++j) a[j] = p0 + j < t1 ? (u32)al[p0 + j] : kNone;
     }
-    // row-start words of the tile (wave-uniform) and the first word of the next tile
-    const int64_t wb = t0 >> 6;
-    u64 W[kC];
-#pragma unroll
-    for (int c = 0; c < kC; ++c) W[c] = rstart[wb + c];
-    // a row ends at the tile's last position when the next tile starts one (a partial
-    // last tile ends its last row at position arcs - 1, tested per lane below)
-    const u64 wnext = t1 < arcs ? rstart[wb + kC] : 1ull;
+    // row-start bits of the lane's positions (bit j: p0 + j), positions >= arcs set
+    u32 sb = (u32)(rstart[(t0 >> 6) + (lane >> 3)] >> ((lane & 7) * 8)) & 0xFFu;
+    const int64_t dead = p0 + kP - arcs;
+    if (dead > 0) sb |= dead >= kP ? 0xFFu : (0xFFu << (kP - (int)dead)) & 0xFFu;
+    // does position p0 + kP start a row (the next lane's bit 0; lane 63: the next tile's)
+    const int tile_next = t0 + kRunTile >= arcs ? 1 : (int)(rstart[(t0 >> 6) + kP] & 1ull);
+    const bool ends = (dpp_i<0x130>(tile_next, (int)(sb & 1u)) & 1) != 0;  // wave_shl:1
+    // carries from before the tile: row, label and (a run continuing into it) length
     const int32_t r_t0 = crow[t0];
-    // carry: row, label, run length and row maximum at the position before the chunk
-    // (the row maximum starts at 0 in a tile: the previous tile folded its part)
-    int32_t cr = -1;
+    int32_t r_before = -1;
     u32 ca = kNone, ck = 0u;
-    u64 cw = 0ull;
     if (t0 > 0) {
-      cr = crow[t0 - 1];
+      r_before = crow[t0 - 1];
       ca = (u32)al[t0 - 1];
-      if (r_t0 == cr && (u32)al[t0] == ca) {
-        // a run continues into the tile (rare): its length up to t0 - 1
-        int64_t k = 1;
-        while (t0 - 1 - k >= 0 && crow[t0 - 1 - k] == cr && (u32)al[t0 - 1 - k] == ca) ++k;
+      if (r_t0 == r_before && (u32)__builtin_amdgcn_readfirstlane((int)a[0]) == ca) {
+        int64_t k = 1;  // a run continues into the tile (rare): its length up to t0 - 1
+        while (t0 - 1 - k >= 0 && crow[t0 - 1 - k] == r_before && (u32)al[t0 - 1 - k] == ca) ++k;
         ck = (u32)k;
       }
     }
-    // rows are contiguous, so a row started inside the tile iff it differs from the row
-    // before the tile
-    const int32_t r_before = cr;
-    int32_t rbase = r_t0;   // row of the chunk's first position, minus its own start bit
+    // row of the position before the lane (lane 0: position t0's row; its start bit
+    // is not a new row inside the tile)
+    const u32 sbr = lane == 0 ? (sb & ~1u) : sb;
+    const int nst = __popc(sbr);
+    int32_t rr = r_t0 + wave_incl_add(nst) - nst;
+    // run starts, and where the run in progress at the lane's first position started
+    // (relative to t0; lane 0 without a start of its own: -ck)
+    const u32 aprev = (u32)dpp_i<0x138>((int)ca, (int)a[kP - 1]);  // wave_shr:1
+    u32 rsb = sb;
+    rsb |= a[0] != aprev ? 1u : 0u;
 #pragma unroll
-    for (int c = 0; c < kC; ++c) {
-      const int64_t i = t0 + c * 64 + lane;
-      const bool live = i < t1;  // every lane runs every shuffle
-      // starts after t0 only (position t0 is row r_t0 whatever its bit)
-      const u64 wc = c == 0 ? (W[0] & ~1ull) : W[c];
-      const int32_t r = rbase + (int32_t)__popcll(wc & upto);
-      const u32 a = aa[c];
-      // lane - 1's label (DPP wave_shr:1; lane 0 takes the carry)
-      const u32 aprev = (u32)__builtin_amdgcn_update_dpp((int)ca, (int)a, 0x138, 0xF, 0xF, false);
-      const u64 starts = W[c] | __ballot(a != aprev);
-      const u64 m = starts & upto;
-      const u32 k = m ? (u32)(lane - (63 - __clzll((long long)m)) + 1) : (u32)lane + 1u + ck;
-      u64 w = live ? (((u64)k << 32) | (u64)(~a)) : 0ull;
-      if (r == cr && cw > w) w = cw;
-      seg_max_step<0x111, 0xF>(w, r);  // row_shr:1
-      seg_max_step<0x112, 0xF>(w, r);  // row_shr:2
-      seg_max_step<0x114, 0xF>(w, r);  // row_shr:4
-      seg_max_step<0x118, 0xF>(w, r);  // row_shr:8
-      seg_max_step<0x142, 0xA>(w, r);  // row_bcast:15 into rows 1, 3
-      seg_max_step<0x143, 0xC>(w, r);  // row_bcast:31 into rows 2, 3
-      // the row ends at i iff position i + 1 starts a row (the next chunk's / tile's bit 0)
-      const u64 nb = c + 1 < kC ? (W[c + 1 < kC ? c + 1 : c] & 1ull) : (wnext & 1ull);
-      const u64 ends = (W[c] >> 1) | (nb << 63);
-      if (live && (((ends >> lane) & 1ull) || i + 1 == arcs)) {  // the row ends at i
-        if (r != r_before) Ln[r] = (int32_t)(~(u32)w);
-        else atomicMax(&best[r], w);
-      } else if (live && i + 1 == t1) {
-        atomicMax(&best[r], w);  // continues in the next tile
+    for (int j = 1; j < kP; ++j) rsb |= a[j] != a[j - 1] ? (1u << j) : 0u;
+    const int pl = kP * lane;
+    const int last_rs = rsb ? pl + 31 - __clz(rsb) : (lane == 0 ? -(int)ck : (int)0x80000000);
+    int cur = dpp_i<0x138>(-(int)ck, wave_incl_max(last_rs));
+    // the lane's positions in order
+    u64 acc = 0ull, fw = 0ull;
+    bool multi = false;  // a segment ended inside the lane: fw holds the first one
+    int32_t rfirst = 0;
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      if ((sbr >> j) & 1u) {
+        if (j > 0) {
+          if (!multi) {
+            fw = acc;
+            multi = true;
+          } else if (acc) {
+            Ln[rr] = (int32_t)(~(u32)acc);  // started and ended inside the lane
+          }
+        }
+        ++rr;
+        acc = 0ull;
       }
-      rbase += (int32_t)__popcll(wc);
-      cr = __builtin_amdgcn_readlane(r, 63);
-      ca = (u32)__builtin_amdgcn_readlane((int)a, 63);
-      ck = (u32)__builtin_amdgcn_readlane((int)k, 63);
-      cw = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(w >> 32), 63) << 32) |
-           (u64)(u32)__builtin_amdgcn_readlane((int)(u32)w, 63);
+      if (j == 0) rfirst = rr;
+      if ((rsb >> j) & 1u) cur = pl + j;
+      if (a[j] != kNone) {
+        const u64 w = ((u64)(u32)(pl + j - cur + 1) << 32) | (u64)(~a[j]);
+        acc = w > acc ? w : acc;
+      }
+    }
+    // segmented (by row) inclusive max of the lanes' last segments
+    u64 T = acc;
+    seg_max_step<0x111, 0xF>(T, rr);
+    seg_max_step<0x112, 0xF>(T, rr);
+    seg_max_step<0x114, 0xF>(T, rr);
+    seg_max_step<0x118, 0xF>(T, rr);
+    seg_max_step<0x142, 0xA>(T, rr);
+    seg_max_step<0x143, 0xC>(T, rr);
+    // the lane's first segment, ended inside the lane: plus the lanes before in its row
+    const int32_t rprev = dpp_i<0x138>((int)0x80000000, rr);
+    const u32 tlo = (u32)dpp_i<0x138>(0, (int)(u32)T), thi = (u32)dpp_i<0x138>(0, (int)(u32)(T >> 32));
+    if (multi) {
+      const u64 tp = ((u64)thi << 32) | tlo;
+      const u64 v = rprev == rfirst && tp > fw ? tp : fw;
+      if (v) {
+        if (rfirst == r_before) atomicMax(&best[rfirst], v);  // started before the tile
+        else Ln[rfirst] = (int32_t)(~(u32)v);
+      }
+    }
+    // the lane's last segment: ends at the lane's end, or (lane 63) continues in the
+    // next tile
+    if (T && (ends || lane == 63)) {
+      if (!ends || rr == r_before) atomicMax(&best[rr], T);
+      else Ln[rr] = (int32_t)(~(u32)T);
     }
   }
 }
@@ -2625,12 +2789,12 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     const unsigned gb = cap_grid((ngrp + 3) / 4, 4096), gr = cap_grid((g->arcs + 2047) / 2048, 8192);
     if (if_wanted) {
       hipLaunchKernelGGL(k_giant_bits<true>, dim3(gb), dim3(256), 0, s, ctr, thr, L, g->vpad, g->gword,
-                         (unsigned long long*)g->gbits);
+                         (unsigned long long*)g->gbits, g->abits, (int64_t)0);
       hipLaunchKernelGGL(k_al_rebuild_small<true>, dim3(gr), dim3(256), 0, s, ctr, thr, g->col, g->arcs, L, g->al,
                          g->gbits, g->vpad, g->gword, g->abits);
     } else {
       hipLaunchKernelGGL(k_giant_bits<false>, dim3(gb), dim3(256), 0, s, ctr, thr, L, g->vpad, g->gword,
-                         (unsigned long long*)g->gbits);
+                         (unsigned long long*)g->gbits, g->abits, (int64_t)0);
       hipLaunchKernelGGL(k_al_rebuild_small<false>, dim3(gr), dim3(256), 0, s, ctr, thr, g->col, g->arcs, L, g->al,
                          g->gbits, g->vpad, g->gword, g->abits);
     }
@@ -2651,19 +2815,26 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     // the giant-label bitmap of L first (same wanted-check: both return at once when
     // the scatter refreshes instead)
     const int64_t ngrp = (g->vpad + 511) / 512;
+    // class-blocked labels-mode rebuild (P = 1): a grid of whole 8-block groups
+    const bool blk = !ranked && g->blk_pieces && g->blk_a0 > 0 && dev_cus >= 8;
+    if (blk) dev_cus &= ~7;
+    const int64_t nzero = blk ? g->blk_a0 / 64 : 0;
     if (if_wanted)
       hipLaunchKernelGGL(k_giant_bits<true>, dim3(cap_grid((ngrp + 3) / 4, 4096)), dim3(256), 0, s, ctr, thr, L,
-                         g->vpad, g->gword, (unsigned long long*)g->gbits);
+                         g->vpad, g->gword, (unsigned long long*)g->gbits, g->abits, nzero);
     else
       hipLaunchKernelGGL(k_giant_bits<false>, dim3(cap_grid((ngrp + 3) / 4, 4096)), dim3(256), 0, s, ctr, thr, L,
-                         g->vpad, g->gword, (unsigned long long*)g->gbits);
+                         g->vpad, g->gword, (unsigned long long*)g->gbits, g->abits, nzero);
     LPA_HIP(hipGetLastError());
     // ranked without a usable bit share: nbits 0 keeps every block in labels mode
     const int64_t nbits = (ranked && hb_lg == 0) ? 0 : g->vpad;
+    BlkInfo binfo;
+    for (int x = 0; x < 9; ++x) binfo.off[x] = g->blk_off[x];
+    binfo.a0 = blk ? g->blk_a0 : 0;
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
                      g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \
-                     g->rebuild_hybrid)
+                     g->rebuild_hybrid, blk ? g->blk_pieces : nullptr, binfo)
     if (if_wanted) {
       if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
     } else {

@@ -80,6 +80,9 @@ typedef struct lpa_graph_info {
   int64_t exchanges_delta; /* P > 1: label exchanges done as changed-label deltas */
   int64_t exchanges_giant; /* P > 1: label exchanges done giant-compressed (bitmap of the
                               giant label + changed non-giant labels) */
+  int64_t blocked_rows;    /* P = 1: rows whose columns are in (class, column) order for
+                              the class-blocked al[] rebuild (0: off, LPA_BLOCK_DEG)  */
+  int64_t blocked_pieces;  /* ... and the rebuild's piece-list length                */
 } lpa_graph_info;
 
 /* Outlier summary. */

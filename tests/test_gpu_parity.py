@@ -629,3 +629,38 @@ def test_quality_matches_numpy(gfa, golden, graph):
         assert g.quality(dl) == g.quality(lab)
         with pytest.raises(ValueError, match="int32"):
             g.quality(torch.arange(V, device="cuda"))
+
+
+@pytest.fixture(scope="module")
+def rmat22(gfa, oracle):
+    s, d = gfa.gen_rmat(22, 16, seed=11)
+    sn, dn = s.cpu().numpy(), d.cpu().numpy()
+    _, hist, _ = oracle.lpa(1 << 22, sn, dn, 5, per_iter=True)
+    return sn, dn, hist
+
+
+@pytest.mark.parametrize("env", [{"LPA_BLOCK_DEG": "0"}, {"LPA_BLOCK_DEG": "8"}, {"LPA_BLOCK_DEG": "64"},
+                                 {"LPA_BLOCK_DEG": "1000"}, {"LPA_BLOCK_DEG": "64", "LPA_LOCALITY": "0"},
+                                 {"LPA_BLOCK_DEG": "64", "LPA_REBUILD_HYBRID": "1"}])
+def test_class_blocked_rebuild_bit_exact(gfa, rmat22, monkeypatch, env):
+    """The class-blocked labels-mode al[] rebuild (rows of degree > LPA_BLOCK_DEG in
+    (class, column) order, per-XCD class pieces + the plain stream below; its arc giant
+    bits ORed piecewise): R-MAT-22 (4 M slots, the LDS hot-set rebuild) bit-exact against
+    the oracle at supersteps 1..5 -- superstep 1's column runs over the reordered rows,
+    the labels-/hybrid-mode rebuild after it, superstep 2's settles from its arc bits."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sn, dn, hist = rmat22
+    V = 1 << 22
+    with gfa.Graph(sn, dn, V) as g:
+        info = g.info()
+        if env["LPA_BLOCK_DEG"] == "0":
+            assert info["blocked_rows"] == 0
+        else:
+            assert info["blocked_rows"] > 0 and info["blocked_pieces"] % 8 == 0, info
+        for t in range(5):
+            g.step(1)
+            bad = int((g.labels() != hist[t]).sum())
+            assert bad == 0, f"{env} superstep {t + 1}: {bad} labels differ"
+        g.reset()
+        assert np.array_equal(g.run(5), hist[4]), f"{env} lpa_run(5) after reset"
