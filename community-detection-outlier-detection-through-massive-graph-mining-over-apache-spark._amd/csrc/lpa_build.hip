@@ -789,7 +789,8 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     // class-blocked rows (P = 1 hot-set rebuild sizes; the class needs 3 key bits)
     g->cols_sorted = !g->pooled;
     int64_t H = 0;
-    if (P == 1 && g->cols_sorted && g->block_deg > 0 && g->vpad >= kHotMinSlots && blo + 3 <= 32) {
+    if (P == 1 && g->cols_sorted && g->block_deg > 0 && g->vpad >= kHotMinSlots &&
+        g->vpad >= g->block_min_slots && blo + 3 <= 32) {
       int64_t* d_h = nullptr;
       LPA_TRY(scratch_alloc(g, (void**)&d_h, sizeof(int64_t)));
       LPA_HIP(hipMemsetAsync(d_h, 0, sizeof(int64_t), s));

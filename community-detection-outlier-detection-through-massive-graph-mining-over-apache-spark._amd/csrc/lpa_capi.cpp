@@ -165,6 +165,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
   if (const char* f = getenv("LPA_REBUILD_HYBRID")) g->rebuild_hybrid = atoi(f);
   if (const char* f = getenv("LPA_BLOCK_DEG")) g->block_deg = atoi(f);
+  if (const char* f = getenv("LPA_BLOCK_MIN_SLOTS")) g->block_min_slots = atoll(f);
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;

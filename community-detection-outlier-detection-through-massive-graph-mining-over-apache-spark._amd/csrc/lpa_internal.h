@@ -59,9 +59,11 @@ constexpr double kFrontierFrac = 0.005;
 // P = 1 label vectors of at least this many slots take the LDS hot-set rebuild
 // (k_al_rebuild_hot); smaller ones stay in L2 / the Infinity Cache (k_al_rebuild_small)
 constexpr int64_t kHotMinSlots = 4ll << 20;
-// column class of the class-blocked rebuild: the 128-B line (32 slots) of the column's
-// label, mod 8
-__host__ __device__ inline uint32_t col_class(int32_t c) { return ((uint32_t)c >> 5) & 7u; }
+// column class of the class-blocked rebuild: the 4-KB chunk (1024 slots) of the column's
+// label, mod 8.  (Line-interleaved classes, (c >> 5) & 7, fixed address bits 7-9 of an
+// XCD's gathers and crowded them onto a few L2 channels: 2.5x fewer bytes fetched than
+// the plain stream, yet 1.5x its time.)
+__host__ __device__ inline uint32_t col_class(int32_t c) { return ((uint32_t)c >> 10) & 7u; }
 
 struct Segment {   // one unit of a seg-bin row
   int64_t begin;  // first arc (local CSR index)
@@ -231,10 +233,13 @@ struct lpa_graph {
                                             //   gathers + the arc giant bits, 1 also G from the bits
                                             //   of cold columns, 0 neither (LPA_REBUILD_HYBRID, A/B)
   // class-blocked labels-mode rebuild (P = 1, lpa_iter.hip rebuild_pieces): rows of
-  // degree > block_deg keep their columns in (class, column) order, class = column line
-  // (32 slots) mod 8; the class segments cut into <= 64-arc pieces, listed per class
+  // degree > block_deg keep their columns in (class, column) order (col_class); the
+  // class segments cut into <= 64-arc pieces, listed per class
   // (padded to multiples of 8) so that one block group (one XCD) gathers one class
-  int block_deg = 64;                       // LPA_BLOCK_DEG (0: off; a power of two)
+  int block_deg = 512;                      // LPA_BLOCK_DEG (0: off; a power of two)
+  int64_t block_min_slots = 32ll << 20;     // ... on label vectors of >= this many slots
+                                            //   (LPA_BLOCK_MIN_SLOTS): C5 176 -> 186 GTEPS,
+                                            //   but C3 (64 MB of labels) 0.9 ms slower
   lpa::u64* blk_pieces = nullptr;           // [n] (len << 32 | first position)
   int64_t blk_off[9] = {};                  // class x: pieces [blk_off[x], blk_off[x + 1])
   int64_t blk_a0 = 0;                       // arcs [0, blk_a0) are listed (a multiple of 512)

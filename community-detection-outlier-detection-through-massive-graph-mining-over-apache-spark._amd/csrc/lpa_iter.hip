@@ -1954,34 +1954,94 @@ __device__ __forceinline__ void rebuild_stream(Lab lab, int32_t G, bool bits, co
 // so each wave keeps three batches' dependent loads in flight instead of one batch's
 // chain (col -> bit word -> label).  Rings of 3 column sets and 2 word / label sets,
 // six steps unrolled so no set is copied while its loads are in flight.
+// The main loop is branch-free (every stage's batch exists, and p1 / p2 issue their
+// loads unconditionally, at a clamped address where the value is not needed): the
+// vector-memory counter is then tracked exactly, and waiting for batch t's labels does
+// not wait for the loads of batches t + 1 .. t + 3 -- with a conditional load in the
+// loop the compiler waited for every outstanding load (vmcnt(0)) at each step, which
+// serialised the pipeline.  The last few batches run guarded.
+//   fetch(t, c)  batch t's columns        probe(c, w)   p1 words
+//   resolve(c, w, r)  p2 labels          store(t, r)    stores (+ arc giant bits)
+template <typename Pre, typename F, typename Q, typename R, typename St>
+__device__ __forceinline__ void pipe3(int64_t nb, Pre pre, F fetch, Q probe, R resolve, St store) {
+  int32_t c0[8], c1[8], c2[8], r0[8], r1[8];
+  u32 w0[8], w1[8];
+  int64_t t = 0;
+  if (nb <= 0) return;
+  // pre(t, slot): batch t's descriptors (six slots, batch t in slot t mod 6), four
+  // steps ahead of its fetch
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k < nb) pre(k, k);
+  fetch(0, c0, 0);
+  if (nb > 1) fetch(1, c1, 1);
+  if (nb > 2) fetch(2, c2, 2);
+  probe(c0, w0);
+  if (nb > 1) probe(c1, w1);
+  resolve(c0, w0, r0);
+#define LPA_PIPE_STEP(GUARD, I, CA, CB, CC, WA, WB, RA, RB) \
+  if (t + 4 < nb) pre(t + 4, (I + 4) % 6);                \
+  if (!GUARD || t + 3 < nb) fetch(t + 3, CA, (I + 3) % 6); \
+  if (!GUARD || t + 2 < nb) probe(CC, WA);                 \
+  if (!GUARD || t + 1 < nb) resolve(CB, WB, RB);           \
+  store(t, RA, I);                                         \
+  ++t;                                                     \
+  if (GUARD && t >= nb) break;
+#define LPA_PIPE_CYCLE(GUARD)                                 \
+  LPA_PIPE_STEP(GUARD, 0, c0, c1, c2, w0, w1, r0, r1)        \
+  LPA_PIPE_STEP(GUARD, 1, c1, c2, c0, w1, w0, r1, r0)        \
+  LPA_PIPE_STEP(GUARD, 2, c2, c0, c1, w0, w1, r0, r1)        \
+  LPA_PIPE_STEP(GUARD, 3, c0, c1, c2, w1, w0, r1, r0)        \
+  LPA_PIPE_STEP(GUARD, 4, c1, c2, c0, w0, w1, r0, r1)        \
+  LPA_PIPE_STEP(GUARD, 5, c2, c0, c1, w1, w0, r1, r0)
+  while (t + 9 <= nb) {
+    LPA_PIPE_CYCLE(false)
+  }
+  while (true) {
+    LPA_PIPE_CYCLE(true)
+  }
+#undef LPA_PIPE_CYCLE
+#undef LPA_PIPE_STEP
+}
+
+// arc giant bits of one 64-lane chunk at arc position st (len lanes live, lanes
+// consecutive): one word, or two when st is not word-aligned (ORed: other chunks share
+// the words; nzero-ed by k_giant_bits beforehand)
+__device__ __forceinline__ void or_arc_bits(unsigned long long* __restrict__ abits, u32 st, unsigned long long m,
+                                            int lane) {
+  const u32 wd = st >> 6, off = st & 63u;
+  if (m && lane == 0) atomicOr(&abits[wd], m << off);
+  if (m && lane == 1 && off && (m >> (64u - off))) atomicOr(&abits[wd + 1], m >> (64u - off));
+}
+
+// the plain stream: this wave's whole 512-arc batches of [0, arcs), then the partial
+// last batch (one wave)
 template <typename P1, typename P2>
 __device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits, const int32_t* __restrict__ col,
                                              int64_t arcs, int32_t* __restrict__ al,
                                              unsigned long long* __restrict__ abits) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t step = nw * 512;
-  const int64_t nfull = arcs & ~(int64_t)511;
-  int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512;
-  auto L = [&](int32_t (&c)[8], int64_t b) {
-    if (b < nfull) {
+  const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nbatch = arcs >> 9;
+  const int64_t nb = wv < nbatch ? (nbatch - wv + nw - 1) / nw : 0;
+  auto base = [&](int64_t t) { return (wv + t * nw) * 512; };
+  auto pre = [](int64_t, int) {};
+  auto fetch = [&](int64_t t, int32_t (&c)[8], int) {
+    const int64_t b = base(t);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + b + k * 64 + lane);
-    }
+    for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + b + k * 64 + lane);
   };
-  auto Q1 = [&](const int32_t (&c)[8], u32 (&w)[8], int64_t b) {
-    if (b < nfull) {
+  auto probe = [&](const int32_t (&c)[8], u32 (&w)[8]) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) w[k] = p1(c[k]);
-    }
+    for (int k = 0; k < 8; ++k) w[k] = p1(c[k]);
   };
-  auto Q2 = [&](const int32_t (&c)[8], const u32 (&w)[8], int32_t (&r)[8], int64_t b) {
-    if (b < nfull) {
+  auto resolve = [&](const int32_t (&c)[8], const u32 (&w)[8], int32_t (&r)[8]) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) r[k] = p2(c[k], w[k]);
-    }
+    for (int k = 0; k < 8; ++k) r[k] = p2(c[k], w[k]);
   };
-  auto S = [&](const int32_t (&r)[8], int64_t b) {
+  auto store = [&](int64_t t, const int32_t (&r)[8], int) {
+    const int64_t b = base(t);
 #pragma unroll
     for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + b + k * 64 + lane);
     if (bits) {
@@ -1994,42 +2054,18 @@ __device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits,
       if (lane < 8) abits[(b >> 6) + lane] = mine;
     }
   };
-  int32_t c0[8], c1[8], c2[8], r0[8], r1[8];
-  u32 w0[8], w1[8];
-  if (base < nfull) {
-    L(c0, base);
-    L(c1, base + step);
-    L(c2, base + 2 * step);
-    Q1(c0, w0, base);
-    Q1(c1, w1, base + step);
-    Q2(c0, w0, r0, base);
-#define LPA_PIPE_STEP(CA, CB, CC, WA, WB, RA, RB) \
-    L(CA, base + 3 * step);                       \
-    Q1(CC, WA, base + 2 * step);                  \
-    Q2(CB, WB, RB, base + step);                  \
-    S(RA, base);                                  \
-    base += step;                                 \
-    if (base >= nfull) break;
-    while (true) {
-      LPA_PIPE_STEP(c0, c1, c2, w0, w1, r0, r1)
-      LPA_PIPE_STEP(c1, c2, c0, w1, w0, r1, r0)
-      LPA_PIPE_STEP(c2, c0, c1, w0, w1, r0, r1)
-      LPA_PIPE_STEP(c0, c1, c2, w1, w0, r1, r0)
-      LPA_PIPE_STEP(c1, c2, c0, w0, w1, r0, r1)
-      LPA_PIPE_STEP(c2, c0, c1, w1, w0, r1, r0)
-    }
-#undef LPA_PIPE_STEP
-  }
+  pipe3(nb, pre, fetch, probe, resolve, store);
   // the partial last batch (one wave)
-  if (nfull < arcs && base == nfull) {
+  const int64_t nfull = nbatch << 9;
+  if (nfull < arcs && wv == nbatch % nw) {
     for (int k = 0; k < 8; ++k) {
-      const int64_t i = base + k * 64 + lane;
+      const int64_t i = nfull + k * 64 + lane;
       const bool v = i < arcs;
       const int32_t c = v ? col[i] : 0;
-      const int32_t x = v ? p2(c, p1(c)) : 0;
+      const int32_t x = p2(c, p1(c));
       if (v) al[i] = x;
       const unsigned long long m = __ballot(v && x == G);
-      if (bits && lane == 0 && base + k * 64 < arcs) abits[(base >> 6) + k] = m;
+      if (bits && lane == 0 && nfull + k * 64 < arcs) abits[(nfull >> 6) + k] = m;
     }
   }
 }
@@ -2041,10 +2077,20 @@ __device__ __forceinline__ void rebuild_pipe(P1 p1, P2 p2, int32_t G, bool bits,
 // > block_deg, which keep their columns in (class, column) order -- so an XCD's gathers
 // touch 1/8 of the label lines and its L2 holds far more of them (C3, simulated: 0.18
 // -> 0.02 missing gathers per arc).  8 pieces (<= 64 arcs, lane-consecutive) per batch
-// and wave, in rebuild_pipe's three-stage pipeline; a piece's descriptor is re-read
-// (scalar, cached) where its positions are needed; a dead lane carries column -1.
-// bits: the arc giant bits, ORed into abits (a piece need not start a word; the words
-// were zeroed by k_giant_bits).
+// and wave, in pipe3's pipeline; a lane past its piece carries column 0 (a hot-set LDS
+// read) and stores nothing; the descriptors ride a register ring four batches ahead
+// (scalar loads in the stage that used them cost a round trip per step: the pieces
+// phase ran at ~7 us per batch and wave).  bits: the arc giant bits, ORed.
+#ifdef LPA_BLKTIME
+// diagnostic build only (csrc/Makefile blktime): per block of the last blocked rebuild,
+// the wall clock at its start, after its pieces and at its end
+__device__ unsigned long long g_blk_time[3 * 512];
+extern "C" int lpa_diag_blk_times(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_time), sizeof(g_blk_time)) != hipSuccess) return -1;
+  static unsigned long long zero[3 * 512];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_blk_time), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 struct BlkInfo {
   int64_t off[9];  // class x: pieces [off[x], off[x + 1]), multiples of 8
   int64_t a0;      // listed arcs [0, a0) (0: no blocked part)
@@ -2055,70 +2101,62 @@ __device__ __forceinline__ void rebuild_pieces(P1 p1, P2 p2, int32_t G, bool bit
                                                const int32_t* __restrict__ col, int32_t* __restrict__ al,
                                                unsigned long long* __restrict__ abits) {
   const int lane = threadIdx.x & 63;
-  const int64_t step = nwv * 8;
-  int64_t q = q0 + wi * 8;
-  auto L = [&](int32_t (&c)[8], int64_t qq) {
-    if (qq < q1) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const u64 d = pieces[qq + k];
-        c[k] = lane < (int)(d >> 32) ? __builtin_nontemporal_load(col + (u32)d + lane) : -1;
-      }
-    }
+  auto uni = [](int64_t v) -> int64_t {
+    return (int64_t)(((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)((u64)v >> 32)) << 32) |
+                     (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)v));
   };
-  auto Q1 = [&](const int32_t (&c)[8], u32 (&w)[8], int64_t qq) {
-    if (qq < q1) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) w[k] = c[k] >= 0 ? p1(c[k]) : 0u;
-    }
+  const int64_t step = uni(nwv * 8), first = uni(q0 + wi * 8), last = uni(q1);
+  const int64_t nb = first < last ? (last - first + step - 1) / step : 0;
+  // descriptor ring: lane k < 8 of slot j holds piece k of the batch in slot j, loaded
+  // four steps ahead (a vector load, so waiting for it never waits on newer loads);
+  // the stages read it with readlane
+  u64 dr[6];
+  auto pre = [&](int64_t t, int j) {
+    const int64_t qq = first + t * step;
+    dr[j] = lane < 8 ? pieces[qq + lane] : 0ull;
   };
-  auto Q2 = [&](const int32_t (&c)[8], const u32 (&w)[8], int32_t (&r)[8], int64_t qq) {
-    if (qq < q1) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) r[k] = c[k] >= 0 ? p2(c[k], w[k]) : 0;
-    }
+  auto desc = [&](int j, int k) -> u64 {
+    return ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(dr[j] >> 32), k) << 32) |
+           (u64)(u32)__builtin_amdgcn_readlane((int)(u32)dr[j], k);
   };
-  auto S = [&](const int32_t (&r)[8], int64_t qq) {
+  auto fetch = [&](int64_t, int32_t (&c)[8], int j) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const u64 d = pieces[qq + k];
-      const int ln = (int)(d >> 32);
-      const u32 st = (u32)d;
-      if (lane < ln) __builtin_nontemporal_store(r[k], al + st + lane);
-      if (bits) {
-        const unsigned long long m = __ballot(lane < ln && r[k] == G);
-        const u32 wd = st >> 6, off = st & 63u;
-        if (m && lane == 0) atomicOr(&abits[wd], m << off);
-        if (m && lane == 1 && off && (m >> (64u - off))) atomicOr(&abits[wd + 1], m >> (64u - off));
-      }
+      const u64 d = desc(j, k);
+      const bool live = lane < (int)(d >> 32);
+#if defined(LPA_BLK_ABL) && LPA_BLK_ABL == 3
+      const int32_t x = (int32_t)(((u32)d + lane) * 2654435761u >> 8);  // ablation: no column loads
+#else
+      const int32_t x = __builtin_nontemporal_load(col + (u32)d + (live ? lane : 0));
+#endif
+      c[k] = live ? x : 0;
     }
   };
-  int32_t c0[8], c1[8], c2[8], r0[8], r1[8];
-  u32 w0[8], w1[8];
-  if (q < q1) {
-    L(c0, q);
-    L(c1, q + step);
-    L(c2, q + 2 * step);
-    Q1(c0, w0, q);
-    Q1(c1, w1, q + step);
-    Q2(c0, w0, r0, q);
-#define LPA_PIECE_STEP(CA, CB, CC, WA, WB, RA, RB) \
-    L(CA, q + 3 * step);                           \
-    Q1(CC, WA, q + 2 * step);                      \
-    Q2(CB, WB, RB, q + step);                      \
-    S(RA, q);                                      \
-    q += step;                                     \
-    if (q >= q1) break;
-    while (true) {
-      LPA_PIECE_STEP(c0, c1, c2, w0, w1, r0, r1)
-      LPA_PIECE_STEP(c1, c2, c0, w1, w0, r1, r0)
-      LPA_PIECE_STEP(c2, c0, c1, w0, w1, r0, r1)
-      LPA_PIECE_STEP(c0, c1, c2, w1, w0, r1, r0)
-      LPA_PIECE_STEP(c1, c2, c0, w0, w1, r0, r1)
-      LPA_PIECE_STEP(c2, c0, c1, w1, w0, r1, r0)
+  // the probe word is read where it is used (an LDS read in the labels / hybrid modes
+  // this path serves): no word ring, 16 VGPRs fewer
+  auto probe = [&](const int32_t (&)[8], u32 (&)[8]) {};
+  auto resolve = [&](const int32_t (&c)[8], const u32 (&)[8], int32_t (&r)[8]) {
+#pragma unroll
+#if defined(LPA_BLK_ABL) && LPA_BLK_ABL == 1
+    for (int k = 0; k < 8; ++k) r[k] = c[k];  // ablation: no label gathers
+#else
+    for (int k = 0; k < 8; ++k) r[k] = p2(c[k], p1(c[k]));
+#endif
+  };
+  auto store = [&](int64_t, const int32_t (&r)[8], int j) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u64 d = desc(j, k);
+      const int ln = (int)(d >> 32);
+#if defined(LPA_BLK_ABL) && LPA_BLK_ABL == 2
+      if (lane < ln && r[k] == -7) al[(u32)d + lane] = 0;  // ablation: no stores
+#else
+      if (lane < ln) __builtin_nontemporal_store(r[k], al + (u32)d + lane);
+      if (bits) or_arc_bits(abits, (u32)d, __ballot(lane < ln && r[k] == G), lane);
+#endif
     }
-#undef LPA_PIECE_STEP
-  }
+  };
+  pipe3(nb, pre, fetch, probe, resolve, store);
 }
 
 // al[] rebuild with an LDS hot set (the slots of the highest-degree vertices: at P = 1
@@ -2206,25 +2244,68 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
   if constexpr (kRanked) {
     rebuild_stream(lab, G, bits, col, arcs, al, abits);
   } else {
-    auto p1 = [&](int c) -> u32 {
-      if (bits) return (u32)c < (u32)nhb ? hot[(u32)c >> 5] : gbits[(u32)c >> 5];
-      if (hyb_bits) return (u32)c < nh ? hot[c] : gbits[(u32)c >> 5];
-      return (u32)c < nh ? hot[c] : 0u;
+    // branch-free probes (pipe3): both sources are read -- the LDS word at a clamped
+    // index, the gbits word / the label at a fixed address where it is not needed (the
+    // wave's lanes then share one line)
+    const u32 nhbu = (u32)nhb;
+    auto run = [&](auto p1, auto p2, bool wbits) {
+      if (!bits && pieces) {  // uniform: labels / hybrid mode of a blocked handle
+        const int grp = blockIdx.x & 7;
+        const int64_t nwv = (int64_t)(gridDim.x >> 3) * (blockDim.x >> 6);
+        const int64_t wi = (int64_t)(blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+#ifdef LPA_BLKTIME
+        if (threadIdx.x == 0 && blockIdx.x < 512) g_blk_time[3 * blockIdx.x] = wall_clock64();
+#endif
+        rebuild_pieces(p1, p2, G, wbits, pieces, blk.off[grp], blk.off[grp + 1], wi, nwv, col, al, abits);
+#ifdef LPA_BLKTIME
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 512) atomicMax(&g_blk_time[3 * blockIdx.x + 1], wall_clock64());
+#endif
+        // then every block: the plain stream over the rows below block_deg
+        rebuild_pipe(p1, p2, G, wbits, col + blk.a0, arcs - blk.a0, al + blk.a0, abits + blk.a0 / 64);
+#ifdef LPA_BLKTIME
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 512) atomicMax(&g_blk_time[3 * blockIdx.x + 2], wall_clock64());
+#endif
+      } else {
+        rebuild_pipe(p1, p2, G, wbits, col, arcs, al, abits);
+      }
     };
-    auto p2 = [&](int c, u32 w) -> int32_t {
-      if (bits) return ((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c];
-      if (hyb_bits) return (u32)c < nh ? (int32_t)w : (((w >> ((u32)c & 31u)) & 1u) ? G : Ln[c]);
-      return (u32)c < nh ? (int32_t)w : Ln[c];
-    };
-    if (!bits && pieces) {  // uniform: labels / hybrid mode of a blocked handle
-      const int grp = blockIdx.x & 7;
-      const int64_t nwv = (int64_t)(gridDim.x >> 3) * (blockDim.x >> 6);
-      const int64_t wi = (int64_t)(blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-      rebuild_pieces(p1, p2, G, hyb, pieces, blk.off[grp], blk.off[grp + 1], wi, nwv, col, al, abits);
-      // then every block: the plain stream over the rows below block_deg
-      rebuild_pipe(p1, p2, G, hyb, col + blk.a0, arcs - blk.a0, al + blk.a0, abits + blk.a0 / 64);
+    if (bits) {
+      run(
+          [&](int c) -> u32 {
+            const bool h = (u32)c < nhbu;
+            const u32 hw = hot[(h ? (u32)c : nhbu - 1u) >> 5];
+            const u32 gw = gbits[h ? 0u : (u32)c >> 5];
+            return h ? hw : gw;
+          },
+          [&](int c, u32 w) -> int32_t {
+            const bool g = (w >> ((u32)c & 31u)) & 1u;
+            const int32_t x = Ln[g ? 0 : c];
+            return g ? G : x;
+          },
+          true);
+    } else if (hyb_bits) {
+      run(
+          [&](int c) -> u32 {
+            const bool h = (u32)c < nh;
+            const u32 hw = hot[h ? (u32)c : nh - 1u];
+            const u32 gw = gbits[h ? 0u : (u32)c >> 5];
+            return h ? hw : gw;
+          },
+          [&](int c, u32 w) -> int32_t {
+            const bool h = (u32)c < nh;
+            const bool g = !h && ((w >> ((u32)c & 31u)) & 1u);
+            const int32_t x = Ln[(h || g) ? 0 : c];
+            return h ? (int32_t)w : (g ? G : x);
+          },
+          true);
     } else {
-      rebuild_pipe(p1, p2, G, bits || hyb, col, arcs, al, abits);
+      run([&](int c) -> u32 { return hot[(u32)c < nh ? (u32)c : nh - 1u]; },
+          [&](int c, u32 w) -> int32_t {
+            const bool h = (u32)c < nh;
+            const int32_t x = Ln[h ? 0 : c];
+            return h ? (int32_t)w : x;
+          },
+          hyb);
     }
   }
 }

@@ -648,6 +648,7 @@ def test_class_blocked_rebuild_bit_exact(gfa, rmat22, monkeypatch, env):
     bits ORed piecewise): R-MAT-22 (4 M slots, the LDS hot-set rebuild) bit-exact against
     the oracle at supersteps 1..5 -- superstep 1's column runs over the reordered rows,
     the labels-/hybrid-mode rebuild after it, superstep 2's settles from its arc bits."""
+    monkeypatch.setenv("LPA_BLOCK_MIN_SLOTS", "0")   # shipped: label vectors of >= 32 M slots
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     sn, dn, hist = rmat22
