@@ -158,12 +158,12 @@ __global__ void k_owned_degree(const int32_t* __restrict__ old_of_own,
 // class sits above the column's blo bits of the key
 __global__ void k_emit_arcs_single(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                    int64_t m, const int32_t* __restrict__ new_of,
-                                   u64* __restrict__ keys, int64_t H, int blo) {
+                                   u64* __restrict__ keys, int64_t H, int blo, u32 ncls) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m;
        e += (int64_t)gridDim.x * blockDim.x) {
     u64 s = (u32)new_of[src[e]], d = (u32)new_of[dst[e]];
-    const u64 cd = (int64_t)s < H ? (u64)col_class((int32_t)d) << blo : 0ull;
-    const u64 cs = (int64_t)d < H ? (u64)col_class((int32_t)s) << blo : 0ull;
+    const u64 cd = (int64_t)s < H ? (u64)col_class((int32_t)d, ncls) << blo : 0ull;
+    const u64 cs = (int64_t)d < H ? (u64)col_class((int32_t)s, ncls) << blo : 0ull;
     keys[2 * e] = (s << 32) | cd | d;
     keys[2 * e + 1] = (d << 32) | cs | s;
   }
@@ -181,8 +181,8 @@ __global__ void k_count_hub_rows(const int32_t* __restrict__ deg_own, int64_t S,
 // of row h with class >= x by binary search (the row is in (class, column) order), and
 // the segment's piece count (<= 64 arcs each)
 __global__ void k_class_segments(const int64_t* __restrict__ rp, const int32_t* __restrict__ col, int64_t H,
-                                 uint32_t* __restrict__ seg_start, int32_t* __restrict__ npieces) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 8 * H;
+                                 u32 ncls, uint32_t* __restrict__ seg_start, int32_t* __restrict__ npieces) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)ncls * H;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t x = i / H, h = i - x * H;
     const int64_t b = rp[h], e = rp[h + 1];
@@ -190,25 +190,25 @@ __global__ void k_class_segments(const int64_t* __restrict__ rp, const int32_t* 
       int64_t lo = b, hi = e;
       while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
-        if (col_class(col[mid]) < cls) lo = mid + 1;
+        if (col_class(col[mid], ncls) < cls) lo = mid + 1;
         else hi = mid;
       }
       return lo;
     };
-    const int64_t s0 = first_ge((uint32_t)x), s1 = x == 7 ? e : first_ge((uint32_t)x + 1);
+    const int64_t s0 = first_ge((uint32_t)x), s1 = x + 1 == (int64_t)ncls ? e : first_ge((uint32_t)x + 1);
     seg_start[i] = (uint32_t)s0;
     npieces[i] = (int32_t)((s1 - s0 + 63) / 64);
   }
 }
 
 __global__ void k_emit_pieces(const int64_t* __restrict__ rp, const uint32_t* __restrict__ seg_start,
-                              const int64_t* __restrict__ poff, int64_t H, const int64_t* __restrict__ base,
-                              u64* __restrict__ pieces) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 8 * H;
+                              const int64_t* __restrict__ poff, int64_t H, u32 ncls,
+                              const int64_t* __restrict__ base, u64* __restrict__ pieces) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)ncls * H;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t x = i / H, h = i - x * H;
     const int64_t s0 = seg_start[i];
-    const int64_t s1 = x == 7 ? rp[h + 1] : (int64_t)seg_start[i + H];
+    const int64_t s1 = x + 1 == (int64_t)ncls ? rp[h + 1] : (int64_t)seg_start[i + H];
     int64_t q = base[x] + (poff[i] - poff[x * H]);
     for (int64_t p = s0; p < s1; p += 64, ++q)
       pieces[q] = ((u64)(s1 - p < 64 ? s1 - p : 64) << 32) | (u64)p;
@@ -664,42 +664,44 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
 // the positions up to blk_a0, the 512-aligned start of the plain stream.
 int build_pieces(lpa_graph* g, int64_t H) {
   hipStream_t s = g->stream;
+  const int C = g->blk_classes;
   int64_t aH = 0;
   LPA_HIP(hipMemcpyAsync(&aH, g->rp + H, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   uint32_t* seg = nullptr;
   int32_t* np = nullptr;
   int64_t* poff = nullptr;
   int64_t* d_base = nullptr;
-  LPA_TRY(scratch_alloc(g, (void**)&seg, sizeof(uint32_t) * 8 * H));
-  LPA_TRY(scratch_alloc(g, (void**)&np, sizeof(int32_t) * 8 * H));
-  LPA_TRY(scratch_alloc(g, (void**)&poff, sizeof(int64_t) * (8 * H + 1)));
-  LPA_TRY(scratch_alloc(g, (void**)&d_base, sizeof(int64_t) * 8));
-  hipLaunchKernelGGL(k_class_segments, dim3(grid_for(8 * H)), dim3(256), 0, s, g->rp, g->col, H, seg, np);
+  LPA_TRY(scratch_alloc(g, (void**)&seg, sizeof(uint32_t) * C * H));
+  LPA_TRY(scratch_alloc(g, (void**)&np, sizeof(int32_t) * C * H));
+  LPA_TRY(scratch_alloc(g, (void**)&poff, sizeof(int64_t) * (C * H + 1)));
+  LPA_TRY(scratch_alloc(g, (void**)&d_base, sizeof(int64_t) * kMaxBlkClasses));
+  hipLaunchKernelGGL(k_class_segments, dim3(grid_for(C * H)), dim3(256), 0, s, g->rp, g->col, H, (u32)C, seg, np);
   LPA_HIP(hipGetLastError());
-  LPA_TRY(exclusive_scan_i32_i64(np, poff, 8 * H, s));
-  int64_t cum[9];
-  for (int x = 0; x <= 8; ++x)
+  LPA_TRY(exclusive_scan_i32_i64(np, poff, C * H, s));
+  int64_t cum[kMaxBlkClasses + 1];
+  for (int x = 0; x <= C; ++x)
     LPA_HIP(hipMemcpyAsync(&cum[x], poff + x * H, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   LPA_HIP(hipStreamSynchronize(s));
   int64_t a0 = (aH + 511) / 512 * 512;
   if (a0 > g->arcs) a0 = g->arcs;
   const int64_t ntail = (a0 - aH + 63) / 64;
-  int64_t base[8];
+  int64_t base[kMaxBlkClasses];
   g->blk_off[0] = 0;
-  for (int x = 0; x < 8; ++x) {
+  for (int x = 0; x < C; ++x) {
     base[x] = g->blk_off[x];
-    const int64_t n = cum[x + 1] - cum[x] + (x == 7 ? ntail : 0);
+    const int64_t n = cum[x + 1] - cum[x] + (x == C - 1 ? ntail : 0);
     g->blk_off[x + 1] = g->blk_off[x] + (n + 7) / 8 * 8;
   }
-  LPA_TRY(dev_alloc(g, (void**)&g->blk_pieces, sizeof(u64) * (g->blk_off[8] > 0 ? g->blk_off[8] : 1)));
-  LPA_HIP(hipMemsetAsync(g->blk_pieces, 0, sizeof(u64) * (g->blk_off[8] > 0 ? g->blk_off[8] : 1), s));
-  LPA_HIP(hipMemcpyAsync(d_base, base, sizeof(base), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_emit_pieces, dim3(grid_for(8 * H)), dim3(256), 0, s, g->rp, seg, poff, H, d_base,
+  const int64_t npc = g->blk_off[C] > 0 ? g->blk_off[C] : 1;
+  LPA_TRY(dev_alloc(g, (void**)&g->blk_pieces, sizeof(u64) * npc));
+  LPA_HIP(hipMemsetAsync(g->blk_pieces, 0, sizeof(u64) * npc, s));
+  LPA_HIP(hipMemcpyAsync(d_base, base, sizeof(int64_t) * C, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_emit_pieces, dim3(grid_for(C * H)), dim3(256), 0, s, g->rp, seg, poff, H, (u32)C, d_base,
                      g->blk_pieces);
   LPA_HIP(hipGetLastError());
   if (ntail > 0) {
     hipLaunchKernelGGL(k_tail_pieces, dim3(grid_for(ntail)), dim3(256), 0, s, aH, a0,
-                       base[7] + (cum[8] - cum[7]), g->blk_pieces);
+                       base[C - 1] + (cum[C] - cum[C - 1]), g->blk_pieces);
     LPA_HIP(hipGetLastError());
   }
   LPA_HIP(hipStreamSynchronize(s));
@@ -804,9 +806,19 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
       scratch_free(g, d_h);
     }
     g->blk_rows = H;
+    // classes: about one 4 MB L2's worth of labels each (8 per phase), at most
+    // kMaxBlkClasses, and the class bits must fit above the column's in the key half
+    int cb = 3;
+    while ((1ll << cb) * (4ll << 20) < g->vpad * 4 && (1 << (cb + 1)) <= kMaxBlkClasses && blo + cb + 1 <= 32)
+      ++cb;
+    if (g->block_classes_req >= 8)  // LPA_BLOCK_CLASSES (tests / A/B)
+      while ((1 << cb) < g->block_classes_req && (1 << (cb + 1)) <= kMaxBlkClasses && blo + cb + 1 <= 32) ++cb;
+    if (g->block_classes_req >= 8)
+      while ((1 << cb) > g->block_classes_req) --cb;
+    g->blk_classes = 1 << cb;
     if (P == 1) {
       hipLaunchKernelGGL(k_emit_arcs_single, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,
-                         g->e_dst, m, g->new_of, keys, H, blo);
+                         g->e_dst, m, g->new_of, keys, H, blo, (u32)g->blk_classes);
     } else {
       unsigned long long* cursor = nullptr;
       LPA_TRY(scratch_alloc(g, (void**)&cursor, sizeof(unsigned long long)));
@@ -822,7 +834,7 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     // columns.  No tally needs the order (a mode is order-free), so a pooled internal
     // graph (the outlier stage's 5-superstep L2 sub-graph) sorts by row only.
     if (g->cols_sorted)
-      for (int b = 0; b < blo + (H > 0 ? 3 : 0); b += 8) shifts[ns++] = b;
+      for (int b = 0; b < blo + (H > 0 ? cb : 0); b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(keys, keys + arcs, arcs, shifts, ns, s));
     LPA_TRY(dev_alloc(g, (void**)&g->crow, sizeof(int32_t) * arcs));

@@ -166,6 +166,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_REBUILD_HYBRID")) g->rebuild_hybrid = atoi(f);
   if (const char* f = getenv("LPA_BLOCK_DEG")) g->block_deg = atoi(f);
   if (const char* f = getenv("LPA_BLOCK_MIN_SLOTS")) g->block_min_slots = atoll(f);
+  if (const char* f = getenv("LPA_BLOCK_CLASSES")) g->block_classes_req = atoi(f);
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
@@ -567,7 +568,7 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->exchanges_delta = g->n_exch_delta;
   info->exchanges_giant = g->n_exch_giant;
   info->blocked_rows = g->blk_pieces ? g->blk_rows : 0;
-  info->blocked_pieces = g->blk_pieces ? g->blk_off[8] : 0;
+  info->blocked_pieces = g->blk_pieces ? g->blk_off[g->blk_classes] : 0;
   return LPA_OK;
 }
 

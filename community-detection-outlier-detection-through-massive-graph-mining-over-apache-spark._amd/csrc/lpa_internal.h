@@ -60,10 +60,13 @@ constexpr double kFrontierFrac = 0.005;
 // (k_al_rebuild_hot); smaller ones stay in L2 / the Infinity Cache (k_al_rebuild_small)
 constexpr int64_t kHotMinSlots = 4ll << 20;
 // column class of the class-blocked rebuild: the 4-KB chunk (1024 slots) of the column's
-// label, mod 8.  (Line-interleaved classes, (c >> 5) & 7, fixed address bits 7-9 of an
+// label, mod ncls.  (Line-interleaved classes, (c >> 5) & 7, fixed address bits 7-9 of an
 // XCD's gathers and crowded them onto a few L2 channels: 2.5x fewer bytes fetched than
 // the plain stream, yet 1.5x its time.)
-__host__ __device__ inline uint32_t col_class(int32_t c) { return ((uint32_t)c >> 10) & 7u; }
+// (ncls = 8 x phases classes: block group x streams classes x, x + 8, ... one phase after
+// another, so an XCD's gathers cover 1 / ncls of the label vector at a time)
+constexpr int kMaxBlkClasses = 32;
+__host__ __device__ inline uint32_t col_class(int32_t c, uint32_t ncls) { return ((uint32_t)c >> 10) & (ncls - 1u); }
 
 struct Segment {   // one unit of a seg-bin row
   int64_t begin;  // first arc (local CSR index)
@@ -241,7 +244,9 @@ struct lpa_graph {
                                             //   (LPA_BLOCK_MIN_SLOTS): C5 176 -> 186 GTEPS,
                                             //   but C3 (64 MB of labels) 0.9 ms slower
   lpa::u64* blk_pieces = nullptr;           // [n] (len << 32 | first position)
-  int64_t blk_off[9] = {};                  // class x: pieces [blk_off[x], blk_off[x + 1])
+  int blk_classes = 8;                      // 8 x phases (kMaxBlkClasses at most)
+  int block_classes_req = 0;                // LPA_BLOCK_CLASSES: force the class count (>= 8)
+  int64_t blk_off[lpa::kMaxBlkClasses + 1] = {}; // class x: pieces [blk_off[x], blk_off[x + 1])
   int64_t blk_a0 = 0;                       // arcs [0, blk_a0) are listed (a multiple of 512)
   int64_t blk_rows = 0;                     // rows in (class, column) order
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)

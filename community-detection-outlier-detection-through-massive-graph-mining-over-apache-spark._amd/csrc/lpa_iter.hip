@@ -2092,8 +2092,9 @@ extern "C" int lpa_diag_blk_times(unsigned long long* out) {
 }
 #endif
 struct BlkInfo {
-  int64_t off[9];  // class x: pieces [off[x], off[x + 1]), multiples of 8
-  int64_t a0;      // listed arcs [0, a0) (0: no blocked part)
+  int64_t off[kMaxBlkClasses + 1];  // class x: pieces [off[x], off[x + 1]), multiples of 8
+  int64_t a0;                       // listed arcs [0, a0) (0: no blocked part)
+  int phases;                       // classes / 8: group x streams x, x + 8, ...
 };
 template <typename P1, typename P2>
 __device__ __forceinline__ void rebuild_pieces(P1 p1, P2 p2, int32_t G, bool bits, const u64* __restrict__ pieces,
@@ -2256,7 +2257,9 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
 #ifdef LPA_BLKTIME
         if (threadIdx.x == 0 && blockIdx.x < 512) g_blk_time[3 * blockIdx.x] = wall_clock64();
 #endif
-        rebuild_pieces(p1, p2, G, wbits, pieces, blk.off[grp], blk.off[grp + 1], wi, nwv, col, al, abits);
+        for (int ph = 0; ph < blk.phases; ++ph)
+          rebuild_pieces(p1, p2, G, wbits, pieces, blk.off[grp + 8 * ph], blk.off[grp + 8 * ph + 1], wi, nwv,
+                         col, al, abits);
 #ifdef LPA_BLKTIME
         if ((threadIdx.x & 63) == 0 && blockIdx.x < 512) atomicMax(&g_blk_time[3 * blockIdx.x + 1], wall_clock64());
 #endif
@@ -2910,8 +2913,9 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     // ranked without a usable bit share: nbits 0 keeps every block in labels mode
     const int64_t nbits = (ranked && hb_lg == 0) ? 0 : g->vpad;
     BlkInfo binfo;
-    for (int x = 0; x < 9; ++x) binfo.off[x] = g->blk_off[x];
+    for (int x = 0; x <= kMaxBlkClasses; ++x) binfo.off[x] = g->blk_off[x];
     binfo.a0 = blk ? g->blk_a0 : 0;
+    binfo.phases = g->blk_classes / 8;
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
                      g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \

@@ -641,11 +641,13 @@ def rmat22(gfa, oracle):
 
 @pytest.mark.parametrize("env", [{"LPA_BLOCK_DEG": "0"}, {"LPA_BLOCK_DEG": "8"}, {"LPA_BLOCK_DEG": "64"},
                                  {"LPA_BLOCK_DEG": "1000"}, {"LPA_BLOCK_DEG": "64", "LPA_LOCALITY": "0"},
-                                 {"LPA_BLOCK_DEG": "64", "LPA_REBUILD_HYBRID": "1"}])
+                                 {"LPA_BLOCK_DEG": "64", "LPA_REBUILD_HYBRID": "1"},
+                                 {"LPA_BLOCK_DEG": "64", "LPA_BLOCK_CLASSES": "32"},
+                                 {"LPA_BLOCK_DEG": "512", "LPA_BLOCK_CLASSES": "16"}])
 def test_class_blocked_rebuild_bit_exact(gfa, rmat22, monkeypatch, env):
     """The class-blocked labels-mode al[] rebuild (rows of degree > LPA_BLOCK_DEG in
-    (class, column) order, per-XCD class pieces + the plain stream below; its arc giant
-    bits ORed piecewise): R-MAT-22 (4 M slots, the LDS hot-set rebuild) bit-exact against
+    (class, column) order, per-XCD class pieces -- 8, 16 or 32 classes, one phase per 8 --
+    + the plain stream below; its arc giant bits ORed piecewise): R-MAT-22 (4 M slots, the LDS hot-set rebuild) bit-exact against
     the oracle at supersteps 1..5 -- superstep 1's column runs over the reordered rows,
     the labels-/hybrid-mode rebuild after it, superstep 2's settles from its arc bits."""
     monkeypatch.setenv("LPA_BLOCK_MIN_SLOTS", "0")   # shipped: label vectors of >= 32 M slots

@@ -6,6 +6,7 @@
 #   c3q       bench.py C3 without the CPU baseline, outlier and quality
 #   c2 / c4 / c5   bench.py --config C2 / C4 / C5 (no CPU baseline, outlier or quality)
 #   prof      rocprofv3 kernel trace + stats of the C3 bench (no CPU baseline)
+#   prof5     the same for C5 (2 timed calls)
 #   outprof   rocprofv3 kernel trace + stats of tools/outlier_prof.py C3
 #   tally     tools/rank_tally.py C4 8 (per-rank tally time, caller-driven ranks)
 # Outputs land in gpurun_out/${TAG}_*; every GPU step has its own time limit and the
@@ -38,6 +39,11 @@ for st in $STEPS; do
     c2) bench c2 300 --config C2 --no-cpu-baseline --no-outlier --no-quality ;;
     c4) bench c4 400 --config C4 --no-cpu-baseline --no-outlier --no-quality --steps 3 ;;
     c5) bench c5 400 --config C5 --no-cpu-baseline --no-outlier --no-quality --steps 3 ;;
+    prof5)
+      cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "gpurun_out/${TAG}_prof5" -o run --output-format csv \
+        -- python3 bench.py --config C5 --no-cpu-baseline --no-outlier --no-quality --steps 2 --warmup 1 \
+        > "gpurun_out/${TAG}_prof5.json" 2> "gpurun_out/${TAG}_prof5.err" || exit 1 ;;
     prof|outprof)
       cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
       if [ $st = prof ]; then
