@@ -1980,7 +1980,7 @@ __device__ __forceinline__ void pipe3(int64_t nb, Pre pre, F fetch, Q probe, R r
   if (nb > 1) probe(c1, w1);
   resolve(c0, w0, r0);
 #define LPA_PIPE_STEP(GUARD, I, CA, CB, CC, WA, WB, RA, RB) \
-  if (t + 4 < nb) pre(t + 4, (I + 4) % 6);                \
+  if (!GUARD || t + 4 < nb) pre(t + 4, (I + 4) % 6);      \
   if (!GUARD || t + 3 < nb) fetch(t + 3, CA, (I + 3) % 6); \
   if (!GUARD || t + 2 < nb) probe(CC, WA);                 \
   if (!GUARD || t + 1 < nb) resolve(CB, WB, RB);           \

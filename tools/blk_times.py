@@ -31,6 +31,9 @@ for call in range(2):
     assert lib.lpa_diag_blk_times(buf) == 0
     t = np.array(buf, dtype=np.int64).reshape(512, 3)
     nb = int((t[:, 0] > 0).sum())
+    if nb == 0:          # no blocked rebuild in this call (e.g. an ablation changed the labels)
+        out[f"call{call}"] = {"blocks": 0}
+        continue
     t = t[:nb]
     t0 = t[:, 0].min()
     rel = (t - t0) / 100.0  # us
