@@ -662,11 +662,36 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
 // H rows (in (class, column) order): per class, every row's class segment in <= 64-arc
 // pieces, row after row, then padding to a multiple of 8 pieces; class 7 also lists
 // the positions up to blk_a0, the 512-aligned start of the plain stream.
+// diagnostic (LPA_BLOCK_NAIVE=1, timing only, labels still exact): the listed range cut
+// into aligned 64-arc pieces, class x taking the x-th contiguous share -- the piece
+// machinery on a plain stream's access pattern
+__global__ void k_naive_pieces(int64_t a0, int64_t n, u64* __restrict__ pieces) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = 64 * j;
+    pieces[j] = ((u64)(a0 - p < 64 ? a0 - p : 64) << 32) | (u64)p;
+  }
+}
+
 int build_pieces(lpa_graph* g, int64_t H) {
   hipStream_t s = g->stream;
   const int C = g->blk_classes;
   int64_t aH = 0;
   LPA_HIP(hipMemcpyAsync(&aH, g->rp + H, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  if (getenv("LPA_BLOCK_NAIVE")) {
+    LPA_HIP(hipStreamSynchronize(s));
+    int64_t a0 = (aH + 511) / 512 * 512;
+    if (a0 > g->arcs) a0 = g->arcs;
+    const int64_t n = (a0 + 63) / 64;
+    const int64_t per = (n / C + 7) / 8 * 8;
+    for (int x = 0; x <= C; ++x) g->blk_off[x] = x == C ? (n + 7) / 8 * 8 : (x * per < n ? x * per : (n + 7) / 8 * 8);
+    LPA_TRY(dev_alloc(g, (void**)&g->blk_pieces, sizeof(u64) * (g->blk_off[C] > 0 ? g->blk_off[C] : 1)));
+    LPA_HIP(hipMemsetAsync(g->blk_pieces, 0, sizeof(u64) * (g->blk_off[C] > 0 ? g->blk_off[C] : 1), s));
+    hipLaunchKernelGGL(k_naive_pieces, dim3(grid_for(n)), dim3(256), 0, s, a0, n, g->blk_pieces);
+    LPA_HIP(hipGetLastError());
+    LPA_HIP(hipStreamSynchronize(s));
+    g->blk_a0 = a0;
+    return LPA_OK;
+  }
   uint32_t* seg = nullptr;
   int32_t* np = nullptr;
   int64_t* poff = nullptr;
