@@ -404,6 +404,13 @@ def main():
     g.step(1)
     g.set_serial(True)
     per_ss = [g.step(1, stats=True) for _ in range(MAX_ITER - 1)]   # supersteps 2..10
+    # the untimed superstep 1's al[] rebuild (labels mode; the serialized schedule tallies
+    # superstep 1 by hash instead of column runs, to the same labels, so its rebuild is
+    # the shipped one), median of 3, HIP events
+    ss1_rb = []
+    for _ in range(3):
+        g.reset()
+        ss1_rb.append(g.step(1, stats=True)["kernel_ms"]["k_al_rebuild_hot"])
     g.set_serial(False)
     g.set_frontier(True)
     kms = {k: sum(st["kernel_ms"][k] for st in per_ss) for k in per_ss[0]["kernel_ms"]}
@@ -458,10 +465,27 @@ def main():
         "traffic_source": rb_src,
         "bytes_per_launch": rb_bytes,
         "bytes_note": "col 4 B/arc + al 4 B/arc + each label once (4 B/vertex); superstep 2's rebuild runs in "
-                      "bits mode (giant-label bits, gathers only for the other labels: PMC traffic 1.12x)",
+                      "bits mode (giant-label bits, gathers only for the other labels: PMC traffic 1.13x)",
         "avg_launch_ms": round(statistics.mean(rb_work), 4),
         "launches": f"{len(rb_work)} rebuilding launch(es) in supersteps 2..{MAX_ITER} (serialized schedule, "
                     f"HIP events on the handle's stream)",
+    }
+
+    ss1_rb_ms = max_over_ranks(statistics.median(ss1_rb))
+    ss1_traffic, ss1_src = measured_traffic("k_al_rebuild_hot_superstep1", config_id)
+    ss1_obj = None if ss1_rb_ms <= 0.1 else {
+        "bound": "hbm",
+        "kernel": "k_al_rebuild_hot",
+        "achieved": round(rb_bytes / (ss1_rb_ms * 1e-3) / 1e9, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(rb_bytes / (ss1_rb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "traffic": ss1_traffic,
+        "traffic_source": ss1_src,
+        "bytes_per_launch": rb_bytes,
+        "avg_launch_ms": round(ss1_rb_ms, 4),
+        "note": "superstep 1's rebuild (labels mode; outside the timed window, inside lpa_run(10)): "
+                "bound by its L2-missing gathers (PMC traffic / algorithmic in traffic), DESIGN.md section 4",
     }
 
     out_json = {
@@ -504,6 +528,7 @@ def main():
         # roofline_tally
         "roofline": rb_obj if rb_obj is not None else tally_obj,
         "roofline_tally": tally_obj,
+        "roofline_superstep1_rebuild": ss1_obj,
         "iteration_roofline": {
             "what": ("north_star 'fraction of HBM-roofline TEPS' against the SURVEY §8(d) contract: B_iter = "
                      "16m+12V+8 bytes per superstep (col 4 B/arc + gathered label 4 B/arc + row offsets + label "
