@@ -168,6 +168,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_BLOCK_MIN_SLOTS")) g->block_min_slots = atoll(f);
   if (const char* f = getenv("LPA_BLOCK_CLASSES")) g->block_classes_req = atoi(f);
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
+  if (const char* f = getenv("LPA_CONV_STREAMS")) g->conv_streams = atoi(f) < 1 ? 1 : atoi(f) > 3 ? 3 : atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
   // internal builds (the outlier stage's L2 sub-graph): the locality order is a

@@ -250,6 +250,7 @@ struct lpa_graph {
   int64_t blk_a0 = 0;                       // arcs [0, blk_a0) are listed (a multiple of 512)
   int64_t blk_rows = 0;                     // rows in (class, column) order
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
+  int conv_streams = 3;                     // LPA_CONV_STREAMS: streams of a converged superstep's tally
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per
   // (superstep, cur, par)

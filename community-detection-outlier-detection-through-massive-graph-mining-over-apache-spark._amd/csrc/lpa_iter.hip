@@ -2607,7 +2607,12 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   hipStream_t s = g->stream;
   // LPA_SERIAL=1 (profiling only): every tally kernel on the main stream, so a
   // kernel trace shows each kernel's standalone duration
-  hipStream_t sb = g->serial ? s : g->aux_stream[0], sc = g->serial ? s : g->aux_stream[1];
+  // converged supersteps (captured graphs): LPA_CONV_STREAMS = 3 (main + two bin streams,
+  // default), 2 (one bin stream) or 1 (everything on the main stream)
+  const bool conv = g->since_reset >= kDenseSupersteps + 2;
+  const int nstr = g->serial ? 1 : (conv ? g->conv_streams : 3);
+  hipStream_t sb = nstr >= 2 ? g->aux_stream[0] : s;
+  hipStream_t sc = nstr >= 3 ? g->aux_stream[1] : sb;
   const int64_t* bb = g->bin_begin;
   const int32_t* fr_all = g->fr_all + g->par;
   int32_t* fcnt = g->fcnt + 16 * g->par;
@@ -2674,10 +2679,10 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(launch_frontier_lists(g));
   }
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
-  if (!g->serial) {
+  if (sb != s) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
     LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
-    LPA_HIP(hipStreamWaitEvent(sc, g->ev_fork, 0));
+    if (sc != sb) LPA_HIP(hipStreamWaitEvent(sc, g->ev_fork, 0));
   }
 
   auto mark = [&](int i, hipStream_t st) -> int {
@@ -2845,11 +2850,13 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], bb[BIN_ISO], false, g->par, BIN_W2, BIN_ISO, dm));
     LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par, BIN_SEG, BIN_W16, dm));
   }
-  if (!g->serial) {
+  if (sb != s) {
     LPA_HIP(hipEventRecord(g->ev_join[0], sb));
-    LPA_HIP(hipEventRecord(g->ev_join[1], sc));
     LPA_HIP(hipStreamWaitEvent(s, g->ev_join[0], 0));
-    LPA_HIP(hipStreamWaitEvent(s, g->ev_join[1], 0));
+    if (sc != sb) {
+      LPA_HIP(hipEventRecord(g->ev_join[1], sc));
+      LPA_HIP(hipStreamWaitEvent(s, g->ev_join[1], 0));
+    }
   }
   return LPA_OK;
 }
