@@ -667,3 +667,29 @@ def test_class_blocked_rebuild_bit_exact(gfa, rmat22, monkeypatch, env):
             assert bad == 0, f"{env} superstep {t + 1}: {bad} labels differ"
         g.reset()
         assert np.array_equal(g.run(5), hist[4]), f"{env} lpa_run(5) after reset"
+
+
+@pytest.fixture(scope="module")
+def chunglu5m(gfa, oracle):
+    # 40,000,002 arcs: not a multiple of the rebuild's 512-arc batches (every BASELINE
+    # config's arc count is), on a label vector large enough for the LDS hot-set rebuild
+    V, m = 5_000_000, 20_000_001
+    s, d = gfa.gen_chunglu(V, m, 2.1, 200_000.0, seed=3)
+    sn, dn = s.cpu().numpy(), d.cpu().numpy()
+    _, hist, _ = oracle.lpa(V, sn, dn, 5, per_iter=True)
+    return V, sn, dn, hist
+
+
+@pytest.mark.parametrize("env", [{}, {"LPA_BLOCK_MIN_SLOTS": "0"}, {"LPA_BLOCK_MIN_SLOTS": "0", "LPA_BLOCK_DEG": "64"}])
+def test_hot_rebuild_partial_batch(gfa, chunglu5m, monkeypatch, env):
+    """The hot-set rebuild's partial last batch (and, blocked, the plain stream after the
+    listed range ending mid-batch), labels and bits modes: bit-exact at supersteps 1..5."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    V, sn, dn, hist = chunglu5m
+    with gfa.Graph(sn, dn, V) as g:
+        assert g.info()["arcs"] % 512 != 0
+        for t in range(5):
+            g.step(1)
+            bad = int((g.labels() != hist[t]).sum())
+            assert bad == 0, f"{env} superstep {t + 1}: {bad} labels differ"
