@@ -621,8 +621,8 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
     LPA_TRY(dev_alloc(g, (void**)&g->first_best, sizeof(u64) * S));
     LPA_HIP(hipMemsetAsync(g->first_best, 0, sizeof(u64) * S, s));
     if (arcs > 0) {
-      // whole 512-arc tiles of words plus the next tile's first word (k_first_runs)
-      const int64_t nwords = (arcs + 511) / 512 * 8 + 8;
+      // whole run tiles of words plus the next tile's words (k_first_runs)
+      const int64_t nwords = (arcs + kRunTile - 1) / kRunTile * (kRunTile / 64) + kRunTile / 64;
       LPA_TRY(dev_alloc(g, (void**)&g->rstart, sizeof(u64) * nwords));
       hipLaunchKernelGGL(k_row_starts, dim3(grid_for(nwords * 64)), dim3(256), 0, s, g->crow, arcs, nwords,
                          g->rstart);

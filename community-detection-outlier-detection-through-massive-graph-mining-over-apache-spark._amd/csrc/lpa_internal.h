@@ -56,6 +56,9 @@ constexpr double kRebuildFrac = 0.25;
 // the al[] scatter marks dirty rows while <= this fraction of the arcs changed; above
 // it the next superstep tallies every row
 constexpr double kFrontierFrac = 0.005;
+// superstep 1's column-run tiles (lpa_iter.hip k_first_runs): arcs per wave tile, 16 per
+// lane; the row-start bitmap holds whole tiles plus the next tile's first word
+constexpr int kRunTile = 1024;
 // P = 1 label vectors of at least this many slots take the LDS hot-set rebuild
 // (k_al_rebuild_hot); smaller ones stay in L2 / the Infinity Cache (k_al_rebuild_small)
 constexpr int64_t kHotMinSlots = 4ll << 20;

@@ -2353,11 +2353,10 @@ __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __r
 // are sorted: its vote counts are the lengths of its runs of equal columns
 // (duplicate edges, a self-loop's two arcs).  The mode -- longest run, ties to the
 // smallest label -- is a segmented max over the arc stream, with no hash table.
-// A wave takes 512-arc tiles (8 positions per lane); a row inside the tile is
+// A wave takes kRunTile-arc tiles (16 positions per lane); a row inside the tile is
 // written directly, a row crossing a tile boundary folds each piece into
 // first_best[row] and k_first_final writes it.
 // ---------------------------------------------------------------------------
-constexpr int kRunTile = 512;
 
 // One step of a segmented (by row id) inclusive max scan over the wave, in DPP: the
 // lane's source (row shift within 16-lane rows, or a row broadcast) is moved by VALU
@@ -2399,8 +2398,8 @@ __device__ __forceinline__ int wave_incl_max(int v) {
   return v;
 }
 
-// Lane-sequential layout: lane l of a wave owns positions t0 + 8 l .. t0 + 8 l + 7 of
-// its 512-arc tile (two 16-B loads), walks them in registers (run lengths, the row's
+// Lane-sequential layout: lane l of a wave owns positions t0 + kP l .. t0 + kP l + kP - 1
+// of its tile (kP / 4 16-B loads), walks them in registers (run lengths, the row's
 // running maximum, rows that start and end inside the lane written at once), and
 // only the lane-crossing parts go through cross-lane scans -- three per tile instead
 // of a segmented scan per 64 arcs (the per-arc-lane form was VALU-bound: ~190
@@ -2421,7 +2420,8 @@ __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ 
                                                     const u64* __restrict__ rstart, int64_t arcs,
                                                     int32_t* __restrict__ Ln, u64* __restrict__ best) {
   constexpr int kP = kRunTile / 64;  // positions per lane
-  static_assert(kP == 8, "one bitmap byte per lane");
+  static_assert(kP % 4 == 0 && kP <= 32 && 64 % kP == 0, "whole 16-B loads, one bitmap field per lane");
+  constexpr u32 kPMask = kP == 32 ? 0xFFFFFFFFu : (1u << kP) - 1u;
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2430,20 +2430,22 @@ __global__ __launch_bounds__(256) void k_first_runs(const int32_t* __restrict__ 
     const int64_t p0 = t0 + kP * lane;
     u32 a[kP];
     if (p0 + kP <= t1) {
-      const v4i_t* q = reinterpret_cast<const v4i_t*>(al + p0);  // 32-B aligned: t0 % 512 == 0
-      const v4i_t x = __builtin_nontemporal_load(q), y = __builtin_nontemporal_load(q + 1);
-      a[0] = (u32)x.x; a[1] = (u32)x.y; a[2] = (u32)x.z; a[3] = (u32)x.w;
-      a[4] = (u32)y.x; a[5] = (u32)y.y; a[6] = (u32)y.z; a[7] = (u32)y.w;
+      const v4i_t* q = reinterpret_cast<const v4i_t*>(al + p0);  // 16-B aligned: t0 % kRunTile == 0
+#pragma unroll
+      for (int v = 0; v < kP / 4; ++v) {
+        const v4i_t x = __builtin_nontemporal_load(q + v);
+        a[4 * v] = (u32)x.x; a[4 * v + 1] = (u32)x.y; a[4 * v + 2] = (u32)x.z; a[4 * v + 3] = (u32)x.w;
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < kP; ++j) a[j] = p0 + j < t1 ? (u32)al[p0 + j] : kNone;
     }
     // row-start bits of the lane's positions (bit j: p0 + j), positions >= arcs set
-    u32 sb = (u32)(rstart[(t0 >> 6) + (lane >> 3)] >> ((lane & 7) * 8)) & 0xFFu;
+    u32 sb = (u32)(rstart[(t0 >> 6) + (lane * kP) / 64] >> ((lane * kP) % 64)) & kPMask;
     const int64_t dead = p0 + kP - arcs;
-    if (dead > 0) sb |= dead >= kP ? 0xFFu : (0xFFu << (kP - (int)dead)) & 0xFFu;
+    if (dead > 0) sb |= dead >= kP ? kPMask : (kPMask << (kP - (int)dead)) & kPMask;
     // does position p0 + kP start a row (the next lane's bit 0; lane 63: the next tile's)
-    const int tile_next = t0 + kRunTile >= arcs ? 1 : (int)(rstart[(t0 >> 6) + kP] & 1ull);
+    const int tile_next = t0 + kRunTile >= arcs ? 1 : (int)(rstart[(t0 + kRunTile) >> 6] & 1ull);
     const bool ends = (dpp_i<0x130>(tile_next, (int)(sb & 1u)) & 1) != 0;  // wave_shl:1
     // carries from before the tile: row, label and (a run continuing into it) length
     const int32_t r_t0 = crow[t0];
@@ -2788,43 +2790,45 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     }                                                                                         \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                     \
   }
-#define LPA_GROUP_LAUNCH(BIN, G)                                                             \
+#define LPA_GROUP_LAUNCH(BIN, G, ST)                                                         \
   {                                                                                          \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
-    LPA_TRY(mark(2 * (BIN + 1), sc));                                                        \
+    LPA_TRY(mark(2 * (BIN + 1), ST));                                                        \
     if (n > 0) {                                                                             \
       hipLaunchKernelGGL(k_lpa_group<G>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
-                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_bins); \
+                         ST, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_bins); \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
-    LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
+    LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                    \
   }
-#define LPA_ROWS_LAUNCH(BIN, G, FR)                                                          \
+#define LPA_ROWS_LAUNCH(BIN, G, FR, ST)                                                      \
   {                                                                                          \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
-    LPA_TRY(mark(2 * (BIN + 1), sc));                                                        \
+    LPA_TRY(mark(2 * (BIN + 1), ST));                                                        \
     if (n > 0) {                                                                             \
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
       hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
-                         sc, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, \
+                         ST, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, \
                          sort_after, gsel);                                                   \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
-    LPA_TRY(mark(2 * (BIN + 1) + 1, sc));                                                    \
+    LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                    \
   }
   // stream balance (measured steady superstep): aux0 w16 + w8 + w4, aux1 w2 + the
-  // row/group bins
+  // row/group bins (round 4: superstep 2's tail bins g16 .. g1 on the main stream, ahead
+  // of the hub combine, measured slower -- 2.08 -> 2.11 ms)
+  hipStream_t st_tail = sc;
   LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_bins)
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_bins)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_bins)
   LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_bins)
-  LPA_ROWS_LAUNCH(BIN_G64, 64, fr_bins)
-  LPA_ROWS_LAUNCH(BIN_G32, 32, fr_bins)
-  LPA_ROWS_LAUNCH(BIN_G16, 16, fr_bins)
-  LPA_ROWS_LAUNCH(BIN_G8, 8, fr_bins)
-  LPA_GROUP_LAUNCH(BIN_G4, 4)
-  LPA_GROUP_LAUNCH(BIN_G2, 2)
-  LPA_GROUP_LAUNCH(BIN_G1, 1)
+  LPA_ROWS_LAUNCH(BIN_G64, 64, fr_bins, sc)
+  LPA_ROWS_LAUNCH(BIN_G32, 32, fr_bins, sc)
+  LPA_ROWS_LAUNCH(BIN_G16, 16, fr_bins, st_tail)
+  LPA_ROWS_LAUNCH(BIN_G8, 8, fr_bins, st_tail)
+  LPA_GROUP_LAUNCH(BIN_G4, 4, st_tail)
+  LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)
+  LPA_GROUP_LAUNCH(BIN_G1, 1, st_tail)
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
