@@ -693,3 +693,20 @@ def test_hot_rebuild_partial_batch(gfa, chunglu5m, monkeypatch, env):
             g.step(1)
             bad = int((g.labels() != hist[t]).sum())
             assert bad == 0, f"{env} superstep {t + 1}: {bad} labels differ"
+
+
+def test_sbm_hot_path_every_superstep(gfa, oracle):
+    """A family with no giant label (planted partition, 400 blocks) at the LDS hot-set
+    rebuild's size (4 M slots): every superstep's giant pick finds no dominant label, so
+    the giant decisions and settles must stand aside -- bit-exact at supersteps 1..10."""
+    V, B, m = 1 << 22, 400, 40_000_000
+    s, d = gfa.gen_sbm(V, B, m)
+    sn, dn = s.cpu().numpy(), d.cpu().numpy()
+    _, hist, _ = oracle.lpa(V, sn, dn, 10, per_iter=True)
+    with gfa.Graph(s, d, V) as g:
+        for t in range(10):
+            g.step(1)
+            bad = int((g.labels() != hist[t]).sum())
+            assert bad == 0, f"SBM-4M superstep {t + 1}: {bad} labels differ"
+        g.reset()
+        assert np.array_equal(g.run(10), hist[9])
