@@ -577,6 +577,20 @@ __device__ __forceinline__ void row_load(u32 (&raw)[NC], const int32_t* __restri
   }
 }
 
+// branch-free form (k_lpa_wave's ring): an empty span (past the bin's end) loads
+// al[0] and its labels are never read -- no control flow for the waitcnt pass to merge
+template <int NC>
+__device__ __forceinline__ void row_load_nb(u32 (&raw)[NC], const int32_t* __restrict__ al,
+                                            const RowSpan& r, int lane) {
+  const int d = span_len(r);
+  const int last = d > 0 ? d - 1 : 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int off = c * 64 + lane;
+    raw[c] = ld_stream(al + r.b + (off < last ? off : last));
+  }
+}
+
 template <int NC>
 __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r, int64_t v,
                                           int32_t* __restrict__ Ln, u64* tab, uint16_t* lst, int lane,
@@ -614,9 +628,55 @@ __device__ __forceinline__ void row_tally(const u32 (&raw)[NC], const RowSpan& r
   }
 }
 
-// bins w2 / w4 / w8 (64 < deg <= 64 * NC): one wave per row, grid-stride; three
-// label register sets in an unrolled ring (labels two rows ahead, no set copied
-// while its loads are in flight), row bounds three rows ahead.
+// Row bounds of 64 work items of a wave in one load per lane: lane k holds item
+// i0 + k * stride (its row, arc begin and end; empty past the bin's end).  The label
+// loads of a row take its bounds by readlane, so they never wait on a bounds load
+// issued after the label loads still in flight (vmcnt counts in order: a wait for the
+// newest load is a wait for every older one).
+struct SpanBatch {
+  int64_t b, e;
+  int32_t v;
+};
+__device__ __forceinline__ SpanBatch span_batch(const int64_t* __restrict__ rp, const BinRows& br, int64_t i0,
+                                                int64_t stride, int lane) {
+  SpanBatch sb;
+  sb.b = sb.e = 0;
+  sb.v = 0;
+  const int64_t i = i0 + (int64_t)lane * stride;
+  if (i < br.n) {
+    const int64_t v = br.row(i);
+    sb.v = (int32_t)v;
+    sb.b = rp[v];
+    sb.e = rp[v + 1];
+  }
+  return sb;
+}
+__device__ __forceinline__ int64_t readlane_i64(int64_t x, int l) {
+  return (int64_t)(((u64)(u32)__builtin_amdgcn_readlane((int)(u32)((u64)x >> 32), l) << 32) |
+                   (u64)(u32)__builtin_amdgcn_readlane((int)(u32)(u64)x, l));
+}
+// item q of the two batches (q < 64: cur, else nxt; uniform).  A branch, not a select:
+// readlane is convergent (not speculated), so the cur side never waits for nxt's load.
+__device__ __forceinline__ RowSpan span_at(const SpanBatch& cur, const SpanBatch& nxt, int q) {
+  RowSpan r;
+  if (q < 64) {
+    r.b = readlane_i64(cur.b, q);
+    r.e = readlane_i64(cur.e, q);
+  } else {
+    r.b = readlane_i64(nxt.b, q - 64);
+    r.e = readlane_i64(nxt.e, q - 64);
+  }
+  return r;
+}
+
+// label register sets in the k_lpa_wave ring: labels of the next D - 1 rows in flight
+// while a row is tallied
+template <int NC>
+constexpr int wave_ring_depth() { return NC <= 2 ? 6 : NC <= 4 ? 4 : 3; }
+
+// bins w2 / w4 / w8 / w16 (64 < deg <= 64 * NC): one wave per row, grid-stride; D
+// label register sets in an unrolled ring (labels D - 1 rows ahead), row bounds by
+// 64-row batches one batch ahead (span_batch).
 template <int NC>
 __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp,
                                                   const int32_t* __restrict__ al,
@@ -626,6 +686,8 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
                                                   const int32_t* __restrict__ fr_all, int pmax,
                                                   const int32_t* __restrict__ gsel) {
   constexpr int kCap = 2 * 64 * NC;
+  constexpr int D = wave_ring_depth<NC>();
+  static_assert(D >= 2 && D <= 64, "ring depth");
   __shared__ u64 tab_all[4][kCap];
   __shared__ uint16_t lst_all[4][64 * NC];
   const int lane = threadIdx.x & 63;
@@ -635,36 +697,37 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   const u64 lt = (1ull << lane) - 1ull;
   const int64_t stride = (int64_t)gridDim.x * 4;
   const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
-  int64_t i = (int64_t)blockIdx.x * 4 + w;   // work item: row br.row(i)
-  if (i >= br.n) return;  // no block-level barriers in this kernel
+  int64_t ib = (int64_t)blockIdx.x * 4 + w;   // work item of the current batch's lane 0
+  if (ib >= br.n) return;  // no block-level barriers in this kernel
   for (int k = lane; k < kCap; k += 64) tab[k] = 0ull;  // only waves with rows clear
   // gsel (label-dense supersteps): the giant-label word of the labels this superstep
   // reads (k_giant_pick: label, worth trying)
   const bool giant = gsel != nullptr && gsel[1] != 0;
   const u32 G = giant ? (u32)gsel[0] : 0u;
-  RowSpan s0 = row_span(rp, br, i), s1 = row_span(rp, br, i + stride), s2 = row_span(rp, br, i + 2 * stride);
-  u32 ra[NC], rb[NC], rc[NC];
-  row_load<NC>(ra, al, s0, lane);
-  row_load<NC>(rb, al, s1, lane);
+  SpanBatch cur = span_batch(rp, br, ib, stride, lane);
+  SpanBatch nxt;  // the next batch: loaded at p == 32, half a batch before its first use
+  nxt.b = nxt.e = 0;
+  nxt.v = 0;
+  int p = 0;  // current row: work item ib + p * stride
+  u32 rl[D][NC];
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k) row_load_nb<NC>(rl[k], al, span_at(cur, nxt, k), lane);
   while (true) {
-    row_load<NC>(rc, al, s2, lane);
-    RowSpan s3 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(ra, s0, br.row(i), Ln, tab, lst, lane, lt, pmax, giant, G);
-    i += stride;
-    if (i >= br.n) break;
-    row_load<NC>(ra, al, s3, lane);
-    RowSpan s4 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(rb, s1, br.row(i), Ln, tab, lst, lane, lt, pmax, giant, G);
-    i += stride;
-    if (i >= br.n) break;
-    row_load<NC>(rb, al, s4, lane);
-    RowSpan s5 = row_span(rp, br, i + 3 * stride);
-    row_tally<NC>(rc, s2, br.row(i), Ln, tab, lst, lane, lt, pmax, giant, G);
-    i += stride;
-    if (i >= br.n) break;
-    s0 = s3;
-    s1 = s4;
-    s2 = s5;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      row_load_nb<NC>(rl[(k + D - 1) % D], al, span_at(cur, nxt, p + D - 1), lane);
+      const RowSpan s = span_at(cur, nxt, p);
+      const int64_t v = (int64_t)__builtin_amdgcn_readlane(cur.v, p);
+      row_tally<NC>(rl[k], s, v, Ln, tab, lst, lane, lt, pmax, giant, G);
+      if (ib + (int64_t)(p + 1) * stride >= br.n) return;
+      ++p;
+      if (p == 32) nxt = span_batch(rp, br, ib + 64 * stride, stride, lane);
+      if (p == 64) {
+        p = 0;
+        ib += 64 * stride;
+        cur = nxt;
+      }
+    }
   }
 }
 
