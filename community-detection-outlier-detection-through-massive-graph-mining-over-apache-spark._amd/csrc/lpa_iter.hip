@@ -41,6 +41,7 @@
 //   seg  deg > 1024     one wave per 512-arc unit (staged unit tally words), merged
 //                       per row by the hub combine (lpa_hub.hip)
 // Tables keep a touched-slot list: finishing a vertex costs O(distinct labels).
+#include <chrono>
 #include <stdio.h>
 #include <string.h>
 
@@ -3133,7 +3134,18 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
   // k (k < kTallyKernels), then kTallyEv after the join, +1 after the exchange, +2
   // after the diff + scatter, +3 after the rebuild, +4 / +5 around the frontier lists
   bool blk_ran[LPA_STATS_MAX_ITERS] = {};  // serialized stats: k_lpa_block ran in superstep t
+  // LPA_HOST_TIMING=1 (diagnostic): host enqueue time per superstep and the final
+  // wait, on stderr -- whether a call is bound by the host's launches or the GPU
+  static const bool host_timing = getenv("LPA_HOST_TIMING") && atoi(getenv("LPA_HOST_TIMING"));
+  const auto h0 = std::chrono::steady_clock::now();
+  double h_prev = 0.0;
+  auto h_ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); };
   for (int32_t t = 0; t < n; ++t) {
+    if (host_timing && t > 0) {
+      const double h = h_ms();
+      fprintf(stderr, "[lpa host] superstep %d enqueue %.3f ms\n", (int)g->since_reset, h - h_prev);
+      h_prev = h;
+    }
     if (t < nt) blk_ran[t] = block_mode_now(g);
     const int32_t* Lc = g->lab[g->cur];
     int32_t* Ln = g->lab[g->cur ^ 1];
@@ -3240,7 +3252,11 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     ++g->since_reset;
   }
   if (timed) LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS + 1], s));
+  const double h_enq = host_timing ? h_ms() : 0.0;
   LPA_HIP(hipStreamSynchronize(s));
+  if (host_timing)
+    fprintf(stderr, "[lpa host] superstep %d enqueue %.3f ms; call: enqueue %.3f ms, final wait %.3f ms\n",
+            (int)g->since_reset, h_enq - h_prev, h_enq, h_ms() - h_enq);
   if (n > 0) {
     int32_t err = 0;
     LPA_HIP(hipMemcpy(&err, g->dev_err, sizeof(err), hipMemcpyDeviceToHost));
