@@ -898,6 +898,42 @@ __device__ __forceinline__ void rows_labels(u32 (&lab)[kChunks], const int32_t* 
   }
 }
 
+// branch-free forms for k_lpa_rows' ring: every lane loads, at an address clamped into
+// the graph (rp[<= vend], al[< arcs]); values past the bin or the row are masked after
+// the load
+constexpr int kRowsRing = 3;
+template <int G>
+__device__ __forceinline__ void rows_rp_nb(const int64_t* __restrict__ rp, int64_t r0, int64_t vend,
+                                           int lane, int64_t& rpl, int64_t& rpe) {
+  constexpr int RB = 512 / G;
+  const int64_t i = r0 + lane;
+  rpl = rp[i < vend ? i : vend];
+  rpe = rp[r0 + RB < vend ? r0 + RB : vend];
+}
+
+// (vbits bit c: chunk c's label is a vote -- one register per set, applied when the set
+// is tallied, so nothing 64-bit stays live while the loads are in flight)
+template <int G>
+__device__ __forceinline__ void rows_labels_nb(u32 (&lab)[kChunks], u32& vbits, const int32_t* __restrict__ al,
+                                               int64_t r0, int64_t vend, int64_t rpl, int64_t rpe,
+                                               int lane) {
+  constexpr int RB = 512 / G;
+  vbits = 0u;
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) {
+    const int rl = c * (64 / G) + lane / G;
+    const int j = lane & (G - 1);
+    const int64_t b = __shfl(rpl, rl, 64);
+    const int64_t en = __shfl(rpl, rl + 1 < 64 ? rl + 1 : 63, 64);
+    const int64_t e = rl + 1 < RB ? en : rpe;
+    int64_t a = b + j < e ? b + j : e - 1;
+    a = a > 0 ? a : 0;
+    lab[c] = ld_stream(al + a);
+    vbits |= (r0 + rl < vend && j < e - b) ? (1u << c) : 0u;
+  }
+  asm volatile("" : "+v"(vbits));  // computed here: not sunk to the tally (64-bit bounds would stay live)
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp,
                                                   const int32_t* __restrict__ al,
@@ -940,28 +976,12 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
   u32* hg = &ghist_all[w][(lane / G) * kGB];
   const int gj = lane & (G - 1);   // G >= kGB when giant: lane gj < kGB owns bucket gj
   if (gj < kGB) hg[gj] = 0u;
-  int64_t rpl0, rpe0, rpl1 = 0, rpe1 = 0;
-  rows_rp<G>(rp, vbeg + bi * RB, vend, lane, rpl0, rpe0);
-  if (bi + stride < nb) rows_rp<G>(rp, vbeg + (bi + stride) * RB, vend, lane, rpl1, rpe1);
-  u32 lab[kChunks];
-  rows_labels<G>(lab, al, vbeg + bi * RB, vend, rpl0, rpe0, lane);
   const int gbase = lane & ~(G - 1);
   const u64 gm = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
-  while (true) {
-    const int64_t bn = bi + stride;
-    int64_t rpl2 = 0, rpe2 = 0;
-    if (bn + stride < nb) rows_rp<G>(rp, vbeg + (bn + stride) * RB, vend, lane, rpl2, rpe2);
-    u32 labn[kChunks];
-    if (bn < nb) {
-      rows_labels<G>(labn, al, vbeg + bn * RB, vend, rpl1, rpe1, lane);
-    } else {
-#pragma unroll
-      for (int c = 0; c < kChunks; ++c) labn[c] = kNone;
-    }
-    const int64_t r0 = vbeg + bi * RB;
+  auto tally_batch = [&](const u32 (&lab)[kChunks], u32 vbits, int64_t r0) {
 #pragma unroll
     for (int c = 0; c < kChunks; ++c) {
-      const u32 lb = lab[c];
+      const u32 lb = (vbits >> c) & 1u ? lab[c] : kNone;
       u64 act = __ballot(lb != kNone);
       u64 best = 0ull;
       if constexpr (G >= kGB) if (giant) {
@@ -999,14 +1019,32 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       const int64_t row = r0 + c * (64 / G) + lane / G;
       if ((lane & (G - 1)) == 0 && row < vend && best) Ln[row] = (int32_t)(~(u32)best);
     }
-    if (bn >= nb) break;
-    bi = bn;
-    rpl0 = rpl1;
-    rpe0 = rpe1;
-    rpl1 = rpl2;
-    rpe1 = rpe2;
+  };
+  // Ring of kRowsRing batches (batch j in slot j % kRowsRing): the offsets of batch
+  // i + kRowsRing are issued before the labels of batch i + kRowsRing - 1, so the wait
+  // for those labels' offsets (issued one batch earlier, ahead of the previous batch's
+  // labels) leaves the previous batch's labels in flight -- two label batches load
+  // while one is tallied.  Loads branch-free (rows_rp_nb / rows_labels_nb); scheduling
+  // barriers keep each batch's loads from being hoisted into the tally before them.
+  constexpr int D = kRowsRing;
+  int64_t rpl[D], rpe[D];
+  u32 lab[D][kChunks], vb[D];
 #pragma unroll
-    for (int c = 0; c < kChunks; ++c) lab[c] = labn[c];
+  for (int k = 0; k < D; ++k) rows_rp_nb<G>(rp, vbeg + (bi + k * stride) * RB, vend, lane, rpl[k], rpe[k]);
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k) rows_labels_nb<G>(lab[k], vb[k], al, vbeg + (bi + k * stride) * RB, vend, rpl[k], rpe[k], lane);
+  while (true) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      __builtin_amdgcn_sched_barrier(0);
+      rows_rp_nb<G>(rp, vbeg + (bi + D * stride) * RB, vend, lane, rpl[k], rpe[k]);
+      const int kl = (k + D - 1) % D;
+      rows_labels_nb<G>(lab[kl], vb[kl], al, vbeg + (bi + (D - 1) * stride) * RB, vend, rpl[kl], rpe[kl], lane);
+      __builtin_amdgcn_sched_barrier(0);
+      tally_batch(lab[k], vb[k], vbeg + bi * RB);
+      bi += stride;
+      if (bi >= nb) return;
+    }
   }
 }
 
