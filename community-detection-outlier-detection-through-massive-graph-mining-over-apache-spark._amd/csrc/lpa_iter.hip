@@ -1098,6 +1098,57 @@ __device__ __forceinline__ void unit_load(u32 (&raw)[kChunks], const int32_t* __
   }
 }
 
+// 64 work items' unit descriptors in one load per lane (lane k: item i0 + k * stride;
+// empty past the list or for a block-tier unit), read back by readlane
+struct UnitBatch {
+  int64_t begin;
+  int32_t len, id;
+};
+__device__ __forceinline__ UnitBatch unit_batch(const Segment* __restrict__ units, const UnitIds& ui, int64_t i0,
+                                                int64_t stride, int lane) {
+  UnitBatch b;
+  b.begin = 0;
+  b.len = 0;
+  b.id = 0;
+  const int64_t i = i0 + (int64_t)lane * stride;
+  if (i < ui.n) {
+    const int64_t id = ui.id(i);
+    b.id = (int32_t)id;
+    if (id < ui.lim) {
+      const Segment d = units[id];
+      b.begin = d.begin;
+      b.len = d.len;
+    }
+  }
+  return b;
+}
+// item q of the two batches (uniform; a branch so the cur side never waits for nxt)
+__device__ __forceinline__ Segment unit_at(const UnitBatch& cur, const UnitBatch& nxt, int q) {
+  Segment d;
+  d.v = 0;
+  if (q < 64) {
+    d.begin = readlane_i64(cur.begin, q);
+    d.len = __builtin_amdgcn_readlane(cur.len, q);
+  } else {
+    d.begin = readlane_i64(nxt.begin, q - 64);
+    d.len = __builtin_amdgcn_readlane(nxt.len, q - 64);
+  }
+  return d;
+}
+constexpr int kUnitsRing = 4;
+
+// branch-free unit_load (k_lpa_units' ring): an empty unit loads al[begin] (begin 0)
+__device__ __forceinline__ void unit_load_nb(u32 (&raw)[kChunks], const int32_t* __restrict__ al,
+                                             const Segment& d, int lane) {
+  const int len = d.len & 1023;
+  const int last = len > 0 ? len - 1 : 0;
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) {
+    const int off = c * 64 + lane;
+    raw[c] = ld_stream(al + d.begin + (off < last ? off : last));
+  }
+}
+
 // tally one unit whose labels are in `raw` (loaded earlier)
 __device__ __forceinline__ void unit_tally(const u32 (&raw)[kChunks], const Segment& d, int64_t u,
                                            u64* __restrict__ stage, int32_t* __restrict__ ucnt,
@@ -1148,8 +1199,6 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t u = (int64_t)blockIdx.x * 4 + w;
   if (u >= nunits) return;  // no block-level barriers in this kernel
-  // three register sets in a ring, unrolled so no set is ever copied (a copy of a
-  // register with a load in flight would wait for it): labels two units ahead
   UnitIds ui;
   ui.n = *fr_all ? nunits : (int64_t)*fcnt_u;
   ui.lim = nunits;
@@ -1158,31 +1207,36 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
   // the wave's table is cleared only by waves with work (a frontier superstep lists
   // few units: most of the grid leaves at once)
   for (int i = lane; i < kCap; i += 64) tab[i] = 0ull;
-  Segment d0 = load_unit(units, ui, u);
-  Segment d1 = load_unit(units, ui, u + stride);
-  Segment d2 = load_unit(units, ui, u + 2 * stride);
-  u32 ra[kChunks], rb[kChunks], rc[kChunks];
-  unit_load(ra, al, d0, lane);
-  unit_load(rb, al, d1, lane);
+  // unit descriptors by 64-unit batches (lane k: work item ib + k * stride), the next
+  // batch loaded half a batch ahead; kUnitsRing label sets in an unrolled ring (labels
+  // kUnitsRing - 1 units ahead), branch-free loads: no label load waits on a
+  // descriptor load issued after other label loads (vmcnt counts in order)
+  constexpr int D = kUnitsRing;
+  int64_t ib = u;
+  UnitBatch cur = unit_batch(units, ui, ib, stride, lane), nxt;
+  nxt.begin = 0;
+  nxt.len = 0;
+  nxt.id = 0;
+  int p = 0;
+  u32 rl[D][kChunks];
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k) unit_load_nb(rl[k], al, unit_at(cur, nxt, k), lane);
   while (true) {
-    unit_load(rc, al, d2, lane);
-    Segment d3 = load_unit(units, ui, u + 3 * stride);
-    unit_tally(ra, d0, ui.id(u), stage, ucnt, tab, lst, lane, lt, pmax);
-    u += stride;
-    if (u >= ui.n) break;
-    unit_load(ra, al, d3, lane);
-    Segment d4 = load_unit(units, ui, u + 3 * stride);
-    unit_tally(rb, d1, ui.id(u), stage, ucnt, tab, lst, lane, lt, pmax);
-    u += stride;
-    if (u >= ui.n) break;
-    unit_load(rb, al, d4, lane);
-    Segment d5 = load_unit(units, ui, u + 3 * stride);
-    unit_tally(rc, d2, ui.id(u), stage, ucnt, tab, lst, lane, lt, pmax);
-    u += stride;
-    if (u >= ui.n) break;
-    d0 = d3;
-    d1 = d4;
-    d2 = d5;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      unit_load_nb(rl[(k + D - 1) % D], al, unit_at(cur, nxt, p + D - 1), lane);
+      const Segment d = unit_at(cur, nxt, p);
+      const int64_t id = (int64_t)__builtin_amdgcn_readlane(cur.id, p);
+      unit_tally(rl[k], d, id, stage, ucnt, tab, lst, lane, lt, pmax);
+      if (ib + (int64_t)(p + 1) * stride >= ui.n) return;
+      ++p;
+      if (p == 32) nxt = unit_batch(units, ui, ib + 64 * stride, stride, lane);
+      if (p == 64) {
+        p = 0;
+        ib += 64 * stride;
+        cur = nxt;
+      }
+    }
   }
 }
 
@@ -1213,9 +1267,6 @@ __global__ __launch_bounds__(256) void k_lpa_units_giant(const int32_t* __restri
   ui.n = nunits;
   ui.lim = nunits;
   ui.list = nullptr;
-  Segment d0 = load_unit(units, ui, u), d1 = load_unit(units, ui, u + stride);
-  u32 ra[kChunks], rb[kChunks];
-  unit_load(ra, al, d0, lane);
   auto one = [&](const u32 (&raw)[kChunks], const Segment& d, int64_t id) {
     const int len = d.len & 1023;
     u32 lab[kChunks];
@@ -1231,19 +1282,31 @@ __global__ __launch_bounds__(256) void k_lpa_units_giant(const int32_t* __restri
       umx[id] = hm;
     }
   };
+  // descriptor batches and a label ring as k_lpa_units
+  constexpr int D = kUnitsRing;
+  int64_t ib = u;
+  UnitBatch cur = unit_batch(units, ui, ib, stride, lane), nxt;
+  nxt.begin = 0;
+  nxt.len = 0;
+  nxt.id = 0;
+  int p = 0;
+  u32 rl[D][kChunks];
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k) unit_load_nb(rl[k], al, unit_at(cur, nxt, k), lane);
   while (true) {
-    unit_load(rb, al, d1, lane);
-    Segment d2 = load_unit(units, ui, u + 2 * stride);
-    one(ra, d0, u);
-    u += stride;
-    if (u >= nunits) break;
-    unit_load(ra, al, d2, lane);
-    Segment d3 = load_unit(units, ui, u + 2 * stride);
-    one(rb, d1, u);
-    u += stride;
-    if (u >= nunits) break;
-    d0 = d2;
-    d1 = d3;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      unit_load_nb(rl[(k + D - 1) % D], al, unit_at(cur, nxt, p + D - 1), lane);
+      one(rl[k], unit_at(cur, nxt, p), ib + (int64_t)p * stride);
+      if (ib + (int64_t)(p + 1) * stride >= nunits) return;
+      ++p;
+      if (p == 32) nxt = unit_batch(units, ui, ib + 64 * stride, stride, lane);
+      if (p == 64) {
+        p = 0;
+        ib += 64 * stride;
+        cur = nxt;
+      }
+    }
   }
 }
 
