@@ -9,7 +9,7 @@ for r in $(seq 1 ${N:-2}); do
     timeout -k 10 300 python3 -u bench.py --config ${CFG:-C3} --no-cpu-baseline --no-outlier --no-quality ${ARGS} \
       > gpurun_out/ab_${CFG:-C3}_${v}_$r.json 2> gpurun_out/ab_${CFG:-C3}_${v}_$r.err || { tail -5 gpurun_out/ab_${CFG:-C3}_${v}_$r.err; exit 1; }
     python3 -c "
-import json,sys; d=json.load(open("gpurun_out/ab_${CFG:-C3}_${v}_$r.json"))
+import json,sys; d=json.load(open('gpurun_out/ab_${CFG:-C3}_${v}_$r.json'))
 print('$v', d['value'], d['ms_per_step'], d['baseline_method']['median_ms_per_superstep_2_to_10'][:4])"
   done
 done
