@@ -64,6 +64,8 @@ class LpaGraphInfo(ctypes.Structure):
         ("exchanges_giant", ctypes.c_int64),
         ("blocked_rows", ctypes.c_int64),
         ("blocked_pieces", ctypes.c_int64),
+        ("code_refresh", ctypes.c_int64),
+        ("graph_replays", ctypes.c_int64),
     ]
 
     def to_dict(self):
@@ -124,7 +126,9 @@ SIGNATURES = {
     "lpa_exchange_put": (ctypes.c_int, [_vp, _i32p]),
     "lpa_exchange_get_delta": (ctypes.c_int, [_vp, _vp, _i64p]),
     "lpa_exchange_put_delta": (ctypes.c_int, [_vp, _vp, _i64p, ctypes.c_int64]),
+    "lpa_abi_version": (ctypes.c_int, []),
     "lpa_graph_get_info": (ctypes.c_int, [_vp, ctypes.POINTER(LpaGraphInfo)]),
+    "lpa_graph_get_info_sized": (ctypes.c_int, [_vp, ctypes.POINTER(LpaGraphInfo), ctypes.c_int64]),
     "lpa_graph_destroy": (None, [_vp]),
     "lpa_last_error": (ctypes.c_char_p, []),
     "lpa_gen_rmat": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32,

@@ -457,7 +457,10 @@ int init_labels(lpa_graph* g) {
   LPA_HIP(hipMemsetD32Async((hipDeviceptr_t)g->fr_all, 1, 2, g->stream));
   LPA_HIP(hipMemsetAsync(g->fcnt, 0, sizeof(int32_t) * 32, g->stream));
   LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 8, g->stream));
-  if (g->gword) LPA_HIP(hipMemsetAsync(g->gword + 2, 0, sizeof(int32_t), g->stream));  // abits stale
+  if (g->gword) {
+    LPA_HIP(hipMemsetAsync(g->gword + 2, 0, sizeof(int32_t), g->stream));  // abits stale
+    LPA_HIP(hipMemsetAsync(g->gword + 5, 0, sizeof(int32_t), g->stream));  // no giant-code refresh pending
+  }
   g->cur = 0;
   g->since_reset = 0;
   g->force_all_next = false;
@@ -645,6 +648,15 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
     LPA_TRY(dev_alloc(g, (void**)&g->al0, sizeof(int32_t) * g->arcs));
     LPA_HIP(hipMemcpyAsync(g->al0, g->al, sizeof(int32_t) * g->arcs, hipMemcpyDeviceToDevice, s));
   }
+  // giant codes (lpa_iter.hip): one GPU, the LDS hot-set rebuild's label vectors, and
+  // a superstep 2 whose hub rows take the giant decision (block mode, or no hub rows)
+  g->code_ok = P == 1 && !g->pooled && !g->no_scatter && g->rebuild_hot && g->vpad >= kHotMinSlots &&
+               g->arcs > 0 && (g->n_hub == 0 || g->hub_lane_begin < g->n_hub);
+  if (g->code_ok) {
+    for (int b = 0; b < BIN_G64; ++b) g->code_p64 += g->bin_arcs[b];
+    LPA_TRY(dev_alloc(g, (void**)&g->code8, g->vpad));
+    LPA_TRY(dev_alloc(g, (void**)&g->al8, (size_t)((g->code_p64 + 511) / 512 * 512 + 512)));
+  }
   LPA_HIP(hipStreamSynchronize(s));
   // the kept edge list serves the outlier stage (single-GPU handles) and lpa_quality,
   // which a distributed job runs on rank 0: the other ranks release it (at C5 over 8
@@ -662,36 +674,11 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
 // H rows (in (class, column) order): per class, every row's class segment in <= 64-arc
 // pieces, row after row, then padding to a multiple of 8 pieces; class 7 also lists
 // the positions up to blk_a0, the 512-aligned start of the plain stream.
-// diagnostic (LPA_BLOCK_NAIVE=1, timing only, labels still exact): the listed range cut
-// into aligned 64-arc pieces, class x taking the x-th contiguous share -- the piece
-// machinery on a plain stream's access pattern
-__global__ void k_naive_pieces(int64_t a0, int64_t n, u64* __restrict__ pieces) {
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t p = 64 * j;
-    pieces[j] = ((u64)(a0 - p < 64 ? a0 - p : 64) << 32) | (u64)p;
-  }
-}
-
 int build_pieces(lpa_graph* g, int64_t H) {
   hipStream_t s = g->stream;
   const int C = g->blk_classes;
   int64_t aH = 0;
   LPA_HIP(hipMemcpyAsync(&aH, g->rp + H, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  if (getenv("LPA_BLOCK_NAIVE")) {
-    LPA_HIP(hipStreamSynchronize(s));
-    int64_t a0 = (aH + 511) / 512 * 512;
-    if (a0 > g->arcs) a0 = g->arcs;
-    const int64_t n = (a0 + 63) / 64;
-    const int64_t per = (n / C + 7) / 8 * 8;
-    for (int x = 0; x <= C; ++x) g->blk_off[x] = x == C ? (n + 7) / 8 * 8 : (x * per < n ? x * per : (n + 7) / 8 * 8);
-    LPA_TRY(dev_alloc(g, (void**)&g->blk_pieces, sizeof(u64) * (g->blk_off[C] > 0 ? g->blk_off[C] : 1)));
-    LPA_HIP(hipMemsetAsync(g->blk_pieces, 0, sizeof(u64) * (g->blk_off[C] > 0 ? g->blk_off[C] : 1), s));
-    hipLaunchKernelGGL(k_naive_pieces, dim3(grid_for(n)), dim3(256), 0, s, a0, n, g->blk_pieces);
-    LPA_HIP(hipGetLastError());
-    LPA_HIP(hipStreamSynchronize(s));
-    g->blk_a0 = a0;
-    return LPA_OK;
-  }
   uint32_t* seg = nullptr;
   int32_t* np = nullptr;
   int64_t* poff = nullptr;
@@ -836,10 +823,6 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
     int cb = 3;
     while ((1ll << cb) * (4ll << 20) < g->vpad * 4 && (1 << (cb + 1)) <= kMaxBlkClasses && blo + cb + 1 <= 32)
       ++cb;
-    if (g->block_classes_req >= 8)  // LPA_BLOCK_CLASSES (tests / A/B)
-      while ((1 << cb) < g->block_classes_req && (1 << (cb + 1)) <= kMaxBlkClasses && blo + cb + 1 <= 32) ++cb;
-    if (g->block_classes_req >= 8)
-      while ((1 << cb) > g->block_classes_req) --cb;
     g->blk_classes = 1 << cb;
     if (P == 1) {
       hipLaunchKernelGGL(k_emit_arcs_single, dim3(grid_for(m)), dim3(256), 0, s, g->e_src,

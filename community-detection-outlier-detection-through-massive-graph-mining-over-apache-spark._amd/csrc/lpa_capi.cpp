@@ -87,7 +87,7 @@ void destroy(lpa_graph* g) {
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
                   g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best, g->rstart,
                   g->blk_pieces, g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword, g->al0, g->abits,
-                  g->glist};
+                  g->glist, g->code8, g->al8};
   for (void* p : bufs) dev_free(g, p);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
@@ -163,12 +163,9 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_REBUILD_HOT")) g->rebuild_hot = atoi(f);
   if (const char* f = getenv("LPA_SERIAL")) g->serial = atoi(f);
   if (const char* f = getenv("LPA_LOCALITY")) g->locality = atoi(f);
-  if (const char* f = getenv("LPA_REBUILD_HYBRID")) g->rebuild_hybrid = atoi(f);
   if (const char* f = getenv("LPA_BLOCK_DEG")) g->block_deg = atoi(f);
   if (const char* f = getenv("LPA_BLOCK_MIN_SLOTS")) g->block_min_slots = atoll(f);
-  if (const char* f = getenv("LPA_BLOCK_CLASSES")) g->block_classes_req = atoi(f);
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
-  if (const char* f = getenv("LPA_CONV_STREAMS")) g->conv_streams = atoi(f) < 1 ? 1 : atoi(f) > 3 ? 3 : atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
   // internal builds (the outlier stage's L2 sub-graph): the locality order is a
@@ -570,6 +567,26 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->exchanges_giant = g->n_exch_giant;
   info->blocked_rows = g->blk_pieces ? g->blk_rows : 0;
   info->blocked_pieces = g->blk_pieces ? g->blk_off[g->blk_classes] : 0;
+  info->graph_replays = g->n_graph_replays;
+  if (g->code_ok && g->gword) {
+    int32_t w = 0;
+    LPA_HIP(hipMemcpyAsync(&w, g->gword + 5, sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));
+    LPA_HIP(hipStreamSynchronize(g->stream));
+    info->code_refresh = w;
+  }
+  return LPA_OK;
+}
+
+int lpa_abi_version(void) { return LPA_ABI_VERSION; }
+
+int lpa_graph_get_info_sized(const lpa_graph* g, lpa_graph_info* info, int64_t info_size) {
+  if (!info || info_size < 0) {
+    set_error("null info or negative size");
+    return LPA_EINVAL;
+  }
+  lpa_graph_info full;
+  LPA_TRY(lpa_graph_get_info(g, &full));
+  memcpy(info, &full, (size_t)(info_size < (int64_t)sizeof(full) ? info_size : (int64_t)sizeof(full)));
   return LPA_OK;
 }
 

@@ -159,6 +159,14 @@ int loop_allgather(lpa_graph* g, const void* send, void* recv, size_t bytes, hip
   }
   for (int q = 0; q < P; ++q)
     if (q != r) LPA_HIP(hipStreamWaitEvent(s, lb->rank_g[q]->loop_ev[1], 0));
+  // third meeting: every rank has queued its waits on the others' events, so no rank
+  // runs ahead into a stream capture (the converged supersteps' captured tally) while a
+  // peer still makes its stream wait on an event of the capturing stream -- the runtime
+  // refuses that ("dependency created on uncaptured work")
+  if (!lb->barrier()) {
+    set_error("loopback allgather: a peer rank did not arrive (aborted or timed out)");
+    return LPA_ERCCL;
+  }
   return LPA_OK;
 }
 

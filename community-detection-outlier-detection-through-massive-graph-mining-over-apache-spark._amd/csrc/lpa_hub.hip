@@ -804,14 +804,24 @@ __global__ __launch_bounds__(64 * kW) void k_hub_mid_all(const int32_t* __restri
 // two dependent launches fewer).  What is handed off was built only by device-scope
 // atomics, which execute at the memory side, past the per-XCD L2s: so every wave
 // waits for its atomics to complete (vmcnt), the block takes a ticket, and the block
-// that draws the last one reads the totals with agent-scope loads, does the follow-up
-// pass and resets the tickets.  No release / acquire fences: at agent scope they write
-// back / invalidate the whole L2 of the XCD, and 2048 blocks doing so cost ~90 us.
+// that draws the last one acquires at agent scope, reads the totals with agent-scope
+// loads, does the follow-up pass and resets the tickets.
+//   consumer (memory-model form): the winning ticket RMW is the one relaxed poll, then
+//     ONE agent-scope acquire in the winning lane (gfx950: `s_waitcnt vmcnt(0)
+//     lgkmcnt(0); buffer_inv sc1`, checked in the generated ISA of k_hub_count and
+//     k_hub_bucket), an `s_waitcnt` that holds the lane until the invalidate has
+//     completed, and the workgroup barrier before any wave of the block loads;
+//   producer: relaxed agent-scope atomics, each wave's `s_waitcnt` for them, the block
+//     barrier, then the relaxed ticket add.  A release on the ticket would lower to
+//     `buffer_wbl2 sc1` (write back the XCD L2's dirty lines), and the handed-off data
+//     leaves no dirty line there -- it is written only by device atomics, which execute
+//     at the memory side -- so the write-back has nothing to do for it; 2048 blocks
+//     issuing it cost ~90 us per launch.
 // Tickets are two-level (kTicketGroups counters, one 64-B line each, then one for the
 // groups): returning atomics on ONE address serialise at ~88 M/s, 2048 of them ~23 us.
-// This hand-off leans on gfx950 behaviour the HIP memory model does not promise (device
-// atomics on hipMalloc memory complete at the memory side once vmcnt drains; agent-scope
-// relaxed loads read past the XCD's L2), so the library is built for gfx950 only:
+// The producer side leans on gfx950 behaviour (device atomics on hipMalloc memory
+// complete at the memory side once vmcnt drains), so the library is built for gfx950
+// only:
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "lpa_hub.hip: the fused last-block hand-off is validated on gfx950 only"
 #endif
@@ -833,6 +843,13 @@ __device__ __forceinline__ bool last_block(uint32_t* tk) {
       __hip_atomic_store(t1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__hip_atomic_fetch_add(t2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
         __hip_atomic_store(t2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the winner alone acquires at agent scope (one block per launch, not every
+        // ticket): gfx950 emits `buffer_inv sc1` -- the CU's vector L1 and this XCD's
+        // L2 drop their lines, so the follow-up pass's loads cannot hit a line cached
+        // before the other blocks' atomics landed; the workgroup barrier below carries
+        // it to the block's other waves
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __builtin_amdgcn_s_waitcnt(0);  // the invalidate completes before the barrier releases the block
         last = 1;
       }
     }

@@ -125,6 +125,7 @@ struct lpa_graph {
   lpa::Loopback* loop = nullptr;
   hipEvent_t loop_ev[2] = {nullptr, nullptr};  // loopback: send-ready / copies-done marks
   int64_t n_exch_full = 0, n_exch_delta = 0;   // exchanges by mode (lpa_graph_info)
+  int64_t n_graph_replays = 0;                 // supersteps replayed from a captured graph
 
   int64_t V = 0, m = 0;
   int64_t slice = 0;      // vertex slots per rank
@@ -221,7 +222,17 @@ struct lpa_graph {
   uint32_t* gbits = nullptr;    // [vpad / 32] rebuild: bit u = (L[u] == G), the giant label
   int32_t* gword = nullptr;     // [8] G of the last refreshed vector (k_giant_pick), worth-trying flag,
                                 //     abits valid (bits-mode rebuild, no scatter since), [3] hot-slot
-                                //     giant-bit count (k_giant_bits), [4] superstep 4 bins: 0 = lists
+                                //     giant-bit count (k_giant_bits), [4] superstep 4 bins: 0 = lists,
+                                //     [5] giant-code refresh taken (superstep 2 settles from al8),
+                                //     [6] superstep 2's wave bins: 0 = lists of the unsettled rows
+  // giant codes (round 5, lpa_iter.hip "Giant codes"): the refresh after superstep 1 on
+  // a single GPU, when one label G carries the hubs but not half the hot slots (R-MAT),
+  // writes a 1-byte code per arc instead of al[] (code 0 = G, else an 8-bit label hash)
+  // for the rows above the row bins, and al[] only for the row bins' positions
+  bool code_ok = false;         // the handle can take that refresh (P = 1, hot-set rebuild)
+  uint8_t* code8 = nullptr;     // [vpad] code of every slot's label
+  uint8_t* al8 = nullptr;       // [code_p64 rounded up + 512] code of every arc's column label
+  int64_t code_p64 = 0;         // first arc position of the row bins (deg <= 64)
   unsigned long long* abits = nullptr;  // [arcs / 64] bit i = (al[i] == G): the bits-mode rebuild's by-product
   int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
   uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])
@@ -235,9 +246,6 @@ struct lpa_graph {
   int64_t n_chunk_scan = 0;     // chunks below this belong to every multi-chunk column
   int32_t* chlist = nullptr;    // [vpad] changed one-chunk columns (count: counters[par][0])
   int rebuild_hot = 1;                      // LDS hot-label rebuild (LPA_REBUILD_HOT=0 disables)
-  int rebuild_hybrid = 2;                   // G on 1/8..1/2 of the bit-range slots: 2 labels-mode
-                                            //   gathers + the arc giant bits, 1 also G from the bits
-                                            //   of cold columns, 0 neither (LPA_REBUILD_HYBRID, A/B)
   // class-blocked labels-mode rebuild (P = 1, lpa_iter.hip rebuild_pieces): rows of
   // degree > block_deg keep their columns in (class, column) order (col_class); the
   // class segments cut into <= 64-arc pieces, listed per class
@@ -248,12 +256,10 @@ struct lpa_graph {
                                             //   but C3 (64 MB of labels) 0.9 ms slower
   lpa::u64* blk_pieces = nullptr;           // [n] (len << 32 | first position)
   int blk_classes = 8;                      // 8 x phases (kMaxBlkClasses at most)
-  int block_classes_req = 0;                // LPA_BLOCK_CLASSES: force the class count (>= 8)
   int64_t blk_off[lpa::kMaxBlkClasses + 1] = {}; // class x: pieces [blk_off[x], blk_off[x + 1])
   int64_t blk_a0 = 0;                       // arcs [0, blk_a0) are listed (a multiple of 512)
   int64_t blk_rows = 0;                     // rows in (class, column) order
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
-  int conv_streams = 3;                     // LPA_CONV_STREAMS: streams of a converged superstep's tally
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per
   // (superstep, cur, par)

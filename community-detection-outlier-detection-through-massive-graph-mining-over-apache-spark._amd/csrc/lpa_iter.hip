@@ -41,7 +41,6 @@
 //   seg  deg > 1024     one wave per 512-arc unit (staged unit tally words), merged
 //                       per row by the hub combine (lpa_hub.hip)
 // Tables keep a touched-slot list: finishing a vertex costs O(distinct labels).
-#include <chrono>
 #include <stdio.h>
 #include <string.h>
 
@@ -1322,19 +1321,37 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
 // whose G votes exceed that sum without staging or merging a single word; only the
 // units of the rows it cannot settle are then tallied exactly (k_lpa_units, list mode).
 // Block 0 also zeroes the undecided-unit list count (*ndec) for k_hub_decide.
-__global__ __launch_bounds__(256) void k_lpa_units_giant(const int32_t* __restrict__ al,
+// T = uint8_t: the same from the giant codes al8 (code 0 = G; "Giant codes" below), the
+// form that runs when the refresh after superstep 1 took them (gsel[5]); T = int32_t
+// runs otherwise.
+template <typename T>
+__device__ __forceinline__ void unit_load_nb_t(u32 (&raw)[kChunks], const T* __restrict__ al, const Segment& d,
+                                               int lane) {
+  const int len = d.len & 1023;
+  const int last = len > 0 ? len - 1 : 0;
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) {
+    const int off = c * 64 + lane;
+    if constexpr (sizeof(T) == 4) raw[c] = ld_stream(reinterpret_cast<const int32_t*>(al) + d.begin + (off < last ? off : last));
+    else raw[c] = (u32)al[d.begin + (off < last ? off : last)];
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_lpa_units_giant(const T* __restrict__ al,
                                                          const Segment* __restrict__ units, int64_t nunits,
                                                          const int32_t* __restrict__ gsel,
                                                          uint32_t* __restrict__ ugc, uint32_t* __restrict__ umx,
                                                          int32_t* __restrict__ ndec) {
+  constexpr bool kCode = sizeof(T) == 1;
   __shared__ u32 hist_all[4][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0) ndec[0] = ndec[2] = 0;  // unit list, block-row list
+  if ((gsel[5] != 0) != kCode) return;  // the other form's turn (uniform)
   if (gsel[1] == 0) return;  // no giant label worth trying: k_hub_decide lists every row
   u32* hist = hist_all[w];
   hist[lane] = 0u;
-  const u32 G = (u32)gsel[0];
+  const u32 G = kCode ? 0u : (u32)gsel[0];
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t u = (int64_t)blockIdx.x * 4 + w;
   if (u >= nunits) return;  // no block-level barriers in this kernel
@@ -1367,11 +1384,11 @@ __global__ __launch_bounds__(256) void k_lpa_units_giant(const int32_t* __restri
   int p = 0;
   u32 rl[D][kChunks];
 #pragma unroll
-  for (int k = 0; k < D - 1; ++k) unit_load_nb(rl[k], al, unit_at(cur, nxt, k), lane);
+  for (int k = 0; k < D - 1; ++k) unit_load_nb_t<T>(rl[k], al, unit_at(cur, nxt, k), lane);
   while (true) {
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-      unit_load_nb(rl[(k + D - 1) % D], al, unit_at(cur, nxt, p + D - 1), lane);
+      unit_load_nb_t<T>(rl[(k + D - 1) % D], al, unit_at(cur, nxt, p + D - 1), lane);
       one(rl[k], unit_at(cur, nxt, p), ib + (int64_t)p * stride);
       if (ib + (int64_t)(p + 1) * stride >= nunits) return;
       ++p;
@@ -1425,8 +1442,11 @@ constexpr unsigned long long kForcedRebuild = 1ull << 62;
 // Label-dense supersteps (P = 1): the per-stream diffs only counted the changed slots.
 // More than 1/10 of the slots changed: the refresh rebuilds al[] (counters[1] forced),
 // so no position chunk is ever emitted; otherwise the full diff (mode 2) runs next.
-__global__ void k_dense_decide(unsigned long long* __restrict__ counters, int64_t n_slots) {
-  if (threadIdx.x == 0 && (int64_t)counters[2] * 10 > n_slots) counters[1] = kForcedRebuild;
+// A superstep after a giant-code refresh (gword[5]) always rebuilds: its al[] entries were
+// never written for the rows that superstep settled from codes.
+__global__ void k_dense_decide(unsigned long long* __restrict__ counters, int64_t n_slots,
+                               const int32_t* __restrict__ gword) {
+  if (threadIdx.x == 0 && ((int64_t)counters[2] * 10 > n_slots || gword[5] != 0)) counters[1] = kForcedRebuild;
 }
 // fcnt[] slot set by the row settle of a giant superstep (k_settle_*): the bin kernels
 // walk lists of the unsettled rows, but the diff scans every slot (settled rows may
@@ -2090,6 +2110,7 @@ __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__
     if (G != gword[0]) gword[2] = 0;  // the arc giant bits are relative to the old G
     gword[0] = G;
     gword[3] = 0;  // k_giant_bits counts the set bits of the hot slots here
+    gword[5] = 0;  // no giant-code refresh unless k_code_mode takes it below
     gword[1] = n > 0 && 5 * (int64_t)(m >> 32) >= n ? 1 : 0;
   }
 }
@@ -2234,7 +2255,9 @@ __device__ __forceinline__ void pipe3(int64_t nb, Pre pre, F fetch, Q probe, R r
   LPA_PIPE_STEP(GUARD, 3, c0, c1, c2, w1, w0, r1, r0)        \
   LPA_PIPE_STEP(GUARD, 4, c1, c2, c0, w0, w1, r0, r1)        \
   LPA_PIPE_STEP(GUARD, 5, c2, c0, c1, w1, w0, r1, r0)
-  while (t + 9 <= nb) {
+  // unguarded cycles: their last step (t + 5) issues pre(t + 9), so t + 9 < nb keeps
+  // every descriptor read inside the list (a piece list has no padding past its end)
+  while (t + 10 <= nb) {
     LPA_PIPE_CYCLE(false)
   }
   while (true) {
@@ -2421,9 +2444,11 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
                                                          int slice_lg, int hot_lg, int hb_lg,
                                                          const uint32_t* __restrict__ gbits, int64_t nbits,
                                                          int32_t* __restrict__ gword,
-                                                         unsigned long long* __restrict__ abits, int allow_hyb,
-                                                         const u64* __restrict__ pieces, BlkInfo blk) {
+                                                         unsigned long long* __restrict__ abits,
+                                                         const u64* __restrict__ pieces, BlkInfo blk,
+                                                         const int32_t* __restrict__ skip) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
+  if (skip && *skip) return;  // the giant-code refresh replaces this rebuild (k_code_mode)
   __shared__ u32 hot[kHotLabelsSingle];
   u32* s_cnt = &hot[kHotLabelsSingle - 1];   // beyond the bit words; labels mode refills it
   // ---- the giant-label bits of the hot slots, and how many are set ----
@@ -2443,14 +2468,11 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
   if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(s_cnt, (u32)cnt);
   __syncthreads();
   const bool bits = 2 * (int64_t)*s_cnt >= nhb && nhb > 0;  // uniform: the same data in every block
-  // hybrid (P = 1): G on >= 1/8 of the bit-range slots but not on half -- the hot
-  // slots' LABELS in LDS, a cold column's bit from gbits, its label gathered only when
-  // the bit is clear (Chung-Lu C5 superstep 2: G on ~40 % of the arcs, ~30 % of the cold
-  // gathers become L2 / Infinity-Cache hits on the 5 MB bit array)
-  const bool hyb = !kRanked && allow_hyb && !bits && 8 * (int64_t)*s_cnt >= nhb && nhb > 0;
-  // allow_hyb 2: labels-mode gathers, only the arc giant bits written (the next superstep's
-  // settle); 1: cold columns also take G from their bit
-  const bool hyb_bits = hyb && allow_hyb == 1;
+  // hybrid (P = 1): G on >= 1/8 of the bit-range slots but not on half -- labels-mode
+  // gathers that also write the arc giant bits (the next superstep's settle).  (Taking a
+  // cold column's G from its gbits bit instead of its label measured slower: C5 186.7 ->
+  // 176.4 GTEPS.)
+  const bool hyb = !kRanked && !bits && 8 * (int64_t)*s_cnt >= nhb && nhb > 0;
   const int32_t G = gword[0];
   // bits / hybrid modes also write the arc giant bits (abits: bit i = al[i] == G, one
   // ballot per 64 arcs), which the next superstep's full tally settles rows from
@@ -2526,21 +2548,6 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
             return g ? G : x;
           },
           true);
-    } else if (hyb_bits) {
-      run(
-          [&](int c) -> u32 {
-            const bool h = (u32)c < nh;
-            const u32 hw = hot[h ? (u32)c : nh - 1u];
-            const u32 gw = gbits[h ? 0u : (u32)c >> 5];
-            return h ? hw : gw;
-          },
-          [&](int c, u32 w) -> int32_t {
-            const bool h = (u32)c < nh;
-            const bool g = !h && ((w >> ((u32)c & 31u)) & 1u);
-            const int32_t x = Ln[(h || g) ? 0 : c];
-            return h ? (int32_t)w : (g ? G : x);
-          },
-          true);
     } else {
       run([&](int c) -> u32 { return hot[(u32)c < nh ? (u32)c : nh - 1u]; },
           [&](int c, u32 w) -> int32_t {
@@ -2578,6 +2585,276 @@ __global__ __launch_bounds__(256) void k_al_rebuild_small(const unsigned long lo
     return Ln[c];
   };
   rebuild_stream(lab, G, true, col, arcs, al, abits);
+}
+
+// ---------------------------------------------------------------------------
+// Giant codes (round 5): the refresh after superstep 1 without the labels-mode al[]
+// rebuild.  On R-MAT the labels L1 of superstep 1 already have a giant label G (the
+// label of ~97 % of the 1,024 top hubs, ~37 % of the arcs' columns) but not on half the
+// hot slots, so that refresh gathered a full 4-B label per arc (C3: 2.35 ms, 3.6x its
+// algorithmic bytes in L2-missing lines), and superstep 2 read them back only to
+// decide nearly every row for G: a row's G votes above every bucket of a label hash of
+// its other votes make G its strict mode (giant_count; oracle, R-MAT-22: 98 % of the
+// arcs sit in rows so decided with 16 buckets, 100 % of the rows above 64 arcs).
+// A bucket only needs a FUNCTION of the label, so the refresh writes instead:
+//   code8[u]  per slot, 0 = (L1[u] == G), else 1 + an 8-bit hash of L1[u]  (k_code_build)
+//   al8[i]    per arc of the rows above the row bins, code8[col[i]]       (k_code_rebuild,
+//             the hot slots' labels from LDS as in labels mode, the rest gathered as
+//             1-B codes from a 16 MB array -- at C3 the hot 1 M slots are 1 MB of it)
+//   al[i]     per arc of the row bins (<= 64 arcs: 14-18 % of the arcs), their labels
+// and superstep 2 decides the hub rows (k_lpa_units_giant<uint8_t> + k_hub_decide) and
+// the wave-bin rows (k_code_settle_waves) from al8; only the rows left undecided get
+// their al[] entries gathered (k_code_partial_*) and are tallied exactly, in list mode.
+// The row bins tally from al as before.  Exact for any G and any hash (a label's count
+// is at most its bucket's); gword[5] marks the refresh taken, so the labels-mode
+// rebuild is skipped and superstep 2's refresh rebuilds al[] whatever the change count.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u32 giant_code(u32 x, u32 G) {
+  return x == G ? 0u : 1u + ((((x * 0x9E3779B1u) >> 24) * 255u) >> 8);
+}
+
+// gword[5] = take the giant-code refresh: a rebuild is wanted, G is worth trying, and the
+// bits-mode rebuild (G on >= half the hot slots) does not apply; no arc giant bits then
+__global__ void k_code_mode(const unsigned long long* __restrict__ counters, int64_t thr, int64_t nhb,
+                            int32_t* __restrict__ gword) {
+  if (threadIdx.x != 0) return;
+  const bool on = rebuild_wanted(counters, thr) && gword[1] != 0 && 2 * (int64_t)gword[3] < nhb;
+  gword[5] = on ? 1 : 0;
+  if (on) gword[2] = 0;
+}
+
+// code8[u] for every slot (four per 4-B store; vpad is a multiple of 64)
+__global__ __launch_bounds__(256) void k_code_build(const int4* __restrict__ L4, int64_t n4,
+                                                   const int32_t* __restrict__ gword, uint32_t* __restrict__ c4) {
+  if (gword[5] == 0) return;
+  const u32 G = (u32)gword[0];
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const int4 v = L4[q];
+    c4[q] = giant_code((u32)v.x, G) | (giant_code((u32)v.y, G) << 8) | (giant_code((u32)v.z, G) << 16) |
+            (giant_code((u32)v.w, G) << 24);
+  }
+}
+
+// pipe3 over this wave's whole 512-arc batches in [bat0, bat1) (grid-stride by waves)
+template <typename P1, typename P2, typename St>
+__device__ __forceinline__ void range_pipe(P1 p1, P2 p2, St st, const int32_t* __restrict__ col, int64_t bat0,
+                                           int64_t bat1) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nb = bat0 + wv < bat1 ? (bat1 - bat0 - wv + nw - 1) / nw : 0;
+  auto base = [&](int64_t t) { return (bat0 + wv + t * nw) * 512; };
+  auto pre = [](int64_t, int) {};
+  auto fetch = [&](int64_t t, int32_t (&c)[8], int) {
+    const int64_t b = base(t);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + b + k * 64 + lane);
+  };
+  auto probe = [&](const int32_t (&c)[8], u32 (&w)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = p1(c[k]);
+  };
+  auto resolve = [&](const int32_t (&c)[8], const u32 (&w)[8], int32_t (&r)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = p2(c[k], w[k]);
+  };
+  auto store = [&](int64_t t, const int32_t (&r)[8], int) { st(base(t), r); };
+  pipe3(nb, pre, fetch, probe, resolve, store);
+}
+
+// al for [pB, arcs) (pB = code_p64 rounded down to a 512-arc batch) and al8 for [0, pA)
+// (pA = code_p64 rounded up, at most the full batches): the batch across code_p64 gets
+// both; the partial last batch (one wave) writes whichever applies.  One 1024-thread
+// block per CU, 160 KB of LDS: the row bins' labels first, with the 40,960 hottest labels
+// in LDS, then the codes, with the 163,840 hottest slots' CODES in LDS -- the gathers are
+// bound by their lane count, not their bytes (1-B codes from a 16 MB array cost nearly
+// what 4-B labels from 64 MB did), so the wider LDS share is the lever.
+__global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict__ gword,
+                                                       const int32_t* __restrict__ col, int64_t arcs,
+                                                       const int32_t* __restrict__ Ln, int64_t nslots,
+                                                       const uint8_t* __restrict__ code8, int64_t p64,
+                                                       uint8_t* __restrict__ al8, int32_t* __restrict__ al) {
+  if (gword[5] == 0) return;
+  __shared__ u32 hot[kHotLabelsSingle];
+  const u32 G = (u32)gword[0];
+  const int lane = threadIdx.x & 63;
+  const int64_t nfull = arcs >> 9;
+  const int64_t bA = min((p64 + 511) >> 9, nfull), bB = p64 >> 9;
+  // ---- the row bins' labels ----
+  const u32 nh = (u32)(nslots < kHotLabelsSingle ? nslots : kHotLabelsSingle);
+  for (u32 i = threadIdx.x; i < nh; i += 1024) hot[i] = (u32)Ln[i];
+  __syncthreads();
+  range_pipe([&](int c) -> u32 { return hot[(u32)c < nh ? (u32)c : nh - 1u]; },
+             [&](int c, u32 w) -> int32_t {
+               const bool h = (u32)c < nh;
+               const int32_t x = Ln[h ? 0 : c];
+               return h ? (int32_t)w : x;
+             },
+             [&](int64_t b, const int32_t (&r)[8]) {
+#pragma unroll
+               for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + b + k * 64 + lane);
+             },
+             col, bB, nfull);
+  // ---- the codes of the rows above ----
+  __syncthreads();
+  const u32 nc = (u32)(nslots < 4 * kHotLabelsSingle ? nslots : 4 * kHotLabelsSingle);
+  const uint8_t* hc = reinterpret_cast<const uint8_t*>(hot);
+  for (u32 q = threadIdx.x; q < nc / 4; q += 1024) hot[q] = reinterpret_cast<const uint32_t*>(code8)[q];
+  __syncthreads();
+  range_pipe([&](int c) -> u32 { return (u32)hc[(u32)c < nc ? (u32)c : nc - 1u]; },
+             [&](int c, u32 w) -> int32_t {
+               const bool h = (u32)c < nc;
+               const u32 x = code8[h ? 0 : c];
+               return (int32_t)(h ? w : x);
+             },
+             [&](int64_t b, const int32_t (&r)[8]) {
+#pragma unroll
+               for (int k = 0; k < 8; ++k) al8[b + k * 64 + lane] = (uint8_t)r[k];
+             },
+             col, 0, bA);
+  // the partial last batch
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((nfull << 9) < arcs && wv == nfull % nw) {
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = (nfull << 9) + k * 64 + lane;
+      if (i < arcs) {
+        const int32_t c = col[i];
+        const u32 x = (u32)Ln[c];
+        if (i < p64) al8[i] = (uint8_t)giant_code(x, G);
+        else al[i] = (int32_t)x;
+      }
+    }
+  }
+}
+
+// Superstep 2, the rows [vbeg, vend) of one wave bin (64 * NC / 2 < deg <= 64 * NC): one
+// wave per row decides G from the row's al8 codes (its G votes above every one of 64
+// code buckets, as giant_decide) -- the label, and a clear dirty flag -- or flags the
+// row (rdirty = 1) for the wave bins' list mode (gword[6] = 0: their "fr_all"; 1 when no
+// code refresh was taken, and then nothing else happens here).  k_lpa_wave's schedule:
+// row bounds by 64-row batches (span_batch), the codes of the next D - 1 rows in flight
+// (branch-free byte loads at clamped positions), the decision of the current one.
+template <int NC>
+__global__ __launch_bounds__(256) void k_code_settle_wave(const int64_t* __restrict__ rp,
+                                                          const uint8_t* __restrict__ al8, int64_t vbeg,
+                                                          int64_t vend, int32_t* __restrict__ gword,
+                                                          int32_t* __restrict__ Ln, uint8_t* __restrict__ rdirty) {
+  constexpr int D = NC <= 4 ? 4 : 3;
+  __shared__ u32 hist_all[4][64];
+  const bool on = gword[5] != 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[6] = on ? 0 : 1;
+  if (!on) return;  // uniform
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  u32* hist = hist_all[w];
+  hist[lane] = 0u;
+  const int32_t G = gword[0];
+  BinRows br;
+  br.vbeg = vbeg;
+  br.n = vend - vbeg;
+  br.list = nullptr;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t ib = (int64_t)blockIdx.x * 4 + w;
+  if (ib >= br.n) return;
+  auto load = [&](u32 (&x)[NC], const RowSpan& r) {
+    const int d = span_len(r);
+    const int last = d > 0 ? d - 1 : 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int off = c * 64 + lane;
+      x[c] = (u32)al8[r.b + (off < last ? off : last)];
+    }
+  };
+  SpanBatch cur = span_batch(rp, br, ib, stride, lane), nxt;
+  nxt.b = nxt.e = 0;
+  nxt.v = 0;
+  int p = 0;
+  u32 rl[D][NC];
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k) load(rl[k], span_at(cur, nxt, k));
+  while (true) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      load(rl[(k + D - 1) % D], span_at(cur, nxt, p + D - 1));
+      const RowSpan sp = span_at(cur, nxt, p);
+      const int64_t v = (int64_t)__builtin_amdgcn_readlane(cur.v, p);
+      const int d = span_len(sp);
+      u32 lab[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) lab[c] = c * 64 + lane < d ? rl[k][c] : kNone;
+      const u32 cg = wave_sum_u32(giant_count<NC>(lab, NC, 0u, hist, kGiantLg));
+      __builtin_amdgcn_wave_barrier();  // no reordering across (LDS ops of a wave complete in order)
+      const u32 hb = hist[lane];
+      hist[lane] = 0u;
+      const bool settled = cg > wave_max_u32(hb);
+      if (lane == 0) {
+        if (settled) Ln[v] = G;
+        rdirty[v] = settled ? 0 : 1;
+      }
+      if (ib + (int64_t)(p + 1) * stride >= br.n) return;
+      ++p;
+      if (p == 32) nxt = span_batch(rp, br, ib + 64 * stride, stride, lane);
+      if (p == 64) {
+        p = 0;
+        ib += 64 * stride;
+        cur = nxt;
+      }
+    }
+  }
+}
+
+// al[i] = L[col[i]] over the arcs of the rows the code settle left (the wave bins' lists
+// [b0, b1) of this superstep), one wave per row
+__global__ __launch_bounds__(256) void k_code_partial_rows(const int32_t* __restrict__ gword,
+                                                           const int64_t* __restrict__ rp,
+                                                           const int32_t* __restrict__ col,
+                                                           const int32_t* __restrict__ L, int32_t* __restrict__ al,
+                                                           const int32_t* __restrict__ flist,
+                                                           const int32_t* __restrict__ fcnt, BinBounds bb, int b0,
+                                                           int b1) {
+  if (gword[5] == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int64_t total = 0;
+  for (int b = b0; b < b1; ++b) total += fcnt[b];
+  for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < total; i += (int64_t)gridDim.x * 4) {
+    int64_t acc = 0;
+    int b = b0;
+    while (i >= acc + fcnt[b]) acc += fcnt[b++];
+    const int64_t v = flist[bb.b[b] + (i - acc)];
+    const int64_t e = rp[v + 1];
+    for (int64_t p = rp[v] + lane; p < e; p += 64) al[p] = L[col[p]];
+  }
+}
+
+// ... and over the hub rows k_hub_decide left: the block-tier rows of glist (count
+// gdec[2]) and the units of ulist2 (count gdec[0]), one wave per row or unit
+__global__ __launch_bounds__(256) void k_code_partial_hub(const int32_t* __restrict__ gword,
+                                                          const int64_t* __restrict__ rp,
+                                                          const int32_t* __restrict__ col,
+                                                          const int32_t* __restrict__ L, int32_t* __restrict__ al,
+                                                          const int32_t* __restrict__ glist,
+                                                          const int32_t* __restrict__ ulist2,
+                                                          const int32_t* __restrict__ gdec,
+                                                          const Segment* __restrict__ segs) {
+  if (gword[5] == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nr = gdec[2], total = nr + gdec[0];
+  for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < total; i += (int64_t)gridDim.x * 4) {
+    int64_t b, e;
+    if (i < nr) {
+      const int64_t v = glist[i];
+      b = rp[v];
+      e = rp[v + 1];
+    } else {
+      const Segment sg = segs[ulist2[i - nr]];
+      b = sg.begin;
+      e = b + (sg.len & 1023);
+    }
+    for (int64_t p = b + lane; p < e; p += 64) al[p] = L[col[p]];
+  }
 }
 
 __global__ void k_gather_dense(const int32_t* __restrict__ L, const int32_t* __restrict__ new_of,
@@ -2844,15 +3121,19 @@ int launch_first(lpa_graph* g, int32_t* Lown) {
   return LPA_OK;
 }
 
+// the refresh after superstep 1 of a single-GPU handle may take the giant codes
+bool code_refresh_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset == 0; }
+// ... and superstep 2 then settles from them
+bool code_tally_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset == 1; }
+
 int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc,
                  const int32_t* Ln, bool diff) {
   hipStream_t s = g->stream;
   // LPA_SERIAL=1 (profiling only): every tally kernel on the main stream, so a
   // kernel trace shows each kernel's standalone duration
-  // converged supersteps (captured graphs): LPA_CONV_STREAMS = 3 (main + two bin streams,
-  // default), 2 (one bin stream) or 1 (everything on the main stream)
-  const bool conv = g->since_reset >= kDenseSupersteps + 2;
-  const int nstr = g->serial ? 1 : (conv ? g->conv_streams : 3);
+  // (three streams in every superstep, the converged ones too: 2 or 1 measured slower,
+  // the bin chains' overlap is worth more than the fork / join dependencies)
+  const int nstr = g->serial ? 1 : 3;
   hipStream_t sb = nstr >= 2 ? g->aux_stream[0] : s;
   hipStream_t sc = nstr >= 3 ? g->aux_stream[1] : sb;
   const int64_t* bb = g->bin_begin;
@@ -2919,7 +3200,33 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     }
     // frontier lists of this superstep (no-op when every row is tallied)
     LPA_TRY(launch_frontier_lists(g));
+    if (code_tally_now(g)) {
+      // superstep 2 after a giant-code refresh (each kernel returns at once otherwise,
+      // leaving the wave bins in range mode): the wave-bin rows settled from their codes,
+      // the others listed, their al[] entries gathered
+#define LPA_CODE_SETTLE(BIN, NC)                                                                         \
+  {                                                                                                      \
+    const int64_t n = bb[BIN + 1] - bb[BIN];                                                              \
+    hipLaunchKernelGGL(k_code_settle_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, s, g->rp,  \
+                       g->al8, bb[BIN], bb[BIN + 1], g->gword, Lown, g->rdirty[g->par]);                   \
+    LPA_HIP(hipGetLastError());                                                                          \
   }
+      // (every launch sets gword[6], also over an empty bin: the wave bins' flag)
+      LPA_CODE_SETTLE(BIN_W16, 16)
+      LPA_CODE_SETTLE(BIN_W8, 8)
+      LPA_CODE_SETTLE(BIN_W4, 4)
+      LPA_CODE_SETTLE(BIN_W2, 2)
+#undef LPA_CODE_SETTLE
+      LPA_TRY(launch_frontier_lists(g, s, g->gword + 6));
+      BinBounds bnd;
+      for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = bb[b];
+      hipLaunchKernelGGL(k_code_partial_rows, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
+                         g->flist, fcnt, bnd, (int)BIN_W16, (int)BIN_G64);
+      LPA_HIP(hipGetLastError());
+    }
+  }
+  // the wave bins' "fr_all": superstep 2 after a giant-code refresh walks the lists above
+  const int32_t* fr_wave = code_tally_now(g) ? g->gword + 6 : fr_bins;
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (sb != s) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
@@ -2996,10 +3303,20 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   }
   const int64_t n_units = blk ? g->unit_block2_begin : g->n_segs;
   if (giant_units && g->n_segs > 0) {
-    hipLaunchKernelGGL(k_lpa_units_giant, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s, g->al,
-                       g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
+    hipLaunchKernelGGL(k_lpa_units_giant<int32_t>, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
+                       g->al, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
     LPA_HIP(hipGetLastError());
+    if (code_tally_now(g)) {  // the form on the giant codes (one of the two returns at once)
+      hipLaunchKernelGGL(k_lpa_units_giant<uint8_t>, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
+                         g->al8, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
+      LPA_HIP(hipGetLastError());
+    }
     LPA_TRY(launch_hub_decide(g, Lown, g->n_hub, gsel));
+    if (code_tally_now(g)) {  // the undecided hub rows' al[] entries (code refresh only)
+      hipLaunchKernelGGL(k_code_partial_hub, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
+                         g->glist, g->ulist2, g->gdec, g->segs);
+      LPA_HIP(hipGetLastError());
+    }
     // the wide tier's few undecided rows right here on the main stream (the fourth
     // stream shares a hardware queue with aux1, whose row bins it would delay)
     if (split) LPA_TRY(launch_block_wide(s));
@@ -3058,10 +3375,10 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // row/group bins (round 4: superstep 2's tail bins g16 .. g1 on the main stream, ahead
   // of the hub combine, measured slower -- 2.08 -> 2.11 ms)
   hipStream_t st_tail = sc;
-  LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_bins)
-  LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_bins)
-  LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_bins)
-  LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_bins)
+  LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_wave)
+  LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_wave)
+  LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_wave)
+  LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_wave)
   LPA_ROWS_LAUNCH(BIN_G64, 64, fr_bins, sc)
   LPA_ROWS_LAUNCH(BIN_G32, 32, fr_bins, sc)
   LPA_ROWS_LAUNCH(BIN_G16, 16, fr_bins, st_tail)
@@ -3110,6 +3427,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
 int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
                    const unsigned long long* ctr) {
   hipStream_t s = g->stream;
+  const bool code = if_wanted && code_refresh_now(g);
   // the giant label of the refreshed vector: the rebuild's bits below and the next
   // superstep's tallies (launch_tally's gsel) read it
   if (g->V > 0) {
@@ -3170,13 +3488,26 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
                      g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \
-                     g->rebuild_hybrid, blk ? g->blk_pieces : nullptr, binfo)
+                     blk ? g->blk_pieces : nullptr, binfo, code ? g->gword + 5 : nullptr)
+    if (code) {
+      hipLaunchKernelGGL(k_code_mode, dim3(1), dim3(64), 0, s, ctr, thr,
+                         (int64_t)(g->vpad < kHotBits ? g->vpad : kHotBits), g->gword);
+      LPA_HIP(hipGetLastError());
+    }
     if (if_wanted) {
       if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
     } else {
       if (ranked) LPA_HOT_LAUNCH(false, true); else LPA_HOT_LAUNCH(false, false);
     }
 #undef LPA_HOT_LAUNCH
+    if (code) {
+      LPA_HIP(hipGetLastError());
+      hipLaunchKernelGGL(k_code_build, dim3(cap_grid((g->vpad / 4 + 255) / 256, 4096)), dim3(256), 0, s,
+                         (const int4*)L, g->vpad / 4, g->gword, (uint32_t*)g->code8);
+      LPA_HIP(hipGetLastError());
+      hipLaunchKernelGGL(k_code_rebuild, dim3(dev_cus), dim3(1024), 0, s, g->gword, g->col, g->arcs, L,
+                         g->vpad, g->code8, g->code_p64, g->al8, g->al);
+    }
   } else {
     const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
     if (if_wanted)
@@ -3229,7 +3560,7 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   if (dense_refresh(g) && !(diff_done && exchanges(g))) {
     // counted changed slots (in the tally, or here) -> rebuild, or the full diff
     if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, false, par, 0, 0, 1));
-    hipLaunchKernelGGL(k_dense_decide, dim3(1), dim3(64), 0, s, ctr, nd);
+    hipLaunchKernelGGL(k_dense_decide, dim3(1), dim3(64), 0, s, ctr, nd, g->gword);
     LPA_HIP(hipGetLastError());
     LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, true, par, 0, 0, 2));
   } else if (!diff_done) {
@@ -3310,18 +3641,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
   // k (k < kTallyKernels), then kTallyEv after the join, +1 after the exchange, +2
   // after the diff + scatter, +3 after the rebuild, +4 / +5 around the frontier lists
   bool blk_ran[LPA_STATS_MAX_ITERS] = {};  // serialized stats: k_lpa_block ran in superstep t
-  // LPA_HOST_TIMING=1 (diagnostic): host enqueue time per superstep and the final
-  // wait, on stderr -- whether a call is bound by the host's launches or the GPU
-  static const bool host_timing = getenv("LPA_HOST_TIMING") && atoi(getenv("LPA_HOST_TIMING"));
-  const auto h0 = std::chrono::steady_clock::now();
-  double h_prev = 0.0;
-  auto h_ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); };
   for (int32_t t = 0; t < n; ++t) {
-    if (host_timing && t > 0) {
-      const double h = h_ms();
-      fprintf(stderr, "[lpa host] superstep %d enqueue %.3f ms\n", (int)g->since_reset, h - h_prev);
-      h_prev = h;
-    }
     if (t < nt) blk_ran[t] = block_mode_now(g);
     const int32_t* Lc = g->lab[g->cur];
     int32_t* Ln = g->lab[g->cur ^ 1];
@@ -3362,25 +3682,25 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
           return rc;
         }));
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
+      ++g->n_graph_replays;
       if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
       g->cur ^= 1;
       g->par ^= 1;
       ++g->since_reset;
       continue;
     }
-    if (g->use_graphs && exchanges(g) && g->loop == nullptr && !g->serial &&
-        g->since_reset >= eager) {
+    if (g->use_graphs && exchanges(g) && !g->serial && g->since_reset >= eager) {
       // P > 1: the tally (no collective inside) replays a captured graph per
       // (cur, par); the exchange, whose delta size the host reads, and the refresh
-      // follow on the stream.  Not for a loopback group: its ranks are threads of one
-      // process, and a capture on one rank's stream while another rank's thread waits
-      // on the group's events fails in the runtime ("dependency created on uncaptured
-      // work", P = 8) -- one process per GPU (RCCL) never has two handles.
+      // follow on the stream.  A loopback group (ranks = threads of one process) runs
+      // this same path: its allgather ends with a third host meeting, after which no
+      // peer waits on an event of this rank's stream while it captures (lpa_comm.cpp).
       const int key = g->cur * 2 + g->par;
       if (!g->gexec[key])
         LPA_TRY(capture_graph(g, &g->gexec[key],
                               [&]() -> int { return launch_tally(g, Lown, nullptr, Lc, Ln, diff_in_tally); }));
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
+      ++g->n_graph_replays;
     } else if (first) {
       LPA_TRY(launch_first(g, Lown));
     } else if (early_graph) {
@@ -3395,6 +3715,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
           return rc;
         }));
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
+      ++g->n_graph_replays;
     } else {
       LPA_TRY(launch_tally(g, Lown, bev, Lc, Ln, diff_in_tally));
     }
@@ -3428,11 +3749,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     ++g->since_reset;
   }
   if (timed) LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS + 1], s));
-  const double h_enq = host_timing ? h_ms() : 0.0;
   LPA_HIP(hipStreamSynchronize(s));
-  if (host_timing)
-    fprintf(stderr, "[lpa host] superstep %d enqueue %.3f ms; call: enqueue %.3f ms, final wait %.3f ms\n",
-            (int)g->since_reset, h_enq - h_prev, h_enq, h_ms() - h_enq);
   if (n > 0) {
     int32_t err = 0;
     LPA_HIP(hipMemcpy(&err, g->dev_err, sizeof(err), hipMemcpyDeviceToHost));

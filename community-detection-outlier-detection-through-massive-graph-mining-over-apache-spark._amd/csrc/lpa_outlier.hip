@@ -132,18 +132,19 @@ __global__ void k_t_keys(const u64* __restrict__ ek, int64_t n, u64* __restrict_
 __global__ void k_t_src(const u64* __restrict__ ek, const u64* __restrict__ t, int64_t n, uint32_t* __restrict__ ts) {
   GRID_STRIDE(j, n) ts[j] = (uint32_t)(ek[(u32)t[j]] >> 32);
 }
-// first index of every vertex's run in keys sorted by their high 32 bits ([V + 1])
+// first index of every vertex's run in keys sorted by their high 32 bits ([V + 1]):
+// off[v] = lower_bound(v) by a binary search per vertex, so a long run of edgeless
+// vertices costs no thread a serial fill (neighbouring vertices walk the same upper
+// levels of the search, which stay cached)
 __global__ void k_run_offsets(const u64* __restrict__ k, int64_t n, int64_t V, int64_t* __restrict__ off) {
-  if (n == 0) {
-    GRID_STRIDE(v, V + 1) off[v] = 0;
-    return;
-  }
-  GRID_STRIDE(i, n) {
-    const int64_t cur = (int64_t)(k[i] >> 32);
-    const int64_t prev = i == 0 ? -1 : (int64_t)(k[i - 1] >> 32);
-    for (int64_t v = prev + 1; v <= cur; ++v) off[v] = i;
-    if (i == n - 1)
-      for (int64_t v = cur + 1; v <= V; ++v) off[v] = n;
+  GRID_STRIDE(v, V + 1) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = lo + ((hi - lo) >> 1);
+      if ((int64_t)(k[mid] >> 32) < v) lo = mid + 1;
+      else hi = mid;
+    }
+    off[v] = lo;
   }
 }
 
@@ -319,9 +320,9 @@ int transposed_edges(lpa_graph* g) {
     LPA_HIP(hipGetLastError());
     LPA_HIP(hipStreamSynchronize(s));   // the scratch is freed on return
   }
-  hipLaunchKernelGGL(k_run_offsets, dim3(grid_for(md > V ? md : V + 1)), dim3(256), 0, s, g->de_keys, md, V,
+  hipLaunchKernelGGL(k_run_offsets, dim3(grid_for(V + 1)), dim3(256), 0, s, g->de_keys, md, V,
                      g->de_out_off);
-  hipLaunchKernelGGL(k_run_offsets, dim3(grid_for(md > V ? md : V + 1)), dim3(256), 0, s, g->de_t, md, V,
+  hipLaunchKernelGGL(k_run_offsets, dim3(grid_for(V + 1)), dim3(256), 0, s, g->de_t, md, V,
                      g->de_in_off);
   LPA_HIP(hipGetLastError());
   return LPA_OK;

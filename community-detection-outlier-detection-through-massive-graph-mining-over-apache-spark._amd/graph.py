@@ -109,7 +109,7 @@ class Graph:
     # -- LPA ----------------------------------------------------------------
     def info(self) -> dict:
         info = _lib.LpaGraphInfo()
-        _lib.check(self._lib.lpa_graph_get_info(self._handle(), ctypes.byref(info)))
+        _lib.check(self._lib.lpa_graph_get_info_sized(self._handle(), ctypes.byref(info), ctypes.sizeof(info)))
         return info.to_dict()
 
     def reset(self):

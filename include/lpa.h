@@ -83,6 +83,11 @@ typedef struct lpa_graph_info {
   int64_t blocked_rows;    /* P = 1: rows whose columns are in (class, column) order for
                               the class-blocked al[] rebuild (0: off, LPA_BLOCK_DEG)  */
   int64_t blocked_pieces;  /* ... and the rebuild's piece-list length                */
+  int64_t code_refresh;    /* 1: the last refresh took the giant codes (P = 1: superstep 2
+                              settles rows from 1-byte label codes) -- read
+                              after a superstep-1 step; 0 otherwise (since ABI 6)      */
+  int64_t graph_replays;   /* supersteps run by replaying a captured HIP graph (the
+                              converged ones, P = 1 also supersteps 2-3; since ABI 6)  */
 } lpa_graph_info;
 
 /* Outlier summary. */
@@ -245,7 +250,16 @@ int lpa_quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, l
 /* Symmetrised degree of every vertex (dense ids), host output. */
 int lpa_degrees(lpa_graph* g, int32_t* deg_out);
 
+/* lpa_graph_info has grown across header versions (it carries no size field of its
+ * own): lpa_graph_get_info writes the whole struct of THIS header (LPA_ABI_VERSION);
+ * a caller compiled against another header passes its struct size to
+ * lpa_graph_get_info_sized, which writes only the first min(info_size, sizeof)
+ * bytes (the fields are only ever appended).  lpa_abi_version() returns the
+ * library's LPA_ABI_VERSION, so a binding can check the header it was built for. */
+#define LPA_ABI_VERSION 6
+int lpa_abi_version(void);
 int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info);
+int lpa_graph_get_info_sized(const lpa_graph* g, lpa_graph_info* info, int64_t info_size);
 void lpa_graph_destroy(lpa_graph* g);
 const char* lpa_last_error(void);
 

@@ -154,3 +154,32 @@ def settled_hubs(seed=0, V=20000, n_hub=30, n_mover=40):
         hs = rng.choice(hubs, size=4, replace=False)
         src.append(np.full(4, m)), dst.append(hs)
     return V, np.concatenate(src).astype(np.int32), np.concatenate(dst).astype(np.int32)
+
+
+def code_mix(src, dst, V0):
+    """R-MAT edges (V0 vertices) plus structures whose superstep-2 mode is NOT the giant
+    label, so that the giant-code settle of superstep 2 (lpa_iter.hip "Giant codes")
+    leaves rows to its exact fallback paths: five 200-cliques (wave-bin rows, 199 arcs,
+    their own block's label), a 1,100-clique (block-tier hub rows, glist) and a leader
+    l < hub h pair sharing 9,000 two-arc members (rows of 9,000 arcs above the block
+    tiers, ulist2: every member's superstep-1 label is l).  Returns V, src, dst."""
+    es, ed = [src.astype(np.int64)], [dst.astype(np.int64)]
+    nxt = V0
+
+    def clique(n):
+        nonlocal nxt
+        ids = np.arange(nxt, nxt + n, dtype=np.int64)
+        nxt += n
+        iu, ju = np.triu_indices(n, 1)
+        es.append(ids[iu])
+        ed.append(ids[ju])
+
+    for _ in range(5):
+        clique(200)
+    clique(1100)
+    lead, hub = nxt, nxt + 1
+    mem = np.arange(nxt + 2, nxt + 2 + 9000, dtype=np.int64)
+    nxt += 9002
+    es += [np.full(mem.size, hub), np.full(mem.size, lead)]
+    ed += [mem, mem]
+    return nxt, np.concatenate(es).astype(np.int32), np.concatenate(ed).astype(np.int32)

@@ -6,7 +6,7 @@ superstep (SURVEY.md §8(d) workloads; reference call: Graphframes.py:81
   C3  R-MAT scale 24, edgefactor 16 (16.7 M V / 268 M E): supersteps 1..10 from L0,
       plus lpa_run(10) as a user calls it
   C4  R-MAT scale 26, edgefactor 16 (67 M V / 1.07 B E, 2.1 B arcs): one GPU, and as
-      configured -- vertex-partitioned over P = 2 and P = 8 ranks (an in-process
+      configured -- vertex-partitioned over P = 2, 4 and 8 ranks (an in-process
       loopback group on the one GPU: the library's own exchange code, full allgather
       and changed-label deltas, with D2D copies in place of ncclAllGather)
   C5  Chung-Lu gamma 2.1, 40 M V / 1.4 B E (2.8 B arcs, max degree ~1.25 M): one GPU,
@@ -107,6 +107,9 @@ def _partitioned_every_superstep(gfa, cfg, P, what):
         assert all(i["exchanges_full"] >= 1 and i["exchanges_delta"] >= 2 and i["exchanges_giant"] >= 1
                    for i in infos), infos
         assert all(i["exchanges_full"] + i["exchanges_delta"] + i["exchanges_giant"] == MAX_ITER for i in infos)
+        # the converged supersteps replayed each rank's captured tally graph (the path an
+        # RCCL rank runs; a loopback group captures too since round 5)
+        assert all(i["graph_replays"] >= 1 for i in infos), [i["graph_replays"] for i in infos]
         runs = gfa.run_ranks(ranks, lambda r, g: int((g.run(MAX_ITER) != cfg.hist[MAX_ITER - 1]).sum()))
         assert runs == [0] * P, f"{what} P={P} lpa_run(10) mismatches per rank: {runs}"
     finally:
@@ -154,7 +157,7 @@ def test_c4_rmat26_every_superstep(gfa, c4):
     assert bad == [0] * MAX_ITER, f"C4 one GPU: labels differing per superstep {bad}"
 
 
-@pytest.mark.parametrize("P", [2, 8])
+@pytest.mark.parametrize("P", [2, 4, 8])
 def test_c4_rmat26_partitioned_every_superstep(gfa, c4, P):
     """BASELINE C4 as configured: R-MAT-26 vertex-partitioned over P ranks."""
     _partitioned_every_superstep(gfa, c4, P, "C4")

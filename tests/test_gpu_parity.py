@@ -640,13 +640,11 @@ def rmat22(gfa, oracle):
 
 
 @pytest.mark.parametrize("env", [{"LPA_BLOCK_DEG": "0"}, {"LPA_BLOCK_DEG": "8"}, {"LPA_BLOCK_DEG": "64"},
-                                 {"LPA_BLOCK_DEG": "1000"}, {"LPA_BLOCK_DEG": "64", "LPA_LOCALITY": "0"},
-                                 {"LPA_BLOCK_DEG": "64", "LPA_REBUILD_HYBRID": "1"},
-                                 {"LPA_BLOCK_DEG": "64", "LPA_BLOCK_CLASSES": "32"},
-                                 {"LPA_BLOCK_DEG": "512", "LPA_BLOCK_CLASSES": "16"}])
+                                 {"LPA_BLOCK_DEG": "1000"}, {"LPA_BLOCK_DEG": "64", "LPA_LOCALITY": "0"}])
 def test_class_blocked_rebuild_bit_exact(gfa, rmat22, monkeypatch, env):
     """The class-blocked labels-mode al[] rebuild (rows of degree > LPA_BLOCK_DEG in
-    (class, column) order, per-XCD class pieces -- 8, 16 or 32 classes, one phase per 8 --
+    (class, column) order, per-XCD class pieces -- 8 classes at this size, one phase per 8;
+    the multi-phase class counts run at C4 / C5 size, tests/test_gpu_configs.py --
     + the plain stream below; its arc giant bits ORed piecewise): R-MAT-22 (4 M slots, the LDS hot-set rebuild) bit-exact against
     the oracle at supersteps 1..5 -- superstep 1's column runs over the reordered rows,
     the labels-/hybrid-mode rebuild after it, superstep 2's settles from its arc bits."""
@@ -667,6 +665,34 @@ def test_class_blocked_rebuild_bit_exact(gfa, rmat22, monkeypatch, env):
             assert bad == 0, f"{env} superstep {t + 1}: {bad} labels differ"
         g.reset()
         assert np.array_equal(g.run(5), hist[4]), f"{env} lpa_run(5) after reset"
+
+
+@pytest.fixture(scope="module")
+def codemix22(gfa, oracle):
+    from graphs import code_mix
+    s, d = gfa.gen_rmat(22, 16, seed=11)
+    V, sn, dn = code_mix(s.cpu().numpy(), d.cpu().numpy(), 1 << 22)
+    _, hist, _ = oracle.lpa(V, sn, dn, 5, per_iter=True)
+    return V, sn, dn, hist
+
+
+def test_giant_code_refresh_every_superstep(gfa, codemix22):
+    """The giant-code refresh after superstep 1 (R-MAT: G on the hubs, not on half the
+    hot slots) and superstep 2's settle from the 1-byte codes, with every exact fallback
+    populated -- wave-bin rows, block-tier hub rows and > 8192-arc hub rows whose mode is
+    not G (tests/graphs.py code_mix): bit-exact at supersteps 1..5, then lpa_run(5)."""
+    V, sn, dn, hist = codemix22
+    with gfa.Graph(sn, dn, V) as g:
+        for t in range(5):
+            g.step(1)
+            if t == 0:
+                assert g.info()["code_refresh"] == 1, "the giant-code refresh was not taken"
+            bad = int((g.labels() != hist[t]).sum())
+            assert bad == 0, f"superstep {t + 1}: {bad} labels differ"
+        g.reset()
+        assert np.array_equal(g.run(5), hist[4]), "lpa_run(5) after reset"
+        g.reset()
+        assert np.array_equal(g.run(5), hist[4]), "lpa_run(5), second call (replayed graphs)"
 
 
 @pytest.fixture(scope="module")

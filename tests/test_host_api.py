@@ -49,6 +49,10 @@ def test_last_error_and_null_args():
     assert "null handle" in _lib.last_error()
     assert lib.lpa_step(None, 1, None) == _lib.LPA_EINVAL
     assert lib.lpa_graph_get_info(None, None) == _lib.LPA_EINVAL
+    assert lib.lpa_graph_get_info_sized(None, None, 8) == _lib.LPA_EINVAL
+    # the ctypes struct matches this header version's layout
+    hdr = open(os.path.join(ROOT, "include", "lpa.h")).read()
+    assert lib.lpa_abi_version() == int(re.search(r"#define LPA_ABI_VERSION (\d+)", hdr).group(1))
     lib.lpa_graph_destroy(None)   # no-op
 
 

@@ -89,6 +89,44 @@ __global__ __launch_bounds__(1024) void k_hot_nt(const int32_t* __restrict__ col
     for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
   }
 }
+// code gathers (MB_CODES=1): labels as 16- or 8-bit codes (a denser gather footprint),
+// code -> label through a small dictionary (kDict: global, L2-resident), escape code ->
+// the 4-B label; LDS holds the codes of the first kHot slots (the same 160 KB)
+template <typename C, int kHot, bool kDict>
+__global__ __launch_bounds__(1024) void k_hot_code(const int32_t* __restrict__ col, int64_t arcs,
+                                                   const C* __restrict__ code, const int32_t* __restrict__ dict,
+                                                   const int32_t* __restrict__ L, int32_t* __restrict__ al) {
+  __shared__ C hot[kHot];
+  constexpr u32 kEsc = (u32)(C)(~(C)0);
+  for (int i = threadIdx.x; i < kHot; i += 1024) hot[i] = code[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 512; base + 512 <= arcs; base += nw * 512) {
+    int32_t c[8], r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = __builtin_nontemporal_load(col + base + k * 64 + lane);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int32_t x = c[k];
+      r[k] = (int32_t)(u32)(x < kHot ? hot[x] : code[x]);
+    }
+    if (kDict) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = (u32)r[k] == kEsc ? L[c[k]] : dict[r[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(r[k], al + base + k * 64 + lane);
+  }
+}
+__global__ void k_init_codes(uint16_t* c16, uint8_t* c8, int32_t* dict, int64_t V, int esc_pct16, int esc_pct8) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < V; i += (int64_t)gridDim.x * 256) {
+    const uint64_t h = mix(i + 12345);
+    c16[i] = (int)(h % 100) < esc_pct16 ? 0xFFFF : (uint16_t)((h >> 8) % 65535);
+    c8[i] = (int)((h >> 32) % 100) < esc_pct8 ? 0xFF : (uint8_t)((h >> 40) % 255);
+    if (i < 65536) dict[i] = (int32_t)(mix(i) % V);
+  }
+}
 // XCD-split rebuild: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8);
 // XCDs 0-3 gather the arcs whose column is < T (plus the LDS hot set), XCDs 4-7 the
 // rest, so each XCD's L2 caches half of the gathered label range.  Every block streams
@@ -215,6 +253,18 @@ int main(int argc, char** argv) {
       snprintf(nm, 80, "XCD split at %d", T);
       timeit(nm, [&] { hipLaunchKernelGGL(k_hot_xcd, dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, T); });
     }
+    return 0;
+  }
+  if (getenv("MB_CODES")) {
+    uint16_t* c16; uint8_t* c8; int32_t* dict;
+    CK(hipMalloc(&c16, V * 2)); CK(hipMalloc(&c8, V)); CK(hipMalloc(&dict, 65536 * 4));
+    hipLaunchKernelGGL(k_init_codes, dim3(4096), dim3(256), 0, 0, c16, c8, dict, V, 9, 32);
+    CK(hipDeviceSynchronize());
+    timeit("hot LDS 40960 (NT) [shipped]", [&] { hipLaunchKernelGGL((k_hot<40960, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, L, al, 0, BIG); });
+    timeit("u16 codes, LDS 81920, no dict", [&] { hipLaunchKernelGGL((k_hot_code<uint16_t, 81920, false>), dim3(cus), dim3(1024), 0, 0, col, arcs, c16, dict, L, al); });
+    timeit("u16 codes, LDS 81920, dict + 9% esc", [&] { hipLaunchKernelGGL((k_hot_code<uint16_t, 81920, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, c16, dict, L, al); });
+    timeit("u8 codes, LDS 163840, no dict", [&] { hipLaunchKernelGGL((k_hot_code<uint8_t, 163840, false>), dim3(cus), dim3(1024), 0, 0, col, arcs, c8, dict, L, al); });
+    timeit("u8 codes, LDS 163840, dict + 32% esc", [&] { hipLaunchKernelGGL((k_hot_code<uint8_t, 163840, true>), dim3(cus), dim3(1024), 0, 0, col, arcs, c8, dict, L, al); });
     return 0;
   }
   if (basic) {
