@@ -69,8 +69,33 @@ CONFIGS = {
 MAX_ITER = 10
 
 
+def superstep_traffic(kernel, superstep, config_id):
+    """HBM bytes of `kernel`'s launch(es) in superstep `superstep` of a labelPropagation(10)
+    call from the round-5 per-config PMC summary (tools/pmc_r05.sh ->
+    profiles/r05/traffic/pmc_traffic_<config>.json), or (None, None)."""
+    path = os.path.join(ROOT, "profiles", "r05", "traffic", f"pmc_traffic_{config_id}.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        e = t["per_superstep"][kernel][f"superstep_{superstep}"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    return e["traffic_bytes"], os.path.relpath(path, ROOT)
+
+
 def measured_traffic(kernel, config_id):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (C3 only)."""
+    """HBM bytes per launch of `kernel` from the committed PMC summaries: the round-5
+    per-config files for the rebuild kernels (superstep 2's refresh in the timed window,
+    superstep 1's outside it), else the older C3 files."""
+    if kernel == "k_al_rebuild_hot":
+        b, src = superstep_traffic(kernel, 2, config_id)
+        if b is not None:
+            return b, src
+    if kernel == "k_al_rebuild_hot_superstep1":
+        for k in ("k_code_rebuild", "k_al_rebuild_hot"):
+            b, src = superstep_traffic(k, 1, config_id)
+            if b is not None and b > 0.2 * 1e6:
+                return b, src
     if config_id != "C3":
         return None, None
     for path in TRAFFIC_FILES:
@@ -411,6 +436,8 @@ def main():
     for _ in range(3):
         g.reset()
         ss1_rb.append(g.step(1, stats=True)["kernel_ms"]["k_al_rebuild_hot"])
+    # did that refresh take the giant codes (1-B codes per arc instead of a label rebuild)?
+    ss1_code = bool(g.info()["code_refresh"])
     g.set_serial(False)
     g.set_frontier(True)
     kms = {k: sum(st["kernel_ms"][k] for st in per_ss) for k in per_ss[0]["kernel_ms"]}
@@ -473,19 +500,29 @@ def main():
 
     ss1_rb_ms = max_over_ranks(statistics.median(ss1_rb))
     ss1_traffic, ss1_src = measured_traffic("k_al_rebuild_hot_superstep1", config_id)
+    if ss1_code:
+        # the giant-code refresh: col 4 B/arc, a 1-B code per arc of the rows of > 8 arcs,
+        # a 4-B label per arc of the rows of <= 8, each slot's code and label once
+        pcut = sum(list(info["bin_arcs"].values())[:8])
+        ss1_bytes = 4 * info["arcs"] + pcut + 4 * (info["arcs"] - pcut) + 5 * info["V"]
+    else:
+        ss1_bytes = rb_bytes
     ss1_obj = None if ss1_rb_ms <= 0.1 else {
         "bound": "hbm",
-        "kernel": "k_al_rebuild_hot",
-        "achieved": round(rb_bytes / (ss1_rb_ms * 1e-3) / 1e9, 1),
+        "kernel": "k_code_rebuild" if ss1_code else "k_al_rebuild_hot",
+        "achieved": round(ss1_bytes / (ss1_rb_ms * 1e-3) / 1e9, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": round(rb_bytes / (ss1_rb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "frac": round(ss1_bytes / (ss1_rb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "traffic": ss1_traffic,
         "traffic_source": ss1_src,
-        "bytes_per_launch": rb_bytes,
+        "bytes_per_launch": ss1_bytes,
         "avg_launch_ms": round(ss1_rb_ms, 4),
-        "note": "superstep 1's rebuild (labels mode; outside the timed window, inside lpa_run(10)): "
-                "bound by its L2-missing gathers (PMC traffic / algorithmic in traffic), DESIGN.md section 4",
+        "note": ("superstep 1's refresh (outside the timed window, inside lpa_run(10)), the giant-code form: "
+                 "1-B label codes per arc for superstep 2's settle instead of a 4-B label rebuild; bound by "
+                 "its gather lanes (DESIGN.md section 4, Giant codes)") if ss1_code else
+                ("superstep 1's rebuild (labels mode; outside the timed window, inside lpa_run(10)): "
+                 "bound by its L2-missing gathers (PMC traffic / algorithmic in traffic), DESIGN.md section 4"),
     }
 
     out_json = {

@@ -66,6 +66,8 @@ class LpaGraphInfo(ctypes.Structure):
         ("blocked_pieces", ctypes.c_int64),
         ("code_refresh", ctypes.c_int64),
         ("graph_replays", ctypes.c_int64),
+        ("exchanges_posted", ctypes.c_int64),
+        ("exchanges_post_missed", ctypes.c_int64),
     ]
 
     def to_dict(self):
@@ -107,6 +109,7 @@ SIGNATURES = {
     "lpa_set_stream": (ctypes.c_int, [_vp, _vp]),
     "lpa_set_serial": (ctypes.c_int, [_vp, ctypes.c_int32]),
     "lpa_set_frontier": (ctypes.c_int, [_vp, ctypes.c_int32]),
+    "lpa_set_posted": (ctypes.c_int, [_vp, ctypes.c_int64]),
     "lpa_reset": (ctypes.c_int, [_vp]),
     "lpa_step": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(LpaStats)]),
     "lpa_get_labels": (ctypes.c_int, [_vp, _vp, ctypes.c_int32]),

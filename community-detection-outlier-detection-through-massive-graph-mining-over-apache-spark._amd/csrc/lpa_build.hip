@@ -653,9 +653,10 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
   g->code_ok = P == 1 && !g->pooled && !g->no_scatter && g->rebuild_hot && g->vpad >= kHotMinSlots &&
                g->arcs > 0 && (g->n_hub == 0 || g->hub_lane_begin < g->n_hub);
   if (g->code_ok) {
-    for (int b = 0; b < BIN_G64; ++b) g->code_p64 += g->bin_arcs[b];
+    for (int b = 0; b < BIN_G8; ++b) g->code_pcut += g->bin_arcs[b];
     LPA_TRY(dev_alloc(g, (void**)&g->code8, g->vpad));
-    LPA_TRY(dev_alloc(g, (void**)&g->al8, (size_t)((g->code_p64 + 511) / 512 * 512 + 512)));
+    LPA_TRY(dev_alloc(g, (void**)&g->al8, (size_t)((g->code_pcut + 511) / 512 * 512 + 512)));
+    LPA_HIP(hipHostMalloc((void**)&g->h_flag, sizeof(int32_t), hipHostMallocDefault));
   }
   LPA_HIP(hipStreamSynchronize(s));
   // the kept edge list serves the outlier stage (single-GPU handles) and lpa_quality,

@@ -89,6 +89,7 @@ void destroy(lpa_graph* g) {
                   g->blk_pieces, g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword, g->al0, g->abits,
                   g->glist, g->code8, g->al8};
   for (void* p : bufs) dev_free(g, p);
+  if (g->h_flag) (void)hipHostFree(g->h_flag);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : g->bin_ev)
@@ -385,6 +386,15 @@ int lpa_set_serial(lpa_graph* g, int32_t serial) {
   return LPA_OK;
 }
 
+int lpa_set_posted(lpa_graph* g, int64_t cap) {
+  if (!g) {
+    set_error("null handle");
+    return LPA_EINVAL;
+  }
+  g->post_fixed = cap < 0 ? -1 : cap;
+  return LPA_OK;
+}
+
 int lpa_set_frontier(lpa_graph* g, int32_t on) {
   if (!g) {
     set_error("null handle");
@@ -568,6 +578,8 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->blocked_rows = g->blk_pieces ? g->blk_rows : 0;
   info->blocked_pieces = g->blk_pieces ? g->blk_off[g->blk_classes] : 0;
   info->graph_replays = g->n_graph_replays;
+  info->exchanges_posted = g->n_exch_posted;
+  info->exchanges_post_missed = g->n_exch_post_missed;
   if (g->code_ok && g->gword) {
     int32_t w = 0;
     LPA_HIP(hipMemcpyAsync(&w, g->gword + 5, sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));

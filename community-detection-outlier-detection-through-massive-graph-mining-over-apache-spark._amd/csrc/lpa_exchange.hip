@@ -22,6 +22,13 @@
 // the host takes the form of fewest bytes among those that fit (delta and giant entries
 // <= slice / 4 per rank).  All give the identical full label vector, so the mode never
 // affects labels.
+//   posted (round 5) after a delta exchange of few entries the next delta goes out at a
+//          capacity fixed from the last counts (twice the largest, identical on every
+//          rank) BEFORE the host reads the new counts, with its apply and the refresh's
+//          change chunks queued behind it: the GPU works through the host's read instead
+//          of idling.  Kernels that find a count above the capacity stand down on the
+//          device and the host, reading the same counts, exchanges again in the form
+//          that fits.
 //
 // Completing the next-label buffer Ln after a delta exchange.  Ln (the ping-pong
 // partner of the current vector Lc = L_t) still holds L_{t-1} outside the own
@@ -167,9 +174,20 @@ __global__ void k_copy_other(const int4* __restrict__ Lc, int4* __restrict__ Ln,
 
 // apply gathered changes (rank r's entries: drecv[r * cap, r * cap + counts[r])),
 // except those of rank `skip` (its slice of Ln is the tally output already)
+// Posted form (spec != 0): the entries were gathered at a capacity fixed before the
+// counts were known; if any rank's count exceeds it the kernel does nothing (the host,
+// reading the same counts, then runs the exchange again in a form that fits).
+__device__ __forceinline__ bool posted_overflow(const unsigned long long* __restrict__ counts, int32_t P,
+                                                int64_t cap) {
+  bool ovf = false;
+  for (int r = 0; r < P; ++r) ovf |= (int64_t)counts[r] > cap;
+  return ovf;
+}
+
 __global__ void k_delta_apply(const u64* __restrict__ drecv, const unsigned long long* __restrict__ counts,
                               int64_t cap, int32_t P, int32_t skip, int64_t slice,
-                              int32_t* __restrict__ Ln) {
+                              int32_t* __restrict__ Ln, int spec) {
+  if (spec && posted_overflow(counts, P, cap)) return;
   const int64_t tot = cap * P;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot;
        k += (int64_t)gridDim.x * blockDim.x) {
@@ -194,7 +212,9 @@ __global__ __launch_bounds__(256) void k_delta_chunks(const u64* __restrict__ dr
                                                       uint8_t* __restrict__ chflag,
                                                       int32_t* __restrict__ chlist,
                                                       unsigned long long* __restrict__ counters,
-                                                      int32_t own, int32_t* __restrict__ Lsync) {
+                                                      int32_t own, int32_t* __restrict__ Lsync,
+                                                      int spec) {
+  if (spec && posted_overflow(counts, P, cap)) return;
   const int lane = threadIdx.x & 63;
   const int64_t tot = cap * P;
   unsigned long long dirty = 0;
@@ -246,6 +266,7 @@ int exchange_alloc(lpa_graph* g) {
   LPA_TRY(dev_alloc(g, (void**)&g->xpair, sizeof(unsigned long long) * (2 + 2 * P)));
   LPA_TRY(dev_alloc(g, (void**)&g->gcounts, sizeof(unsigned long long) * P));
   LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * 2 * P, hipHostMallocDefault));
+  LPA_HIP(hipEventCreateWithFlags(&g->cnt_ev, hipEventDisableTiming));
   g->dbuf = 0;
   g->prev_delta_ok = false;
   return LPA_OK;
@@ -254,6 +275,8 @@ int exchange_alloc(lpa_graph* g) {
 void exchange_free(lpa_graph* g) {
   if (g->h_dcounts) (void)hipHostFree(g->h_dcounts);
   g->h_dcounts = nullptr;
+  if (g->cnt_ev) (void)hipEventDestroy(g->cnt_ev);
+  g->cnt_ev = nullptr;
 }
 
 u64* exchange_recv_buf(lpa_graph* g) { return g->drecv + (int64_t)g->dbuf * g->dcap * g->nranks; }
@@ -271,8 +294,10 @@ int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
 
 // Ln := L_{t+1} from the gathered changes in the current receive buffer (cap entries
 // per rank) -- see the header; also queues the al[] position chunks of the changes
-// (counters of parity `par`, the superstep's).  Flips the receive buffer.
-int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par) {
+// (counters of parity `par`, the superstep's).  Flips the receive buffer.  posted: the
+// entries were gathered at the fixed capacity `cap` before the counts were read (the
+// kernels stand down on the device if a count exceeds it).
+int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par, bool posted) {
   hipStream_t s = g->stream;
   const int P = g->nranks;
   const int64_t n4 = g->vpad / 4;
@@ -281,7 +306,7 @@ int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t 
     if (g->prev_cap > 0) {
       hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(g->prev_cap * P, 8192)), dim3(256), 0, s,
                          g->drecv + (int64_t)pb * g->dcap * P, g->dcount + 1 + (int64_t)pb * P,
-                         g->prev_cap, P, g->rank, g->slice, Ln);
+                         g->prev_cap, P, g->rank, g->slice, Ln, 0);
       LPA_HIP(hipGetLastError());
     }
   } else {
@@ -291,17 +316,27 @@ int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t 
   }
   if (cap > 0) {
     hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(cap * P, 8192)), dim3(256), 0, s,
-                       exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->rank, g->slice, Ln);
+                       exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->rank, g->slice, Ln, posted);
     LPA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_delta_chunks, dim3(grid_of(cap * P, 4096)), dim3(256), 0, s,
                        exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->slice, g->cptr, g->cch,
-                       g->chflag, g->chlist, g->counters + 4 * par, g->rank, const_cast<int32_t*>(Lc));
+                       g->chflag, g->chlist, g->counters + 4 * par, g->rank, const_cast<int32_t*>(Lc), posted);
     LPA_HIP(hipGetLastError());
   }
   g->prev_cap = cap;
   g->prev_delta_ok = true;
   g->dbuf ^= 1;
   return LPA_OK;
+}
+
+// capacity of the next posted delta: twice the last largest count, at least kPostMin,
+// power of two; none above kPostMax entries per rank (label-dense supersteps exchange
+// the exact count) or beyond the delta buffers
+constexpr int64_t kPostMin = 1024, kPostMax = 1 << 17;
+static int64_t posted_cap(const lpa_graph* g, int64_t capd) {
+  int64_t c = kPostMin;
+  while (c < 2 * capd) c *= 2;
+  return c <= kPostMax && c <= g->dcap ? c : 0;
 }
 
 // In-library exchange of one superstep (P > 1, RCCL communicator or loopback group):
@@ -324,7 +359,39 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
                        exchange_recv_counts(g), g->gcounts);
     LPA_HIP(hipGetLastError());
     LPA_HIP(hipMemcpyAsync(g->h_dcounts, g->xpair + 2, sizeof(unsigned long long) * 2 * P, hipMemcpyDeviceToHost, s));
-    LPA_HIP(hipStreamSynchronize(s));
+    LPA_HIP(hipEventRecord(g->cnt_ev, s));
+    // Posted delta (converged supersteps, after a delta exchange of few entries): the
+    // entries go out at a capacity fixed from the last counts (the same on every rank),
+    // and the apply + the refresh's change chunks are queued behind them BEFORE the host
+    // waits for the counts, so the GPU keeps working through the host's read.  Kernels
+    // that find a count above the capacity do nothing; the host then sees the same
+    // counts and exchanges again below in the form that fits.
+    const int64_t post = !g->prev_delta_ok      ? 0
+                         : g->post_fixed < 0    ? g->post_cap
+                                                : std::min(g->post_fixed, g->dcap);
+    if (post > 0) {
+      LPA_TRY(coll_allgather(g, g->dsend, exchange_recv_buf(g), (size_t)post, 8, s));
+      const int64_t prev_cap = g->prev_cap;
+      const int dbuf = g->dbuf;
+      LPA_TRY(exchange_finish_delta(g, Lc, Ln, post, g->par, true));
+      LPA_HIP(hipEventSynchronize(g->cnt_ev));
+      int64_t capd = 0;
+      for (int k = 0; k < P; ++k) capd = std::max(capd, (int64_t)g->h_dcounts[2 * k]);
+      if (capd <= post) {
+        g->last_exchange_delta = capd;
+        g->post_cap = posted_cap(g, capd);
+        ++g->n_exch_delta;
+        ++g->n_exch_posted;
+        *changes_listed = true;
+        return LPA_OK;
+      }
+      // overflow: the queued kernels stood down; undo the host-side bookkeeping
+      ++g->n_exch_post_missed;
+      g->prev_cap = prev_cap;
+      g->dbuf = dbuf;
+    } else {
+      LPA_HIP(hipEventSynchronize(g->cnt_ev));
+    }
     int64_t capd = 0, capg = 0;
     for (int k = 0; k < P; ++k) {
       capd = std::max(capd, (int64_t)g->h_dcounts[2 * k]);
@@ -337,6 +404,7 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
     if (delta_b <= giant_b && delta_b < full_b) {
       if (capd > 0) LPA_TRY(coll_allgather(g, g->dsend, exchange_recv_buf(g), (size_t)capd, 8, s));
       g->last_exchange_delta = capd;
+      g->post_cap = posted_cap(g, capd);
       ++g->n_exch_delta;
       *changes_listed = true;
       return exchange_finish_delta(g, Lc, Ln, capd, g->par);
@@ -352,7 +420,7 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
       LPA_HIP(hipGetLastError());
       if (capg > 0) {
         hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(capg * P, 8192)), dim3(256), 0, s, ent, g->gcounts, capg,
-                           P, g->rank, S, Ln);
+                           P, g->rank, S, Ln, 0);
         LPA_HIP(hipGetLastError());
       }
       g->last_exchange_delta = -2;

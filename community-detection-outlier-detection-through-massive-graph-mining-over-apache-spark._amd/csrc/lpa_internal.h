@@ -228,11 +228,14 @@ struct lpa_graph {
   // giant codes (round 5, lpa_iter.hip "Giant codes"): the refresh after superstep 1 on
   // a single GPU, when one label G carries the hubs but not half the hot slots (R-MAT),
   // writes a 1-byte code per arc instead of al[] (code 0 = G, else an 8-bit label hash)
-  // for the rows above the row bins, and al[] only for the row bins' positions
+  // for the rows of > 8 arcs, and al[] only for the positions of the rows of <= 8
   bool code_ok = false;         // the handle can take that refresh (P = 1, hot-set rebuild)
   uint8_t* code8 = nullptr;     // [vpad] code of every slot's label
-  uint8_t* al8 = nullptr;       // [code_p64 rounded up + 512] code of every arc's column label
-  int64_t code_p64 = 0;         // first arc position of the row bins (deg <= 64)
+  uint8_t* al8 = nullptr;       // [code_pcut rounded up + 512] code of every arc's column label
+  int64_t code_pcut = 0;        // first arc position of the rows of <= 8 arcs (they keep labels)
+  bool code3 = false;           // superstep 3 follows a giant-code refresh (read by the host
+                                //   before it: its schedule differs, see run_supersteps)
+  int32_t* h_flag = nullptr;    // [1] pinned host word for that read
   unsigned long long* abits = nullptr;  // [arcs / 64] bit i = (al[i] == G): the bits-mode rebuild's by-product
   int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
   uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])
@@ -262,7 +265,7 @@ struct lpa_graph {
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per
-  // (superstep, cur, par)
+  // (superstep, cur, par); [12, 16) superstep 3 after a giant-code refresh
   hipGraphExec_t gexec[16] = {};
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
@@ -285,6 +288,11 @@ struct lpa_graph {
   bool prev_delta_ok = false;                // the other receive buffer holds the previous
                                              //   superstep's delta (L_{t-1} -> L_t)
   int64_t prev_cap = 0;                      // its entries per rank
+  int64_t post_cap = 0;                      // posted delta capacity of the next exchange (0: none)
+  int64_t post_fixed = -1;                   // lpa_set_posted: -1 adaptive (post_cap), 0 off, > 0 fixed
+  int64_t n_exch_posted = 0;                 // delta exchanges that went out before the count read
+  int64_t n_exch_post_missed = 0;            // posted exchanges whose counts exceeded the capacity
+  hipEvent_t cnt_ev = nullptr;               // the count pairs reached h_dcounts
 
   // original edge list kept for the outlier stage (device, dense ids)
   int32_t* e_src = nullptr;
@@ -386,7 +394,8 @@ void exchange_free(lpa_graph* g);
 int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln);
 lpa::u64* exchange_recv_buf(lpa_graph* g);
 unsigned long long* exchange_recv_counts(lpa_graph* g);
-int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par);
+int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par,
+                          bool posted = false);
 int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first, bool* changes_listed);
 int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par);
 

@@ -2662,13 +2662,16 @@ __device__ __forceinline__ void range_pipe(P1 p1, P2 p2, St st, const int32_t* _
   pipe3(nb, pre, fetch, probe, resolve, store);
 }
 
-// al for [pB, arcs) (pB = code_p64 rounded down to a 512-arc batch) and al8 for [0, pA)
-// (pA = code_p64 rounded up, at most the full batches): the batch across code_p64 gets
+// al for [pB, arcs) (pB = code_pcut rounded down to a 512-arc batch) and al8 for [0, pA)
+// (pA = code_pcut rounded up, at most the full batches): the batch across code_pcut gets
 // both; the partial last batch (one wave) writes whichever applies.  One 1024-thread
 // block per CU, 160 KB of LDS: the row bins' labels first, with the 40,960 hottest labels
 // in LDS, then the codes, with the 163,840 hottest slots' CODES in LDS -- the gathers are
 // bound by their lane count, not their bytes (1-B codes from a 16 MB array cost nearly
 // what 4-B labels from 64 MB did), so the wider LDS share is the lever.
+// (The class pieces of the blocked labels-mode rebuild measured mixed for the codes: C5's
+// refresh after superstep 2 36.6 -> 34.2 ms, C4's after superstep 1 11.1 -> 13.1 ms; the
+// codes stream plainly.)
 __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict__ gword,
                                                        const int32_t* __restrict__ col, int64_t arcs,
                                                        const int32_t* __restrict__ Ln, int64_t nslots,
@@ -2701,12 +2704,13 @@ __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict
   const uint8_t* hc = reinterpret_cast<const uint8_t*>(hot);
   for (u32 q = threadIdx.x; q < nc / 4; q += 1024) hot[q] = reinterpret_cast<const uint32_t*>(code8)[q];
   __syncthreads();
-  range_pipe([&](int c) -> u32 { return (u32)hc[(u32)c < nc ? (u32)c : nc - 1u]; },
-             [&](int c, u32 w) -> int32_t {
-               const bool h = (u32)c < nc;
-               const u32 x = code8[h ? 0 : c];
-               return (int32_t)(h ? w : x);
-             },
+  auto cp1 = [&](int c) -> u32 { return (u32)hc[(u32)c < nc ? (u32)c : nc - 1u]; };
+  auto cp2 = [&](int c, u32 w) -> int32_t {
+    const bool h = (u32)c < nc;
+    const u32 x = code8[h ? 0 : c];
+    return (int32_t)(h ? w : x);
+  };
+  range_pipe(cp1, cp2,
              [&](int64_t b, const int32_t (&r)[8]) {
 #pragma unroll
                for (int k = 0; k < 8; ++k) al8[b + k * 64 + lane] = (uint8_t)r[k];
@@ -2728,34 +2732,32 @@ __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict
   }
 }
 
-// Superstep 2, the rows [vbeg, vend) of one wave bin (64 * NC / 2 < deg <= 64 * NC): one
-// wave per row decides G from the row's al8 codes (its G votes above every one of 64
-// code buckets, as giant_decide) -- the label, and a clear dirty flag -- or flags the
-// row (rdirty = 1) for the wave bins' list mode (gword[6] = 0: their "fr_all"; 1 when no
-// code refresh was taken, and then nothing else happens here).  k_lpa_wave's schedule:
-// row bounds by 64-row batches (span_batch), the codes of the next D - 1 rows in flight
-// (branch-free byte loads at clamped positions), the decision of the current one.
+// The code settle of one bin (supersteps 2 and 3 after a giant-code refresh): a row is
+// decided for G from its al8 codes (G's votes above every bucket of a hash of its other
+// codes, as giant_decide) -- its label written, its dirty flag cleared -- or flagged (rdirty
+// = 1) for its bin's list mode.  Bodies take their share of the bin's rows as (bx, nbx): the
+// blocks of one merged launch (k_code_settle) are split over the seven bins by rows.
+//   wave bins (64 < deg <= 1024, NC chunks): one wave per row, 64 code buckets (LDS),
+//     k_lpa_wave's schedule -- row bounds by 64-row batches (span_batch), the codes of the
+//     next D - 1 rows in flight (branch-free byte loads at clamped positions)
+//   row bins G = 64 / 32 / 16 (8 < deg <= G): G lanes per row in 512-lane batches of
+//     RB = 512 / G rows (k_lpa_rows' layout, one row-offset load per batch), G's votes
+//     counted by ballot, the other codes into 16 buckets per row (LDS, as the row bins'
+//     giant test), the next batch's codes in flight.  Rows of <= 8 arcs keep their labels
+//     (the refresh wrote them; 16 buckets decide too few of them).
 template <int NC>
-__global__ __launch_bounds__(256) void k_code_settle_wave(const int64_t* __restrict__ rp,
-                                                          const uint8_t* __restrict__ al8, int64_t vbeg,
-                                                          int64_t vend, int32_t* __restrict__ gword,
-                                                          int32_t* __restrict__ Ln, uint8_t* __restrict__ rdirty) {
+__device__ __forceinline__ void code_settle_wave(const int64_t* __restrict__ rp, const uint8_t* __restrict__ al8,
+                                                 int64_t vbeg, int64_t vend, int32_t G, int32_t* __restrict__ Ln,
+                                                 uint8_t* __restrict__ rdirty, u32* hist, int64_t bx, int64_t nbx) {
   constexpr int D = NC <= 4 ? 4 : 3;
-  __shared__ u32 hist_all[4][64];
-  const bool on = gword[5] != 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) gword[6] = on ? 0 : 1;
-  if (!on) return;  // uniform
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  u32* hist = hist_all[w];
-  hist[lane] = 0u;
-  const int32_t G = gword[0];
   BinRows br;
   br.vbeg = vbeg;
   br.n = vend - vbeg;
   br.list = nullptr;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  int64_t ib = (int64_t)blockIdx.x * 4 + w;
+  const int64_t stride = nbx * 4;
+  int64_t ib = bx * 4 + w;
   if (ib >= br.n) return;
   auto load = [&](u32 (&x)[NC], const RowSpan& r) {
     const int d = span_len(r);
@@ -2804,6 +2806,108 @@ __global__ __launch_bounds__(256) void k_code_settle_wave(const int64_t* __restr
   }
 }
 
+template <int G>
+__device__ __forceinline__ void code_settle_rows(const int64_t* __restrict__ rp, const uint8_t* __restrict__ al8,
+                                                 int64_t vbeg, int64_t vend, int32_t Gl, int32_t* __restrict__ Ln,
+                                                 uint8_t* __restrict__ rdirty, u32* hist, int64_t bx, int64_t nbx) {
+  static_assert(G >= 16 && G <= 64, "16 buckets per row: G >= 16 lanes");
+  constexpr int RB = 512 / G;
+  constexpr int kGB = 16;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gj = lane & (G - 1), gbase = lane & ~(G - 1);
+  const u64 gm = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
+  u32* hg = hist + (lane / G) * kGB;   // 64 / G groups x 16 buckets = the wave's 64 words
+  const int64_t nb = (vend - vbeg + RB - 1) / RB;
+  const int64_t stride = nbx * 4;
+  int64_t bi = bx * 4 + w;
+  if (bi >= nb) return;
+  auto load = [&](u32 (&lab)[kChunks], int64_t r0, int64_t rpl, int64_t rpe) {
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+      const int rl = c * (64 / G) + lane / G;
+      const int64_t b = __shfl(rpl, rl, 64);
+      const int64_t en = __shfl(rpl, rl + 1 < 64 ? rl + 1 : 63, 64);
+      const int64_t e = rl + 1 < RB ? en : rpe;
+      int64_t a = b + gj < e ? b + gj : e - 1;
+      a = a > 0 ? a : 0;
+      const u32 x = (u32)al8[a];
+      lab[c] = (r0 + rl < vend && gj < e - b) ? x : kNone;
+    }
+  };
+  // batch bi's codes in flight while the previous batch is decided (rows_rp_nb clamps a
+  // batch past the bin to valid addresses)
+  int64_t rpl, rpe, rpl1, rpe1;
+  rows_rp_nb<G>(rp, vbeg + bi * RB, vend, lane, rpl, rpe);
+  u32 lab[kChunks], labn[kChunks];
+  load(lab, vbeg + bi * RB, rpl, rpe);
+  rows_rp_nb<G>(rp, vbeg + (bi + stride) * RB, vend, lane, rpl1, rpe1);
+  while (true) {
+    const int64_t bn = bi + stride;
+    load(labn, vbeg + bn * RB, rpl1, rpe1);
+    rows_rp_nb<G>(rp, vbeg + (bn + stride) * RB, vend, lane, rpl1, rpe1);
+    const int64_t r0 = vbeg + bi * RB;
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+      const u32 lb = lab[c];
+      const u32 cg = (u32)__popcll((__ballot(lb == 0u) >> gbase) & gm);
+      if (lb != 0u && lb != kNone) atomicAdd(&hg[lb & (kGB - 1)], 1u);
+      __builtin_amdgcn_wave_barrier();  // no reordering across (LDS ops of a wave complete in order)
+      u32 mx = 0u;
+      if (gj < kGB) {
+        mx = hg[gj];
+        hg[gj] = 0u;
+      }
+      for (int off = G >> 1; off > 0; off >>= 1) mx = max(mx, (u32)lane::lane_xor(mx, off, lane));
+      const int64_t row = r0 + c * (64 / G) + lane / G;
+      if (gj == 0 && row < vend) {
+        const bool settled = cg > mx;
+        if (settled) Ln[row] = Gl;
+        rdirty[row] = settled ? 0 : 1;
+      }
+    }
+    if (bn >= nb) return;
+    bi = bn;
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) lab[c] = labn[c];
+  }
+}
+
+// one launch for the seven settled bins (w16 .. w2, g64 .. g16): block b belongs to the
+// task t with first[t] <= b < first[t + 1]; gword[6] = 0 (the bins' "fr_all" of
+// superstep 2: lists) when a giant-code refresh was taken, 1 otherwise (and nothing else
+// happens then)
+struct CodeTasks {
+  int64_t vbeg[7], vend[7];
+  int32_t first[8];
+};
+__global__ __launch_bounds__(256) void k_code_settle(const int64_t* __restrict__ rp, const uint8_t* __restrict__ al8,
+                                                     CodeTasks ct, int32_t* __restrict__ gword,
+                                                     int32_t* __restrict__ Ln, uint8_t* __restrict__ rdirty) {
+  __shared__ u32 hist_all[4][64];
+  const bool on = gword[5] != 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[6] = on ? 0 : 1;
+  if (!on) return;  // uniform
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  u32* hist = hist_all[w];
+  hist[lane] = 0u;
+  const int32_t G = gword[0];
+  int t = 0;
+  while (t < 6 && (int32_t)blockIdx.x >= ct.first[t + 1]) ++t;
+  const int64_t bx = (int64_t)blockIdx.x - ct.first[t], nbx = ct.first[t + 1] - ct.first[t];
+  const int64_t vb = ct.vbeg[t], ve = ct.vend[t];
+  switch (t) {
+    case 0: code_settle_wave<16>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
+    case 1: code_settle_wave<8>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
+    case 2: code_settle_wave<4>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
+    case 3: code_settle_wave<2>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
+    case 4: code_settle_rows<64>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
+    case 5: code_settle_rows<32>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
+    default: code_settle_rows<16>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
+  }
+}
+
 // al[i] = L[col[i]] over the arcs of the rows the code settle left (the wave bins' lists
 // [b0, b1) of this superstep), one wave per row
 __global__ __launch_bounds__(256) void k_code_partial_rows(const int32_t* __restrict__ gword,
@@ -2828,32 +2932,81 @@ __global__ __launch_bounds__(256) void k_code_partial_rows(const int32_t* __rest
   }
 }
 
-// ... and over the hub rows k_hub_decide left: the block-tier rows of glist (count
-// gdec[2]) and the units of ulist2 (count gdec[0]), one wave per row or unit
+// ... and over the hub rows left undecided: listed rows (superstep 2: k_hub_decide's
+// block-tier glist, count *nr) and listed units (superstep 2: its ulist2; superstep 3:
+// the frontier unit list), one wave per row or unit
 __global__ __launch_bounds__(256) void k_code_partial_hub(const int32_t* __restrict__ gword,
                                                           const int64_t* __restrict__ rp,
                                                           const int32_t* __restrict__ col,
                                                           const int32_t* __restrict__ L, int32_t* __restrict__ al,
-                                                          const int32_t* __restrict__ glist,
-                                                          const int32_t* __restrict__ ulist2,
-                                                          const int32_t* __restrict__ gdec,
+                                                          const int32_t* __restrict__ rlist,
+                                                          const int32_t* __restrict__ nrp,
+                                                          const int32_t* __restrict__ ulst,
+                                                          const int32_t* __restrict__ nup,
                                                           const Segment* __restrict__ segs) {
   if (gword[5] == 0) return;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nr = gdec[2], total = nr + gdec[0];
+  const int64_t nr = nrp ? *nrp : 0, total = nr + *nup;
   for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < total; i += (int64_t)gridDim.x * 4) {
     int64_t b, e;
     if (i < nr) {
-      const int64_t v = glist[i];
+      const int64_t v = rlist[i];
       b = rp[v];
       e = rp[v + 1];
     } else {
-      const Segment sg = segs[ulist2[i - nr]];
+      const Segment sg = segs[ulst[i - nr]];
       b = sg.begin;
       e = b + (sg.len & 1023);
     }
     for (int64_t p = b + lane; p < e; p += 64) al[p] = L[col[p]];
+  }
+}
+
+// Superstep 3 after a giant-code refresh (the refresh after superstep 2; Chung-Lu, where
+// L1 has no giant yet but L2 has one on the hubs): every hub row from its units' G counts
+// and bucket bounds (k_lpa_units_giant<uint8_t>), as k_hub_decide -- settled: the label, no
+// dirty flag on the row or its units; otherwise every unit of the row is flagged (the
+// combine merges a dirty row's every unit) -- one wave per row
+__global__ __launch_bounds__(256) void k_code_settle_hubs(const int64_t* __restrict__ uoff,
+                                                          const uint32_t* __restrict__ ugc,
+                                                          const uint32_t* __restrict__ umx, int64_t n_hub,
+                                                          const int32_t* __restrict__ gword, int32_t* __restrict__ Ln,
+                                                          uint8_t* __restrict__ rdirty, uint8_t* __restrict__ udirty) {
+  if (gword[5] == 0) return;  // uniform
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int32_t G = gword[0];
+  for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < n_hub; h += (int64_t)gridDim.x * 4) {
+    const int64_t u0 = uoff[h], u1 = uoff[h + 1];
+    u64 sg = 0, sm = 0;
+    for (int64_t u = u0 + lane; u < u1; u += 64) {
+      sg += ugc[u];
+      sm += umx[u];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      sg += __shfl_xor(sg, off, 64);
+      sm += __shfl_xor(sm, off, 64);
+    }
+    const bool settled = sg > sm;
+    if (lane == 0) {
+      if (settled) Ln[h] = G;
+      rdirty[h] = settled ? 0 : 1;
+    }
+    const uint8_t f = settled ? 0 : 1;
+    for (int64_t u = u0 + lane; u < u1; u += 64) udirty[u] = f;
+  }
+}
+
+// superstep 3: a code settle ran -> list mode for the hub and wave bins (fr_all = 0), the
+// diff scans every slot (settled rows changed), the row bins keep their ranges (gword[7]
+// = 1, their al[] entries were written); otherwise the row bins follow fr_all
+__global__ void k_code_commit(int32_t* __restrict__ fr_all, int32_t* __restrict__ gword, int32_t* __restrict__ fcnt) {
+  if (threadIdx.x != 0) return;
+  gword[7] = gword[5] ? 1 : *fr_all;
+  if (gword[5]) {
+    *fr_all = 0;
+    fcnt[kFcntSettled] = 1;
   }
 }
 
@@ -3122,9 +3275,42 @@ int launch_first(lpa_graph* g, int32_t* Lown) {
 }
 
 // the refresh after superstep 1 of a single-GPU handle may take the giant codes
-bool code_refresh_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset == 0; }
-// ... and superstep 2 then settles from them
+// (after superstep 1 on R-MAT, after superstep 2 on Chung-Lu: the first label vector
+// whose giant carries the hubs without holding half the hot slots)
+bool code_refresh_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset <= 1; }
+// ... and superstep 2 (block mode) or 3 then settles from them
 bool code_tally_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset == 1; }
+bool code_tally3_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset == 2 && g->code3; }
+
+// the code settle of the seven settled bins in one launch (k_code_settle; it returns at
+// once unless a giant-code refresh was taken): blocks split over the bins by rows, the
+// row bins' share counted in 512-lane batches
+int launch_code_settle(lpa_graph* g, hipStream_t st, int32_t* Lown) {
+  const int64_t* bb = g->bin_begin;
+  const int bins[7] = {BIN_W16, BIN_W8, BIN_W4, BIN_W2, BIN_G64, BIN_G32, BIN_G16};
+  const int lanes[7] = {64, 64, 64, 64, 64, 32, 16};   // lanes per row
+  CodeTasks ct;
+  int64_t work[7], tot = 0;
+  for (int t = 0; t < 7; ++t) {
+    ct.vbeg[t] = bb[bins[t]];
+    ct.vend[t] = bb[bins[t] + 1];
+    work[t] = (ct.vend[t] - ct.vbeg[t]) * lanes[t];
+    tot += work[t];
+  }
+  const int64_t kBlocks = 4096;   // 16 waves per CU
+  ct.first[0] = 0;
+  for (int t = 0; t < 7; ++t) {
+    int64_t nb = tot > 0 ? (work[t] * kBlocks + tot - 1) / tot : 0;
+    const int64_t need = (work[t] + 255) / 256;   // no more blocks than 256 lanes of rows
+    if (nb > need) nb = need;
+    if (work[t] > 0 && nb < 1) nb = 1;
+    ct.first[t + 1] = ct.first[t] + (int32_t)nb;
+  }
+  hipLaunchKernelGGL(k_code_settle, dim3((unsigned)(ct.first[7] > 0 ? ct.first[7] : 1)), dim3(256), 0, st, g->rp,
+                     g->al8, ct, g->gword, Lown, g->rdirty[g->par]);
+  LPA_HIP(hipGetLastError());
+  return LPA_OK;
+}
 
 int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc,
                  const int32_t* Ln, bool diff) {
@@ -3182,7 +3368,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     // superstep 3: rows settled from the arc giant bits of superstep 2's rebuild (each
     // kernel returns at once unless they are valid): the others' dirty flags, then the
     // lists of this superstep are built from them in list mode
-    if (g->since_reset == 2 && g->abits && !block_mode_now(g)) {
+    if (g->since_reset == 2 && g->abits && !block_mode_now(g) && !code_tally3_now(g)) {
       if (g->n_hub > 0) {
         hipLaunchKernelGGL(k_settle_big, dim3(cap_grid((g->n_hub + 3) / 4, 2048)), dim3(256), 0, s, g->rp,
                            g->abits, g->n_hub, fr_all, g->gword, Lown, g->rdirty[g->par], g->udirty[g->par],
@@ -3198,40 +3384,64 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
       hipLaunchKernelGGL(k_settle_commit, dim3(1), dim3(1), 0, s, const_cast<int32_t*>(fr_all), g->gword, fcnt);
       LPA_HIP(hipGetLastError());
     }
+    if (code_tally3_now(g)) {
+      // superstep 3 after a giant-code refresh (each kernel returns at once otherwise):
+      // hub rows from their units' code counts, wave-bin rows from their codes; the rest
+      // listed (k_code_commit: list mode), their al[] entries gathered after the lists
+      if (g->n_segs > 0) {
+        hipLaunchKernelGGL(k_lpa_units_giant<uint8_t>, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
+                           g->al8, g->segs, g->n_segs, g->gword, g->ugc, g->umx, g->gdec);
+        LPA_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_code_settle_hubs, dim3(cap_grid((g->n_hub + 3) / 4, 2048)), dim3(256), 0, s,
+                           g->hub_uoff, g->ugc, g->umx, g->n_hub, g->gword, Lown, g->rdirty[g->par],
+                           g->udirty[g->par]);
+        LPA_HIP(hipGetLastError());
+      }
+      LPA_TRY(launch_code_settle(g, s, Lown));
+      hipLaunchKernelGGL(k_code_commit, dim3(1), dim3(64), 0, s, const_cast<int32_t*>(fr_all), g->gword, fcnt);
+      LPA_HIP(hipGetLastError());
+    }
     // frontier lists of this superstep (no-op when every row is tallied)
     LPA_TRY(launch_frontier_lists(g));
-    if (code_tally_now(g)) {
-      // superstep 2 after a giant-code refresh (each kernel returns at once otherwise,
-      // leaving the wave bins in range mode): the wave-bin rows settled from their codes,
-      // the others listed, their al[] entries gathered
-#define LPA_CODE_SETTLE(BIN, NC)                                                                         \
-  {                                                                                                      \
-    const int64_t n = bb[BIN + 1] - bb[BIN];                                                              \
-    hipLaunchKernelGGL(k_code_settle_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, s, g->rp,  \
-                       g->al8, bb[BIN], bb[BIN + 1], g->gword, Lown, g->rdirty[g->par]);                   \
-    LPA_HIP(hipGetLastError());                                                                          \
-  }
-      // (every launch sets gword[6], also over an empty bin: the wave bins' flag)
-      LPA_CODE_SETTLE(BIN_W16, 16)
-      LPA_CODE_SETTLE(BIN_W8, 8)
-      LPA_CODE_SETTLE(BIN_W4, 4)
-      LPA_CODE_SETTLE(BIN_W2, 2)
-#undef LPA_CODE_SETTLE
-      LPA_TRY(launch_frontier_lists(g, s, g->gword + 6));
+    if (code_tally3_now(g)) {
       BinBounds bnd;
       for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = bb[b];
       hipLaunchKernelGGL(k_code_partial_rows, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
-                         g->flist, fcnt, bnd, (int)BIN_W16, (int)BIN_G64);
+                         g->flist, fcnt, bnd, (int)BIN_W16, (int)BIN_G8);
+      LPA_HIP(hipGetLastError());
+      hipLaunchKernelGGL(k_code_partial_hub, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
+                         (const int32_t*)nullptr, (const int32_t*)nullptr, g->ulist, fcnt + kFcntUnits, g->segs);
       LPA_HIP(hipGetLastError());
     }
   }
-  // the wave bins' "fr_all": superstep 2 after a giant-code refresh walks the lists above
+  // the wave bins' "fr_all": superstep 2 after a giant-code refresh walks the lists above;
+  // the row bins': superstep 3's code commit keeps them in range mode (gword[7])
   const int32_t* fr_wave = code_tally_now(g) ? g->gword + 6 : fr_bins;
+  // the row bins of > 8 arcs settle from codes as the wave bins (superstep 2: gword[6];
+  // superstep 3: fr_all, 0 after k_code_commit); those of <= 8 arcs keep their ranges
+  const int32_t* fr_rows_hi = fr_wave;
+  const int32_t* fr_rows = code_tally3_now(g) ? g->gword + 7 : fr_bins;
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (sb != s) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
     LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
     if (sc != sb) LPA_HIP(hipStreamWaitEvent(sc, g->ev_fork, 0));
+  }
+  if (code_tally_now(g)) {
+    // superstep 2 after a giant-code refresh (each kernel returns at once otherwise,
+    // leaving the wave bins in range mode): the wave-bin rows settled from their codes,
+    // the others listed, their al[] entries gathered -- on the wave bins' stream, which
+    // then tallies them (w2 included), beside the hub path on main and the row bins on
+    // the third stream (they read neither the flags nor those al[] entries)
+    LPA_TRY(launch_code_settle(g, sb, Lown));
+    LPA_TRY(launch_frontier_lists(g, sb, g->gword + 6));
+    BinBounds bnd;
+    for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = bb[b];
+    hipLaunchKernelGGL(k_code_partial_rows, dim3(2048), dim3(256), 0, sb, g->gword, g->rp, g->col, Lc, g->al,
+                       g->flist, fcnt, bnd, (int)BIN_W16, (int)BIN_G8);
+    LPA_HIP(hipGetLastError());
+    // the row bins of > 8 arcs (third stream) walk these lists too: they wait for them
+    if (sc != sb) LPA_HIP(hipEventRecord(g->ev_join2[2], sb));
   }
 
   auto mark = [&](int i, hipStream_t st) -> int {
@@ -3314,7 +3524,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(launch_hub_decide(g, Lown, g->n_hub, gsel));
     if (code_tally_now(g)) {  // the undecided hub rows' al[] entries (code refresh only)
       hipLaunchKernelGGL(k_code_partial_hub, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
-                         g->glist, g->ulist2, g->gdec, g->segs);
+                         g->glist, g->gdec + 2, g->ulist2, g->gdec, g->segs);
       LPA_HIP(hipGetLastError());
     }
     // the wide tier's few undecided rows right here on the main stream (the fourth
@@ -3353,7 +3563,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(mark(2 * (BIN + 1), ST));                                                        \
     if (n > 0) {                                                                             \
       hipLaunchKernelGGL(k_lpa_group<G>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
-                         ST, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_bins); \
+                         ST, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_rows); \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                    \
@@ -3378,14 +3588,27 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_wave)
-  LPA_WAVE_LAUNCH(BIN_W2, 2, sc, fr_wave)
-  LPA_ROWS_LAUNCH(BIN_G64, 64, fr_bins, sc)
-  LPA_ROWS_LAUNCH(BIN_G32, 32, fr_bins, sc)
-  LPA_ROWS_LAUNCH(BIN_G16, 16, fr_bins, st_tail)
-  LPA_ROWS_LAUNCH(BIN_G8, 8, fr_bins, st_tail)
-  LPA_GROUP_LAUNCH(BIN_G4, 4, st_tail)
-  LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)
-  LPA_GROUP_LAUNCH(BIN_G1, 1, st_tail)
+  LPA_WAVE_LAUNCH(BIN_W2, 2, code_tally_now(g) ? sb : sc, fr_wave)
+  if (code_tally_now(g)) {
+    // superstep 2 after a giant-code refresh: the bins of <= 8 arcs first (their ranges,
+    // labels written by the refresh), then, behind the code settle, the listed rows above
+    LPA_ROWS_LAUNCH(BIN_G8, 8, fr_rows, st_tail)
+    LPA_GROUP_LAUNCH(BIN_G4, 4, st_tail)
+    LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)
+    LPA_GROUP_LAUNCH(BIN_G1, 1, st_tail)
+    if (sc != sb) LPA_HIP(hipStreamWaitEvent(sc, g->ev_join2[2], 0));
+    LPA_ROWS_LAUNCH(BIN_G64, 64, fr_rows_hi, sc)
+    LPA_ROWS_LAUNCH(BIN_G32, 32, fr_rows_hi, sc)
+    LPA_ROWS_LAUNCH(BIN_G16, 16, fr_rows_hi, st_tail)
+  } else {
+    LPA_ROWS_LAUNCH(BIN_G64, 64, fr_rows_hi, sc)
+    LPA_ROWS_LAUNCH(BIN_G32, 32, fr_rows_hi, sc)
+    LPA_ROWS_LAUNCH(BIN_G16, 16, fr_rows_hi, st_tail)
+    LPA_ROWS_LAUNCH(BIN_G8, 8, fr_rows, st_tail)
+    LPA_GROUP_LAUNCH(BIN_G4, 4, st_tail)
+    LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)
+    LPA_GROUP_LAUNCH(BIN_G1, 1, st_tail)
+  }
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
@@ -3406,9 +3629,11 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     // inside the concurrent tally: no Lc sync here, the scatter refresh does it; the
     // label-dense supersteps only count the changed slots (launch_refresh decides)
     const int dm = dense_refresh(g) ? 1 : 0;
-    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_W2], false, g->par, BIN_W16, BIN_W2, dm));
+    // (the split between the two bin streams follows where w2 ran)
+    const int bw = code_tally_now(g) ? BIN_G64 : BIN_W2;
+    LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[bw], false, g->par, BIN_W16, bw, dm));
     // isolated slots (and the padding) never change: the diff stops at the isolated bin
-    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[BIN_W2], bb[BIN_ISO], false, g->par, BIN_W2, BIN_ISO, dm));
+    LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[bw], bb[BIN_ISO], false, g->par, bw, BIN_ISO, dm));
     LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par, BIN_SEG, BIN_W16, dm));
   }
   if (sb != s) {
@@ -3506,7 +3731,7 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
                          (const int4*)L, g->vpad / 4, g->gword, (uint32_t*)g->code8);
       LPA_HIP(hipGetLastError());
       hipLaunchKernelGGL(k_code_rebuild, dim3(dev_cus), dim3(1024), 0, s, g->gword, g->col, g->arcs, L,
-                         g->vpad, g->code8, g->code_p64, g->al8, g->al);
+                         g->vpad, g->code8, g->code_pcut, g->al8, g->al);
     }
   } else {
     const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
@@ -3576,6 +3801,12 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   fm.n_hub = g->n_hub;
   fm.rdirty = g->rdirty[par ^ 1];
   fm.udirty = g->udirty[par ^ 1];
+  if (code_tally3_now(g)) {
+    // superstep 3 after a giant-code refresh: its settled rows' al[] entries were never
+    // written, so this refresh rebuilds (k_dense_decide's code clause; n_slots: no count)
+    hipLaunchKernelGGL(k_dense_decide, dim3(1), dim3(64), 0, s, ctr, INT64_MAX, g->gword);
+    LPA_HIP(hipGetLastError());
+  }
   if (g->al_pending) {  // the column-run superstep after a lazy reset (al holds nothing)
     hipLaunchKernelGGL(k_al_fill_unless_rebuild, dim3(cap_grid((g->arcs / 4 + 255) / 256, 8192)), dim3(256), 0, s,
                        ctr, thr, (const v4i*)g->al0, (v4i*)g->al, g->arcs);
@@ -3658,6 +3889,14 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t], s));
     // superstep 1 from L0: column runs, no hash tallies (its diff runs in the refresh)
     const bool first = first_runs_now(g);
+    // before superstep 3 on a code-capable handle: did the refresh after superstep 2 take
+    // the giant codes?  One host read (~20 us of idle GPU) instead of ~10 kernels that
+    // return at once in the other case (C3: ~0.1 ms of superstep 3's 0.47)
+    if (g->code_ok && !exchanges(g) && g->since_reset == 2) {
+      LPA_HIP(hipMemcpyAsync(g->h_flag, g->gword + 5, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      LPA_HIP(hipStreamSynchronize(s));
+      g->code3 = *g->h_flag != 0;
+    }
     if (!first) LPA_TRY(ensure_al(g));  // a lazy reset's al is needed by the hash tallies
     const bool diff_in_tally = !exchanges(g) && !g->serial && !first;
     // converged supersteps on one GPU replay a captured HIP graph of the whole
@@ -3707,7 +3946,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
       // supersteps 2 and 3 on one GPU: a captured graph per (superstep, cur, par) too --
       // each has its own fixed schedule (giant decision, row settle), and their ~40-50
       // launches become one graph launch (C2: supersteps 2-3 0.46 / 0.50 -> 0.41 / 0.45 ms)
-      const int key = 4 + ((g->since_reset - 1) * 2 + g->cur) * 2 + g->par;
+      // (superstep 3 after a giant-code refresh has its own schedule: keys 12..15)
+      const int key = code_tally3_now(g) ? 12 + g->cur * 2 + g->par
+                                         : 4 + ((g->since_reset - 1) * 2 + g->cur) * 2 + g->par;
       if (!g->gexec[key])
         LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
           int rc = launch_tally(g, Lown, nullptr, Lc, Ln, true);

@@ -153,6 +153,10 @@ class Graph:
         """Re-tally only rows with a changed neighbour (exact; default on) or every row."""
         _lib.check(self._lib.lpa_set_frontier(self._handle(), int(bool(on))))
 
+    def set_posted(self, cap: int = -1):
+        """P > 1: posted delta exchange capacity (-1 adaptive, 0 off, > 0 fixed; labels identical)."""
+        _lib.check(self._lib.lpa_set_posted(self._handle(), int(cap)))
+
     def set_serial(self, serial: bool = True):
         """Profiling: queue every tally kernel on one stream (standalone kernel times)."""
         _lib.check(self._lib.lpa_set_serial(self._handle(), int(bool(serial))))

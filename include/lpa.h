@@ -88,6 +88,10 @@ typedef struct lpa_graph_info {
                               after a superstep-1 step; 0 otherwise (since ABI 6)      */
   int64_t graph_replays;   /* supersteps run by replaying a captured HIP graph (the
                               converged ones, P = 1 also supersteps 2-3; since ABI 6)  */
+  int64_t exchanges_posted; /* P > 1: delta exchanges sent at a capacity fixed before the
+                              count read, so the GPU works through it (since ABI 6)   */
+  int64_t exchanges_post_missed; /* ... posted ones whose counts exceeded the posted
+                              capacity: exchanged again in the form that fits          */
 } lpa_graph_info;
 
 /* Outlier summary. */
@@ -183,6 +187,15 @@ int lpa_set_serial(lpa_graph* g, int32_t serial);
  * same mode (GraphX Pregel's active-set idea applied to LPA).  Off: every row is
  * tallied every superstep.  Labels are identical either way. */
 int lpa_set_frontier(lpa_graph* g, int32_t on);
+/* P > 1 with a communicator or loopback group: capacity of the posted delta exchange
+ * (converged supersteps after a delta exchange: the changed-label entries go out at a
+ * capacity fixed before the per-rank counts are read, so the GPU works through the
+ * host's read; a count above it makes the queued apply stand down and the host exchange
+ * again in the form that fits).  cap < 0: adaptive (default: twice the last largest
+ * count, 1024..131072 entries); 0: off (the host reads the counts first); > 0: that
+ * fixed capacity (testing: 1 exercises the stand-down path).  Labels are identical
+ * either way.  Since ABI 6. */
+int lpa_set_posted(lpa_graph* g, int64_t cap);
 /* Run on a caller-provided hipStream_t (NULL = the handle's own stream). */
 int lpa_set_stream(lpa_graph* g, void* hip_stream);
 

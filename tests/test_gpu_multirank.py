@@ -92,6 +92,43 @@ def test_loopback_degree_mix_every_superstep(gfa, oracle, P):
         _close(lb, ranks)
 
 
+@pytest.mark.parametrize("P", [2, 4])
+def test_loopback_posted_delta_settings(gfa, oracle, P):
+    """The posted delta exchange (lpa_set_posted; converged supersteps send the changed
+    labels at a capacity fixed before the host reads the counts): adaptive (default),
+    off, a capacity of 1 (nearly every posted exchange overflows: the queued apply
+    stands down on the device and the host exchanges again) and a fixed large one --
+    every superstep bit-exact on every rank."""
+    s, d = gfa.gen_rmat(18, 16, seed=2)
+    V = 1 << 18
+    s, d = s.cpu().numpy(), d.cpu().numpy()
+    _, hist, _ = oracle.lpa(V, s, d, 10, per_iter=True)
+    lb, ranks = _group(gfa, s, d, V, P)
+    try:
+        for cap in (-1, 0, 1, 1 << 20):
+            before = [g.info() for g in ranks]
+            for g in ranks:
+                g.set_posted(cap)
+                g.reset()
+            got = _per_step_all_ranks(gfa, ranks, 10)
+            for r in range(P):
+                for t in range(10):
+                    bad = int((got[r][t] != hist[t]).sum())
+                    assert bad == 0, f"posted={cap} P={P} rank {r} superstep {t + 1}: {bad} labels differ"
+            after = [g.info() for g in ranks]
+            posted = [a["exchanges_posted"] - b["exchanges_posted"] for a, b in zip(after, before)]
+            missed = [a["exchanges_post_missed"] - b["exchanges_post_missed"] for a, b in zip(after, before)]
+            assert len(set(posted)) == 1 and len(set(missed)) == 1, (cap, posted, missed)  # same on every rank
+            if cap == 0:
+                assert posted[0] == 0 and missed[0] == 0
+            elif cap == 1:
+                assert missed[0] >= 1, (posted, missed)
+            else:
+                assert posted[0] >= 1, (cap, posted, missed)
+    finally:
+        _close(lb, ranks)
+
+
 def test_loopback_abort_releases_waiting_rank(gfa):
     """A rank whose peer never arrives is released by lpa_loopback_abort and fails
     with an error instead of blocking its thread."""

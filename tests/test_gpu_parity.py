@@ -721,6 +721,26 @@ def test_hot_rebuild_partial_batch(gfa, chunglu5m, monkeypatch, env):
             assert bad == 0, f"{env} superstep {t + 1}: {bad} labels differ"
 
 
+def test_giant_code_refresh_after_superstep_2(gfa, chunglu5m):
+    """Chung-Lu (5 M / 20 M, max degree ~200 K): the giant-code refresh is taken after
+    superstep 2 (G on the hubs, on 43 % of the hot slots) and superstep 3 settles hub and
+    wave rows from the codes, lists the rest (k_code_commit) and rebuilds al[] after it;
+    the refresh after superstep 1 takes it too on this graph (G on half the top hubs).
+    Bit-exact at supersteps 1..5, the arc count not a multiple of 512 (the code
+    rebuild's partial last batch)."""
+    V, sn, dn, hist = chunglu5m
+    with gfa.Graph(sn, dn, V) as g:
+        taken = []
+        for t in range(5):
+            g.step(1)
+            taken.append(g.info()["code_refresh"])
+            bad = int((g.labels() != hist[t]).sum())
+            assert bad == 0, f"superstep {t + 1}: {bad} labels differ"
+        assert taken[1] == 1, taken   # the refresh after superstep 2
+        g.reset()
+        assert np.array_equal(g.run(5), hist[4]), "lpa_run(5) after reset"
+
+
 def test_sbm_hot_path_every_superstep(gfa, oracle):
     """A family with no giant label (planted partition, 400 blocks) at the LDS hot-set
     rebuild's size (4 M slots): every superstep's giant pick finds no dominant label, so
