@@ -654,8 +654,8 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
                g->arcs > 0 && (g->n_hub == 0 || g->hub_lane_begin < g->n_hub);
   if (g->code_ok) {
     for (int b = 0; b < BIN_G8; ++b) g->code_pcut += g->bin_arcs[b];
-    LPA_TRY(dev_alloc(g, (void**)&g->code8, g->vpad));
-    LPA_TRY(dev_alloc(g, (void**)&g->al8, (size_t)((g->code_pcut + 511) / 512 * 512 + 512)));
+    LPA_TRY(dev_alloc(g, (void**)&g->code2, sizeof(uint32_t) * (size_t)(g->vpad / 16)));
+    LPA_TRY(dev_alloc(g, (void**)&g->al2, sizeof(uint32_t) * (size_t)(((g->code_pcut + 511) / 512 * 512 + 512) / 16)));
     LPA_HIP(hipHostMalloc((void**)&g->h_flag, sizeof(int32_t), hipHostMallocDefault));
   }
   LPA_HIP(hipStreamSynchronize(s));

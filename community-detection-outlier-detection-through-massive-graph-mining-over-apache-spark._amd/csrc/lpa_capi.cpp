@@ -81,13 +81,13 @@ void destroy(lpa_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   void* bufs[] = {g->rp,   g->col,   g->new_of, g->old_of, g->deg,   g->lab[0], g->lab[1],
-                  g->segs, g->e_src,  g->e_dst, g->gsend, g->gbm, g->xpair, g->gcounts, g->dsend, g->drecv, g->dcount, g->de_keys, g->de_t, g->de_ts, g->de_out_off, g->de_in_off, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
+                  g->segs, g->e_src,  g->e_dst, g->gsend, g->gbm, g->xpair, g->dsend, g->drecv, g->dcount, g->de_keys, g->de_t, g->de_ts, g->de_out_off, g->de_in_off, g->al,   g->cptr,  g->cpos,   g->cch, g->cowner, g->chflag, g->chlist,
                   g->counters, g->hub_best, g->hub_wcount, g->stage, g->scat, g->dev_err,
                   g->hub_hoff, g->ghist, g->gcur, g->hub_lists, g->hub_lcnt, g->hub_tickets, g->items_cb,
                   g->items_cc, g->hub_uoff, g->ucnt, g->crow, g->rdirty[0], g->rdirty[1],
                   g->udirty[0], g->udirty[1], g->fr_all, g->flist, g->ulist, g->fcnt, g->first_best, g->rstart,
                   g->blk_pieces, g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword, g->al0, g->abits,
-                  g->glist, g->code8, g->al8};
+                  g->glist, g->code2, g->al2};
   for (void* p : bufs) dev_free(g, p);
   if (g->h_flag) (void)hipHostFree(g->h_flag);
   for (auto& e : g->ev)
@@ -371,7 +371,7 @@ int lpa_exchange_put_delta(lpa_graph* g, const uint64_t* entries, const int64_t*
   LPA_HIP(hipMemsetAsync(g->counters + 4 * pp, 0, sizeof(unsigned long long) * 2, s));
   const int32_t* Lc = g->lab[g->cur ^ 1];
   int32_t* Ln = g->lab[g->cur];
-  LPA_TRY(exchange_finish_delta(g, Lc, Ln, cap, pp));
+  LPA_TRY(exchange_finish_delta(g, const_cast<int32_t*>(Lc), Ln, cap, pp, exchange_recv_counts(g), 1));
   LPA_TRY(launch_refresh_ext(g, Lc, Ln, true, pp));
   LPA_HIP(hipStreamSynchronize(s));
   return LPA_OK;

@@ -31,12 +31,12 @@
 //          that fits.
 //
 // Completing the next-label buffer Ln after a delta exchange.  Ln (the ping-pong
-// partner of the current vector Lc = L_t) still holds L_{t-1} outside the own
-// slice.  If the previous superstep also exchanged deltas (E_t: L_{t-1} -> L_t),
-// applying E_t and then the new E_{t+1} gives L_{t+1} without touching the rest of
-// the vector; otherwise the other slices are first copied from Lc.  The gathered
-// E_{t+1} is also the list of changed vertices, so the al[] refresh takes its
-// position chunks from it instead of diffing the whole vector.
+// partner of the current vector Lc = L_t) holds, outside the own slice, L_t if the
+// previous exchange was a delta too (k_delta_finish writes every entry into both
+// buffers, so they agree afterwards), else L_{t-1} and the other slices are first
+// copied from Lc.  Applying the gathered E_{t+1} then gives L_{t+1}; E_{t+1} is also the
+// list of changed vertices, so the al[] refresh takes its position chunks from it
+// instead of diffing the whole vector.
 #include <algorithm>
 #include <climits>
 
@@ -84,63 +84,101 @@ __global__ __launch_bounds__(256) void k_delta_compact(const int32_t* __restrict
 
 // this rank's changed owned slots -> dsend (slot << 32 | label), count xpair[0]; the
 // changed ones whose new label is not G -> gsend, count xpair[1]; bit i of the slice's
-// bitmap = (new label == G).  One pass, block-aggregated counts (one atomic per block
-// and list).  The slice is a multiple of 64 slots: a wave owns whole bitmap words.
+// bitmap = (new label == G).  One streaming pass: a wave takes kCompactWords bitmap
+// words (64 slots each, one coalesced 256-B load per buffer and word, all issued before
+// the first compare), a ballot per word; only a wave with changes reserves its entries
+// (one atomic per list).  The slice is a multiple of 64 slots.  Entry order differs
+// from run to run; every consumer applies them as a set (distinct slots).
+// Converged supersteps (flist given): when the tally walked its frontier lists (*fr_all
+// == 0, no settle), only the listed rows can have changed -- every other owned row's
+// output slot already holds its label -- so the pass walks the lists instead of the
+// slice; it writes no bitmap then and marks the giant form unavailable (a giant count
+// above any capacity in xpair[1]).
+constexpr int kCompactWords = 8;
+constexpr unsigned long long kNoGiantForm = 1ull << 62;
+struct ListBounds {
+  int64_t b[LPA_NBINS + 1];
+};
 __global__ __launch_bounds__(256) void k_exch_compact(const int32_t* __restrict__ Lc_own,
                                                       const int32_t* __restrict__ Ln_own, int64_t slice,
                                                       const int32_t* __restrict__ gword,
                                                       u64* __restrict__ dsend, u64* __restrict__ gsend,
                                                       unsigned long long* __restrict__ xpair,
-                                                      unsigned long long* __restrict__ bm_own) {
-  __shared__ int wsum[2][4];
-  __shared__ unsigned long long base_s[2];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int32_t G = gword[0];
-  for (int64_t i0 = (int64_t)blockIdx.x * 256; i0 < slice; i0 += (int64_t)gridDim.x * 256) {
-    const int64_t i = i0 + threadIdx.x;
-    int32_t nv = 0;
-    bool chg = false, isg = false;
-    if (i < slice) {
-      nv = Ln_own[i];
-      chg = nv != Lc_own[i];
-      isg = nv == G;
+                                                      unsigned long long* __restrict__ bm_own,
+                                                      const int32_t* __restrict__ flist,
+                                                      const int32_t* __restrict__ fcnt,
+                                                      const int32_t* __restrict__ fr_all, ListBounds lb) {
+  const int lane = threadIdx.x & 63;
+  const u64 lt = (1ull << lane) - 1ull;
+  if (flist != nullptr && *fr_all == 0 && fcnt[kFcntSettled] == 0) {   // uniform
+    if (blockIdx.x == 0 && threadIdx.x == 0) xpair[1] = kNoGiantForm;
+    int64_t total = 0;
+    for (int b = 0; b < BIN_ISO; ++b) total += fcnt[b];
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); i0 < total; i0 += (int64_t)gridDim.x * 256) {
+      const int64_t i = i0 + lane;
+      bool chg = false;
+      int64_t v = 0;
+      int32_t nv = 0;
+      if (i < total) {
+        int64_t acc = 0;
+        int b = 0;
+        while (i >= acc + fcnt[b]) acc += fcnt[b++];
+        v = flist[lb.b[b] + (i - acc)];
+        nv = Ln_own[v];
+        chg = nv != Lc_own[v];
+      }
+      const u64 m = __ballot(chg);
+      if (m == 0) continue;   // wave-uniform
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(&xpair[0], (unsigned long long)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (chg) dsend[base + __popcll(m & lt)] = ((u64)(uint32_t)v << 32) | (u64)(uint32_t)nv;
     }
-    const bool ng = chg && !isg;
-    const u64 m = __ballot(chg), mg = __ballot(ng), mb = __ballot(isg);
-    if (lane == 0) {
-      wsum[0][w] = __popcll(m);
-      wsum[1][w] = __popcll(mg);
-      if (i < slice) bm_own[i >> 6] = mb;
-    }
-    __syncthreads();
-    int before = 0, tot = 0, gbefore = 0, gtot = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (k < w) before += wsum[0][k], gbefore += wsum[1][k];
-      tot += wsum[0][k];
-      gtot += wsum[1][k];
-    }
-    if (threadIdx.x == 0) {
-      if (tot) base_s[0] = atomicAdd(&xpair[0], (unsigned long long)tot);
-      if (gtot) base_s[1] = atomicAdd(&xpair[1], (unsigned long long)gtot);
-    }
-    __syncthreads();
-    const u64 e = ((u64)(uint32_t)i << 32) | (u64)(uint32_t)nv;
-    const u64 lt = (1ull << lane) - 1ull;
-    if (chg) dsend[base_s[0] + before + __popcll(m & lt)] = e;
-    if (ng) gsend[base_s[1] + gbefore + __popcll(mg & lt)] = e;
-    __syncthreads();  // wsum / base_s reused by the next tile
+    return;
   }
-}
-
-// the gathered (delta, giant) count pairs -> the delta protocol's per-rank counts (its
-// receive buffer) and the giant counts
-__global__ void k_split_counts(const unsigned long long* __restrict__ pairs, int P,
-                               unsigned long long* __restrict__ dcounts, unsigned long long* __restrict__ gcounts) {
-  const int r = threadIdx.x;
-  if (r < P) {
-    dcounts[r] = pairs[2 * r];
-    gcounts[r] = pairs[2 * r + 1];
+  const int32_t G = gword[0];
+  const int64_t nwords = slice >> 6;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t w0 = wave * kCompactWords; w0 < nwords; w0 += nwaves * kCompactWords) {
+    int32_t nv[kCompactWords], ov[kCompactWords];
+#pragma unroll
+    for (int k = 0; k < kCompactWords; ++k) {
+      // a word past the slice re-reads word 0 (valid address; masked below)
+      const int64_t i = ((w0 + k < nwords) ? (w0 + k) : 0) * 64 + lane;
+      nv[k] = Ln_own[i];
+      ov[k] = Lc_own[i];
+    }
+    u64 m[kCompactWords], mg[kCompactWords], bmw = 0;
+    int cnt = 0, gcnt = 0;
+#pragma unroll
+    for (int k = 0; k < kCompactWords; ++k) {
+      const bool in = w0 + k < nwords;
+      const bool chg = in && nv[k] != ov[k], isg = in && nv[k] == G;
+      m[k] = __ballot(chg);
+      mg[k] = __ballot(chg && !isg);
+      const u64 mb = __ballot(isg);
+      bmw = lane == k ? mb : bmw;
+      cnt += __popcll(m[k]);
+      gcnt += __popcll(mg[k]);
+    }
+    if (lane < kCompactWords && w0 + lane < nwords) bm_own[w0 + lane] = bmw;
+    if (cnt == 0) continue;   // wave-uniform
+    unsigned long long base = 0, gbase = 0;
+    if (lane == 0) {
+      base = atomicAdd(&xpair[0], (unsigned long long)cnt);
+      if (gcnt) gbase = atomicAdd(&xpair[1], (unsigned long long)gcnt);
+    }
+    base = __shfl(base, 0, 64);
+    gbase = __shfl(gbase, 0, 64);
+#pragma unroll
+    for (int k = 0; k < kCompactWords; ++k) {
+      const u64 e = ((u64)(uint32_t)((w0 + k) * 64 + lane) << 32) | (u64)(uint32_t)nv[k];
+      if ((m[k] >> lane) & 1ull) dsend[base + __popcll(m[k] & lt)] = e;
+      if ((mg[k] >> lane) & 1ull) gsend[gbase + __popcll(mg[k] & lt)] = e;
+      base += __popcll(m[k]);
+      gbase += __popcll(mg[k]);
+    }
   }
 }
 
@@ -172,49 +210,53 @@ __global__ void k_copy_other(const int4* __restrict__ Lc, int4* __restrict__ Ln,
     if (q < own4_begin || q >= own4_end) Ln[q] = Lc[q];
 }
 
-// apply gathered changes (rank r's entries: drecv[r * cap, r * cap + counts[r])),
-// except those of rank `skip` (its slice of Ln is the tally output already)
 // Posted form (spec != 0): the entries were gathered at a capacity fixed before the
 // counts were known; if any rank's count exceeds it the kernel does nothing (the host,
 // reading the same counts, then runs the exchange again in a form that fits).
-__device__ __forceinline__ bool posted_overflow(const unsigned long long* __restrict__ counts, int32_t P,
-                                                int64_t cap) {
+// counts[r * cs]: rank r's count (cs = 2 on the gathered (delta, giant) pairs).
+__device__ __forceinline__ bool posted_overflow(const unsigned long long* __restrict__ counts, int cs,
+                                                int32_t P, int64_t cap) {
   bool ovf = false;
-  for (int r = 0; r < P; ++r) ovf |= (int64_t)counts[r] > cap;
+  for (int r = 0; r < P; ++r) ovf |= (int64_t)counts[(int64_t)r * cs] > cap;
   return ovf;
 }
 
+// apply gathered entries (rank r's: drecv[r * cap, r * cap + counts[r * cs])) to Ln,
+// except those of rank `skip` (its slice of Ln is the tally output already): the
+// giant form's changed non-G labels
 __global__ void k_delta_apply(const u64* __restrict__ drecv, const unsigned long long* __restrict__ counts,
-                              int64_t cap, int32_t P, int32_t skip, int64_t slice,
-                              int32_t* __restrict__ Ln, int spec) {
-  if (spec && posted_overflow(counts, P, cap)) return;
+                              int cs, int64_t cap, int32_t P, int32_t skip, int64_t slice,
+                              int32_t* __restrict__ Ln) {
   const int64_t tot = cap * P;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot;
        k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = k / cap, j = k - r * cap;
-    if (r != skip && j < (int64_t)counts[r]) {
+    if (r != skip && j < (int64_t)counts[r * cs]) {
       const u64 e = drecv[k];
       Ln[r * slice + (int64_t)(e >> 32)] = (int32_t)(uint32_t)e;
     }
   }
 }
 
-// the gathered changes as flagged al[] scatter chunks + the dirty-arc count: k_diff's
-// output, from the change list instead of a scan of the whole vector.  Frontier (as
-// k_diff): this rank's own changed labels are also copied into Lsync (the current
-// vector Lc, the next superstep's output), so an owned row the next superstep skips
-// already holds its label there.
-__global__ __launch_bounds__(256) void k_delta_chunks(const u64* __restrict__ drecv,
-                                                      const unsigned long long* __restrict__ counts,
+// A delta exchange's whole device side in one pass over the gathered entries: every
+// entry is written into BOTH label buffers -- Ln (the new vector; not for the own
+// rank, whose slice is the tally output) and Lc (the current one, every rank's: the
+// next superstep writes its owned rows into Lc and, frontier, a row it skips must
+// already hold its label there, as k_diff's Lsync) -- so after a delta exchange the two
+// buffers agree and the next delta needs no re-apply of this one; and the changes
+// become flagged al[] scatter chunks + the dirty-arc count (k_diff's output, from the
+// change list instead of a scan of the whole vector).
+__global__ __launch_bounds__(256) void k_delta_finish(const u64* __restrict__ drecv,
+                                                      const unsigned long long* __restrict__ counts, int cs,
                                                       int64_t cap, int32_t P, int64_t slice,
                                                       const int64_t* __restrict__ cptr,
                                                       const int64_t* __restrict__ cch,
                                                       uint8_t* __restrict__ chflag,
                                                       int32_t* __restrict__ chlist,
                                                       unsigned long long* __restrict__ counters,
-                                                      int32_t own, int32_t* __restrict__ Lsync,
-                                                      int spec) {
-  if (spec && posted_overflow(counts, P, cap)) return;
+                                                      int32_t own, int32_t* __restrict__ Lc,
+                                                      int32_t* __restrict__ Ln, int spec) {
+  if (spec && posted_overflow(counts, cs, P, cap)) return;
   const int lane = threadIdx.x & 63;
   const int64_t tot = cap * P;
   unsigned long long dirty = 0;
@@ -224,10 +266,12 @@ __global__ __launch_bounds__(256) void k_delta_chunks(const u64* __restrict__ dr
     int64_t u = 0;
     if (k < tot) {
       const int64_t r = k / cap, j = k - r * cap;
-      if (j < (int64_t)counts[r]) {
+      if (j < (int64_t)counts[r * cs]) {
         const u64 e = drecv[k];
         u = r * slice + (int64_t)(e >> 32);
-        if (r == own) Lsync[u] = (int32_t)(uint32_t)e;
+        const int32_t lab = (int32_t)(uint32_t)e;
+        Lc[u] = lab;
+        if (r != own) Ln[u] = lab;
         dirty += (unsigned long long)(cptr[u + 1] - cptr[u]);
         const int64_t nch = cch[u + 1] - cch[u];
         one = nch == 1;
@@ -259,15 +303,13 @@ int exchange_alloc(lpa_graph* g) {
   if (g->dcap < 1) g->dcap = 1;
   const int64_t P = g->nranks;
   LPA_TRY(dev_alloc(g, (void**)&g->dsend, sizeof(u64) * g->slice));
-  LPA_TRY(dev_alloc(g, (void**)&g->drecv, sizeof(u64) * g->dcap * P * 2));
-  LPA_TRY(dev_alloc(g, (void**)&g->dcount, sizeof(unsigned long long) * (1 + 2 * P)));
+  LPA_TRY(dev_alloc(g, (void**)&g->drecv, sizeof(u64) * g->dcap * P));
+  LPA_TRY(dev_alloc(g, (void**)&g->dcount, sizeof(unsigned long long) * (1 + P)));
   LPA_TRY(dev_alloc(g, (void**)&g->gsend, sizeof(u64) * g->slice));
   LPA_TRY(dev_alloc(g, (void**)&g->gbm, sizeof(unsigned long long) * (g->slice / 64) * P));
   LPA_TRY(dev_alloc(g, (void**)&g->xpair, sizeof(unsigned long long) * (2 + 2 * P)));
-  LPA_TRY(dev_alloc(g, (void**)&g->gcounts, sizeof(unsigned long long) * P));
   LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * 2 * P, hipHostMallocDefault));
   LPA_HIP(hipEventCreateWithFlags(&g->cnt_ev, hipEventDisableTiming));
-  g->dbuf = 0;
   g->prev_delta_ok = false;
   return LPA_OK;
 }
@@ -279,8 +321,8 @@ void exchange_free(lpa_graph* g) {
   g->cnt_ev = nullptr;
 }
 
-u64* exchange_recv_buf(lpa_graph* g) { return g->drecv + (int64_t)g->dbuf * g->dcap * g->nranks; }
-unsigned long long* exchange_recv_counts(lpa_graph* g) { return g->dcount + 1 + (int64_t)g->dbuf * g->nranks; }
+u64* exchange_recv_buf(lpa_graph* g) { return g->drecv; }
+unsigned long long* exchange_recv_counts(lpa_graph* g) { return g->dcount + 1; }
 
 // compact this rank's changed owned labels (Lc -> Ln) into dsend; count -> dcount[0]
 int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
@@ -293,39 +335,29 @@ int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln) {
 }
 
 // Ln := L_{t+1} from the gathered changes in the current receive buffer (cap entries
-// per rank) -- see the header; also queues the al[] position chunks of the changes
-// (counters of parity `par`, the superstep's).  Flips the receive buffer.  posted: the
-// entries were gathered at the fixed capacity `cap` before the counts were read (the
-// kernels stand down on the device if a count exceeds it).
-int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par, bool posted) {
+// per rank, counts[r * cs]) -- see the header; Lc gets them too (the buffers agree
+// afterwards), and the al[] position chunks of the changes are queued (counters of
+// parity `par`, the superstep's).  posted: the entries were
+// gathered at the fixed capacity `cap` before the counts were read (the kernel stands
+// down on the device if a count exceeds it; the host bookkeeping is then left as it was).
+int exchange_finish_delta(lpa_graph* g, int32_t* Lc, int32_t* Ln, int64_t cap, int par,
+                          const unsigned long long* counts, int cs, bool posted) {
   hipStream_t s = g->stream;
   const int P = g->nranks;
   const int64_t n4 = g->vpad / 4;
-  if (g->prev_delta_ok) {
-    const int pb = g->dbuf ^ 1;
-    if (g->prev_cap > 0) {
-      hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(g->prev_cap * P, 8192)), dim3(256), 0, s,
-                         g->drecv + (int64_t)pb * g->dcap * P, g->dcount + 1 + (int64_t)pb * P,
-                         g->prev_cap, P, g->rank, g->slice, Ln, 0);
-      LPA_HIP(hipGetLastError());
-    }
-  } else {
+  if (!g->prev_delta_ok) {
+    // the last exchange was not a delta: Ln outside the own slice still holds L_{t-1}
     hipLaunchKernelGGL(k_copy_other, dim3(grid_of(n4, 8192)), dim3(256), 0, s, (const int4*)Lc,
                        (int4*)Ln, n4, g->own_begin / 4, (g->own_begin + g->slice) / 4);
     LPA_HIP(hipGetLastError());
   }
   if (cap > 0) {
-    hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(cap * P, 8192)), dim3(256), 0, s,
-                       exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->rank, g->slice, Ln, posted);
-    LPA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_delta_chunks, dim3(grid_of(cap * P, 4096)), dim3(256), 0, s,
-                       exchange_recv_buf(g), exchange_recv_counts(g), cap, P, g->slice, g->cptr, g->cch,
-                       g->chflag, g->chlist, g->counters + 4 * par, g->rank, const_cast<int32_t*>(Lc), posted);
+    hipLaunchKernelGGL(k_delta_finish, dim3(grid_of(cap * P, 4096)), dim3(256), 0, s, exchange_recv_buf(g),
+                       counts, cs, cap, P, g->slice, g->cptr, g->cch, g->chflag, g->chlist,
+                       g->counters + 4 * par, g->rank, Lc, Ln, posted ? 1 : 0);
     LPA_HIP(hipGetLastError());
   }
-  g->prev_cap = cap;
-  g->prev_delta_ok = true;
-  g->dbuf ^= 1;
+  if (!posted) g->prev_delta_ok = true;
   return LPA_OK;
 }
 
@@ -351,32 +383,39 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
   *changes_listed = false;
   if (!first) {
     LPA_HIP(hipMemsetAsync(g->xpair, 0, 2 * sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(k_exch_compact, dim3(grid_of(S, 4096)), dim3(256), 0, s, Lc + g->own_begin, Lown, S,
-                       g->gword, g->dsend, g->gsend, g->xpair, g->gbm + (int64_t)g->rank * wpr);
+    // converged supersteps: the frontier lists of this superstep's tally (g->par)
+    const bool list_mode = g->since_reset >= kDenseSupersteps + 2;
+    ListBounds lbd;
+    for (int b = 0; b <= LPA_NBINS; ++b) lbd.b[b] = g->bin_begin[b];
+    hipLaunchKernelGGL(k_exch_compact, dim3(grid_of(S / kCompactWords, 4096)), dim3(256), 0, s, Lc + g->own_begin,
+                       Lown, S,
+                       g->gword, g->dsend, g->gsend, g->xpair, g->gbm + (int64_t)g->rank * wpr,
+                       list_mode ? g->flist : (const int32_t*)nullptr, g->fcnt + 16 * g->par, g->fr_all + g->par, lbd);
     LPA_HIP(hipGetLastError());
     LPA_TRY(coll_allgather(g, g->xpair, g->xpair + 2, 2, 8, s));
-    hipLaunchKernelGGL(k_split_counts, dim3(1), dim3(64 * ((P + 63) / 64)), 0, s, g->xpair + 2, P,
-                       exchange_recv_counts(g), g->gcounts);
-    LPA_HIP(hipGetLastError());
-    LPA_HIP(hipMemcpyAsync(g->h_dcounts, g->xpair + 2, sizeof(unsigned long long) * 2 * P, hipMemcpyDeviceToHost, s));
+    const unsigned long long* pairs = g->xpair + 2;   // rank r: (delta, giant) counts at 2r, 2r + 1
+    LPA_HIP(hipMemcpyAsync(g->h_dcounts, pairs, sizeof(unsigned long long) * 2 * P, hipMemcpyDeviceToHost, s));
     LPA_HIP(hipEventRecord(g->cnt_ev, s));
     // Posted delta (converged supersteps, after a delta exchange of few entries): the
     // entries go out at a capacity fixed from the last counts (the same on every rank),
-    // and the apply + the refresh's change chunks are queued behind them BEFORE the host
-    // waits for the counts, so the GPU keeps working through the host's read.  Kernels
-    // that find a count above the capacity do nothing; the host then sees the same
-    // counts and exchanges again below in the form that fits.
+    // and their apply + the refresh's change chunks are queued behind them BEFORE the
+    // host waits for the counts, so the GPU keeps working through the host's read.  A
+    // count above the capacity makes the queued kernel stand down; the host then sees
+    // the same counts and exchanges again below in the form that fits.
     const int64_t post = !g->prev_delta_ok      ? 0
                          : g->post_fixed < 0    ? g->post_cap
                                                 : std::min(g->post_fixed, g->dcap);
     if (post > 0) {
       LPA_TRY(coll_allgather(g, g->dsend, exchange_recv_buf(g), (size_t)post, 8, s));
-      const int64_t prev_cap = g->prev_cap;
-      const int dbuf = g->dbuf;
-      LPA_TRY(exchange_finish_delta(g, Lc, Ln, post, g->par, true));
-      LPA_HIP(hipEventSynchronize(g->cnt_ev));
-      int64_t capd = 0;
-      for (int k = 0; k < P; ++k) capd = std::max(capd, (int64_t)g->h_dcounts[2 * k]);
+      LPA_TRY(exchange_finish_delta(g, const_cast<int32_t*>(Lc), Ln, post, g->par, pairs, 2, true));
+    }
+    LPA_HIP(hipEventSynchronize(g->cnt_ev));
+    int64_t capd = 0, capg = 0;
+    for (int k = 0; k < P; ++k) {
+      capd = std::max(capd, (int64_t)g->h_dcounts[2 * k]);
+      capg = std::max(capg, (int64_t)g->h_dcounts[2 * k + 1]);
+    }
+    if (post > 0) {
       if (capd <= post) {
         g->last_exchange_delta = capd;
         g->post_cap = posted_cap(g, capd);
@@ -385,17 +424,7 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
         *changes_listed = true;
         return LPA_OK;
       }
-      // overflow: the queued kernels stood down; undo the host-side bookkeeping
-      ++g->n_exch_post_missed;
-      g->prev_cap = prev_cap;
-      g->dbuf = dbuf;
-    } else {
-      LPA_HIP(hipEventSynchronize(g->cnt_ev));
-    }
-    int64_t capd = 0, capg = 0;
-    for (int k = 0; k < P; ++k) {
-      capd = std::max(capd, (int64_t)g->h_dcounts[2 * k]);
-      capg = std::max(capg, (int64_t)g->h_dcounts[2 * k + 1]);
+      ++g->n_exch_post_missed;   // the queued kernel stood down
     }
     // bytes every rank receives per form (the full slice otherwise)
     const int64_t full_b = 4 * S;
@@ -407,7 +436,7 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
       g->post_cap = posted_cap(g, capd);
       ++g->n_exch_delta;
       *changes_listed = true;
-      return exchange_finish_delta(g, Lc, Ln, capd, g->par);
+      return exchange_finish_delta(g, const_cast<int32_t*>(Lc), Ln, capd, g->par, pairs, 2);
     }
     if (giant_b < full_b) {
       // in place: rank r's bitmap words at gbm + r * wpr
@@ -419,8 +448,8 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
                          g->gbm, n4, g->own_begin / 4, (g->own_begin + S) / 4, g->gword);
       LPA_HIP(hipGetLastError());
       if (capg > 0) {
-        hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(capg * P, 8192)), dim3(256), 0, s, ent, g->gcounts, capg,
-                           P, g->rank, S, Ln, 0);
+        hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(capg * P, 8192)), dim3(256), 0, s, ent, pairs + 1, 2, capg,
+                           P, g->rank, S, Ln);
         LPA_HIP(hipGetLastError());
       }
       g->last_exchange_delta = -2;

@@ -25,6 +25,16 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));  // native 16-B vector 
 enum Bin { BIN_SEG = 0, BIN_W16 = 1, BIN_W8 = 2, BIN_W4 = 3, BIN_W2 = 4, BIN_G64 = 5, BIN_G32 = 6,
            BIN_G16 = 7, BIN_G8 = 8, BIN_G4 = 9, BIN_G2 = 10, BIN_G1 = 11, BIN_ISO = 12 };
 static_assert(BIN_ISO + 1 == LPA_NBINS, "bin table");
+// fcnt[] slots (per parity, 16): [b] the dirty-row count of bin b, [kFcntUnits] the unit
+// list's, [kFcntSettled] set by a giant superstep's row settle (lpa_iter.hip)
+// supersteps after L0 that are label-dense: their hub combine runs forked over two
+// streams (launch_hub_combine) and the hub rows of <= kBlockMaxDeg2 arcs are tallied by
+// k_lpa_block (block mode); from kDenseSupersteps + 2 on a superstep is "converged"
+// (captured graphs, frontier lists)
+constexpr int kDenseSupersteps = 2;
+constexpr int kFcntUnits = LPA_NBINS;
+constexpr int kFcntSettled = LPA_NBINS + 1;
+static_assert(kFcntSettled < 16, "fcnt: 16 slots per parity");
 // upper degree bound of each bin (bin b holds bin_max[b+1] < deg <= bin_max[b])
 constexpr int kBinMaxDeg[LPA_NBINS] = {1 << 30, 1024, 512, 256, 128, 64, 32, 16, 8, 4, 2, 1, 0};
 
@@ -223,15 +233,16 @@ struct lpa_graph {
   int32_t* gword = nullptr;     // [8] G of the last refreshed vector (k_giant_pick), worth-trying flag,
                                 //     abits valid (bits-mode rebuild, no scatter since), [3] hot-slot
                                 //     giant-bit count (k_giant_bits), [4] superstep 4 bins: 0 = lists,
-                                //     [5] giant-code refresh taken (superstep 2 settles from al8),
+                                //     [5] giant-code refresh taken (superstep 2 settles from al2),
                                 //     [6] superstep 2's wave bins: 0 = lists of the unsettled rows
   // giant codes (round 5, lpa_iter.hip "Giant codes"): the refresh after superstep 1 on
   // a single GPU, when one label G carries the hubs but not half the hot slots (R-MAT),
   // writes a 1-byte code per arc instead of al[] (code 0 = G, else an 8-bit label hash)
   // for the rows of > 8 arcs, and al[] only for the positions of the rows of <= 8
   bool code_ok = false;         // the handle can take that refresh (P = 1, hot-set rebuild)
-  uint8_t* code8 = nullptr;     // [vpad] code of every slot's label
-  uint8_t* al8 = nullptr;       // [code_pcut rounded up + 512] code of every arc's column label
+  uint32_t* code2 = nullptr;    // [vpad / 16] 2-bit code of every slot's label (16 per word)
+  uint32_t* al2 = nullptr;      // [(code_pcut rounded up to 512 + 512) / 16] 2-bit code of every
+                                //   arc's column label (arc i: word i / 16, bits 2 (i % 16))
   int64_t code_pcut = 0;        // first arc position of the rows of <= 8 arcs (they keep labels)
   bool code3 = false;           // superstep 3 follows a giant-code refresh (read by the host
                                 //   before it: its schedule differs, see run_supersteps)
@@ -272,22 +283,19 @@ struct lpa_graph {
 
   // label exchange (P > 1, lpa_exchange.hip): changed-label deltas
   lpa::u64* dsend = nullptr;                 // [slice] this rank's (slot << 32 | label)
-  lpa::u64* drecv = nullptr;                 // [2][nranks * dcap] gathered deltas
-  unsigned long long* dcount = nullptr;      // [1 + 2 nranks] own count, then every rank's (x2)
+  lpa::u64* drecv = nullptr;                 // [nranks * dcap] gathered deltas
+  unsigned long long* dcount = nullptr;      // [1 + nranks] own count, then every rank's (caller-driven)
   unsigned long long* h_dcounts = nullptr;   // [2 nranks] pinned host copy of the count pairs
   // giant-compressed exchange (lpa_exchange.hip): the giant-label bitmap of every slice
   // ([nranks][slice / 64] words, own slice in place) and the changed non-G entries
   lpa::u64* gsend = nullptr;                 // [slice] this rank's changed non-G (slot << 32 | label)
   unsigned long long* gbm = nullptr;         // [nranks * slice / 64] bit = (label == G)
   unsigned long long* xpair = nullptr;       // [2 + 2 nranks] own (delta, giant) counts, then every rank's
-  unsigned long long* gcounts = nullptr;     // [nranks] every rank's giant-entry count
   int64_t n_exch_giant = 0;                  // exchanges done in the giant-compressed form
   int64_t dcap = 0;                          // delta entries per rank (slice / 4)
   int64_t last_exchange_delta = -1;          // entries per rank of the last exchange (-1 full)
-  int dbuf = 0;                              // receive buffer of the next delta (ping-pong)
-  bool prev_delta_ok = false;                // the other receive buffer holds the previous
-                                             //   superstep's delta (L_{t-1} -> L_t)
-  int64_t prev_cap = 0;                      // its entries per rank
+  bool prev_delta_ok = false;                // the last exchange was a delta: the two label
+                                             //   buffers agree outside the own slice
   int64_t post_cap = 0;                      // posted delta capacity of the next exchange (0: none)
   int64_t post_fixed = -1;                   // lpa_set_posted: -1 adaptive (post_cap), 0 off, > 0 fixed
   int64_t n_exch_posted = 0;                 // delta exchanges that went out before the count read
@@ -394,8 +402,8 @@ void exchange_free(lpa_graph* g);
 int exchange_compact(lpa_graph* g, const int32_t* Lc, const int32_t* Ln);
 lpa::u64* exchange_recv_buf(lpa_graph* g);
 unsigned long long* exchange_recv_counts(lpa_graph* g);
-int exchange_finish_delta(lpa_graph* g, const int32_t* Lc, int32_t* Ln, int64_t cap, int par,
-                          bool posted = false);
+int exchange_finish_delta(lpa_graph* g, int32_t* Lc, int32_t* Ln, int64_t cap, int par,
+                          const unsigned long long* counts, int cs, bool posted = false);
 int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first, bool* changes_listed);
 int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par);
 

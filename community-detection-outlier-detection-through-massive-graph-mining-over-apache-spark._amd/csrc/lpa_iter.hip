@@ -73,10 +73,6 @@ namespace {
 #define LPA_DIAG 0
 #endif
 
-// supersteps after L0 that are label-dense: their hub combine runs forked over two
-// streams (launch_hub_combine) and the hub rows of <= kBlockMaxDeg2 arcs are tallied by
-// k_lpa_block (block mode)
-constexpr int kDenseSupersteps = 2;
 // peel rounds of the wave / unit / block tallies in the label-dense supersteps, where a
 // round rarely retires more than a few votes (measured best of 0/2/4/8 at C3)
 constexpr int kDensePeel = 2;
@@ -1321,9 +1317,8 @@ __global__ __launch_bounds__(256) void k_lpa_units(const int32_t* __restrict__ a
 // whose G votes exceed that sum without staging or merging a single word; only the
 // units of the rows it cannot settle are then tallied exactly (k_lpa_units, list mode).
 // Block 0 also zeroes the undecided-unit list count (*ndec) for k_hub_decide.
-// T = uint8_t: the same from the giant codes al8 (code 0 = G; "Giant codes" below), the
-// form that runs when the refresh after superstep 1 took them (gsel[5]); T = int32_t
-// runs otherwise.
+// (k_lpa_units_code2 below: the same from the 2-bit giant codes, when the refresh took
+// them -- gsel[5]; this form returns at once then.)
 template <typename T>
 __device__ __forceinline__ void unit_load_nb_t(u32 (&raw)[kChunks], const T* __restrict__ al, const Segment& d,
                                                int lane) {
@@ -1342,16 +1337,15 @@ __global__ __launch_bounds__(256) void k_lpa_units_giant(const T* __restrict__ a
                                                          const int32_t* __restrict__ gsel,
                                                          uint32_t* __restrict__ ugc, uint32_t* __restrict__ umx,
                                                          int32_t* __restrict__ ndec) {
-  constexpr bool kCode = sizeof(T) == 1;
   __shared__ u32 hist_all[4][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0) ndec[0] = ndec[2] = 0;  // unit list, block-row list
-  if ((gsel[5] != 0) != kCode) return;  // the other form's turn (uniform)
+  if (gsel[5] != 0) return;  // k_lpa_units_code2's turn (uniform)
   if (gsel[1] == 0) return;  // no giant label worth trying: k_hub_decide lists every row
   u32* hist = hist_all[w];
   hist[lane] = 0u;
-  const u32 G = kCode ? 0u : (u32)gsel[0];
+  const u32 G = (u32)gsel[0];
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t u = (int64_t)blockIdx.x * 4 + w;
   if (u >= nunits) return;  // no block-level barriers in this kernel
@@ -1451,8 +1445,6 @@ __global__ void k_dense_decide(unsigned long long* __restrict__ counters, int64_
 // fcnt[] slot set by the row settle of a giant superstep (k_settle_*): the bin kernels
 // walk lists of the unsettled rows, but the diff scans every slot (settled rows may
 // have changed label)
-constexpr int kFcntSettled = LPA_NBINS + 1;
-static_assert(kFcntSettled < 16, "fcnt: 16 slots per parity");
 __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
                                               const int4* __restrict__ Ln4, int32_t* __restrict__ Lsync,
                                               int64_t s0, int64_t s1,
@@ -1550,7 +1542,6 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
 // the consumed flags and zeroes the other parity's counts.  When every row is
 // tallied (*fr_all) the bin kernels take their ranges and the flags are left alone
 // (a stale flag only costs one redundant tally later).
-constexpr int kFcntUnits = LPA_NBINS;  // fcnt[] slot of the unit count
 constexpr int kListSub = 8;            // 16-byte flag groups per thread, all loaded up front
 constexpr int kListTile = 256 * 16 * kListSub;  // flags per block (32 K: few global atomics per count)
 // bin of slot i from the block's bin bounds in LDS (binary search, 4 reads)
@@ -2596,21 +2587,70 @@ __global__ __launch_bounds__(256) void k_al_rebuild_small(const unsigned long lo
 // decide nearly every row for G: a row's G votes above every bucket of a label hash of
 // its other votes make G its strict mode (giant_count; oracle, R-MAT-22: 98 % of the
 // arcs sit in rows so decided with 16 buckets, 100 % of the rows above 64 arcs).
-// A bucket only needs a FUNCTION of the label, so the refresh writes instead:
-//   code8[u]  per slot, 0 = (L1[u] == G), else 1 + an 8-bit hash of L1[u]  (k_code_build)
-//   al8[i]    per arc of the rows above the row bins, code8[col[i]]       (k_code_rebuild,
-//             the hot slots' labels from LDS as in labels mode, the rest gathered as
-//             1-B codes from a 16 MB array -- at C3 the hot 1 M slots are 1 MB of it)
-//   al[i]     per arc of the row bins (<= 64 arcs: 14-18 % of the arcs), their labels
-// and superstep 2 decides the hub rows (k_lpa_units_giant<uint8_t> + k_hub_decide) and
-// the wave-bin rows (k_code_settle_waves) from al8; only the rows left undecided get
-// their al[] entries gathered (k_code_partial_*) and are tallied exactly, in list mode.
-// The row bins tally from al as before.  Exact for any G and any hash (a label's count
-// is at most its bucket's); gword[5] marks the refresh taken, so the labels-mode
-// rebuild is skipped and superstep 2's refresh rebuilds al[] whatever the change count.
+// A bucket only needs a FUNCTION of the label -- and three buckets suffice (oracle,
+// R-MAT-21 superstep 2: rows of 65-1024 arcs holding 99.9 % of their arcs, every hub row,
+// 90 % of the 9-64-arc rows' arcs decided; 63 buckets: 100 / 100 / 99.4 %) -- so the
+// refresh writes 2-bit codes, 0 = (label == G), else 1 + a hash of the label mod 3:
+//   code2     per slot, 16 to a word (k_code_build): 4 MB at C3, one XCD's L2
+//   al2[i]    per arc of the rows above 8 arcs, code2[col[i]], 16 arcs to a word
+//             (k_code_rebuild; the 655,360 hottest slots' codes in LDS)
+//   al[i]     per arc of the rows of <= 8 arcs, their labels
+// and superstep 2 decides the hub rows (k_lpa_units_code2 + k_hub_decide) and the rows of
+// the wave bins and of > 8 arcs (k_code_settle) by popcounts of the code words -- no
+// table, no atomics; only the rows left undecided get their al[] entries gathered
+// (k_code_partial_*) and are tallied exactly, in list mode.  Exact for any G and any hash
+// (a label's count is at most its bucket's); gword[5] marks the refresh taken, so the
+// labels-mode rebuild is skipped and superstep 2's refresh rebuilds al[] whatever the
+// change count.
+// (Round 5 first shipped 8-bit codes with 64-bucket LDS histograms: C3 code rebuild 1.41
+// ms, code settle 0.63 ms -- the histogram atomics and the 16 MB code array's L2 misses.)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ u32 giant_code(u32 x, u32 G) {
-  return x == G ? 0u : 1u + ((((x * 0x9E3779B1u) >> 24) * 255u) >> 8);
+__device__ __forceinline__ u32 giant_code2(u32 x, u32 G) {
+  return x == G ? 0u : 1u + ((((x * 0x9E3779B1u) >> 24) * 3u) >> 8);
+}
+
+// the four codes' counts among the fields of w whose low bits fm selects:
+// c0 | c1 << 16 (x) and c2 | c3 << 16 (y)
+__device__ __forceinline__ void code2_counts(u32 w, u32 fm, u32& x, u32& y) {
+  const u32 lo = w & fm, hi = (w >> 1) & fm;
+  x += (u32)__popc(fm & ~(lo | hi)) | ((u32)__popc(lo & ~hi) << 16);
+  y += (u32)__popc(hi & ~lo) | ((u32)__popc(lo & hi) << 16);
+}
+// low bits of the fields of word wi that hold arcs [b, e)
+__device__ __forceinline__ u32 code2_fmask(int64_t wi, int64_t b, int64_t e) {
+  const int64_t base = wi * 16;
+  const int64_t l0 = b - base, h0 = e - base;
+  const int lo = (int)(l0 < 0 ? 0 : l0 > 16 ? 16 : l0), hi = (int)(h0 < 0 ? 0 : h0 > 16 ? 16 : h0);
+  const u32 mh = hi >= 16 ? 0xFFFFFFFFu : ((1u << (2 * hi)) - 1u);
+  const u32 ml = lo >= 16 ? 0xFFFFFFFFu : ((1u << (2 * lo)) - 1u);
+  return mh & ~ml & 0x55555555u;
+}
+// G decided from summed counts: its votes above every bucket
+__device__ __forceinline__ bool code2_decided(u32 x, u32 y) {
+  const u32 c0 = x & 0xFFFFu, c1 = x >> 16, c2 = y & 0xFFFFu, c3 = y >> 16;
+  return c0 > max(c1, max(c2, c3));
+}
+__device__ __forceinline__ u32 spread16(u32 v) {
+  v = (v | (v << 8)) & 0x00FF00FFu;
+  v = (v | (v << 4)) & 0x0F0F0F0Fu;
+  v = (v | (v << 2)) & 0x33333333u;
+  return (v | (v << 1)) & 0x55555555u;
+}
+// the 2-bit codes r[k] of arcs b + 64 k + lane (b a multiple of 512) -> 32 words at
+// al2[b / 16 ..): two ballots per chunk, lane l < 32 assembles word l (chunk l / 4)
+__device__ __forceinline__ void store_code2(uint32_t* __restrict__ al2, int64_t b, const int32_t (&r)[8], int lane) {
+  u64 m0 = 0, m1 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const u64 b0 = __ballot(r[k] & 1), b1 = __ballot((r[k] >> 1) & 1);
+    if ((lane >> 2) == k) {
+      m0 = b0;
+      m1 = b1;
+    }
+  }
+  const int sh = (lane & 3) * 16;
+  const u32 w = spread16((u32)(m0 >> sh) & 0xFFFFu) | (spread16((u32)(m1 >> sh) & 0xFFFFu) << 1);
+  if (lane < 32) al2[(b >> 4) + lane] = w;
 }
 
 // gword[5] = take the giant-code refresh: a rebuild is wanted, G is worth trying, and the
@@ -2623,15 +2663,21 @@ __global__ void k_code_mode(const unsigned long long* __restrict__ counters, int
   if (on) gword[2] = 0;
 }
 
-// code8[u] for every slot (four per 4-B store; vpad is a multiple of 64)
-__global__ __launch_bounds__(256) void k_code_build(const int4* __restrict__ L4, int64_t n4,
-                                                   const int32_t* __restrict__ gword, uint32_t* __restrict__ c4) {
+// code2 for every slot: 16 labels (four int4 loads) -> one word (vpad is a multiple of 64)
+__global__ __launch_bounds__(256) void k_code_build(const int4* __restrict__ L4, int64_t nw,
+                                                   const int32_t* __restrict__ gword, uint32_t* __restrict__ code2) {
   if (gword[5] == 0) return;
   const u32 G = (u32)gword[0];
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
-    const int4 v = L4[q];
-    c4[q] = giant_code((u32)v.x, G) | (giant_code((u32)v.y, G) << 8) | (giant_code((u32)v.z, G) << 16) |
-            (giant_code((u32)v.w, G) << 24);
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += (int64_t)gridDim.x * blockDim.x) {
+    u32 w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int4 v = L4[4 * q + k];
+      w |= (giant_code2((u32)v.x, G) | (giant_code2((u32)v.y, G) << 2) | (giant_code2((u32)v.z, G) << 4) |
+            (giant_code2((u32)v.w, G) << 6))
+           << (8 * k);
+    }
+    code2[q] = w;
   }
 }
 
@@ -2662,28 +2708,25 @@ __device__ __forceinline__ void range_pipe(P1 p1, P2 p2, St st, const int32_t* _
   pipe3(nb, pre, fetch, probe, resolve, store);
 }
 
-// al for [pB, arcs) (pB = code_pcut rounded down to a 512-arc batch) and al8 for [0, pA)
+// al for [pB, arcs) (pB = code_pcut rounded down to a 512-arc batch) and al2 for [0, pA)
 // (pA = code_pcut rounded up, at most the full batches): the batch across code_pcut gets
 // both; the partial last batch (one wave) writes whichever applies.  One 1024-thread
-// block per CU, 160 KB of LDS: the row bins' labels first, with the 40,960 hottest labels
-// in LDS, then the codes, with the 163,840 hottest slots' CODES in LDS -- the gathers are
-// bound by their lane count, not their bytes (1-B codes from a 16 MB array cost nearly
-// what 4-B labels from 64 MB did), so the wider LDS share is the lever.
-// (The class pieces of the blocked labels-mode rebuild measured mixed for the codes: C5's
-// refresh after superstep 2 36.6 -> 34.2 ms, C4's after superstep 1 11.1 -> 13.1 ms; the
-// codes stream plainly.)
+// block per CU, 160 KB of LDS: the rows of <= 8 arcs' labels first, with the 40,960
+// hottest labels in LDS, then the codes, with the 655,360 hottest slots' codes in LDS --
+// the gathers are bound by their lane count, not their bytes, so the LDS share is the
+// lever -- and the others from the 2-bit code array (vpad / 4 bytes: L2-resident at C3).
 __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict__ gword,
                                                        const int32_t* __restrict__ col, int64_t arcs,
                                                        const int32_t* __restrict__ Ln, int64_t nslots,
-                                                       const uint8_t* __restrict__ code8, int64_t p64,
-                                                       uint8_t* __restrict__ al8, int32_t* __restrict__ al) {
+                                                       const uint32_t* __restrict__ code2, int64_t p64,
+                                                       uint32_t* __restrict__ al2, int32_t* __restrict__ al) {
   if (gword[5] == 0) return;
   __shared__ u32 hot[kHotLabelsSingle];
   const u32 G = (u32)gword[0];
   const int lane = threadIdx.x & 63;
   const int64_t nfull = arcs >> 9;
   const int64_t bA = min((p64 + 511) >> 9, nfull), bB = p64 >> 9;
-  // ---- the row bins' labels ----
+  // ---- the labels of the rows of <= 8 arcs ----
   const u32 nh = (u32)(nslots < kHotLabelsSingle ? nslots : kHotLabelsSingle);
   for (u32 i = threadIdx.x; i < nh; i += 1024) hot[i] = (u32)Ln[i];
   __syncthreads();
@@ -2700,56 +2743,114 @@ __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict
              col, bB, nfull);
   // ---- the codes of the rows above ----
   __syncthreads();
-  const u32 nc = (u32)(nslots < 4 * kHotLabelsSingle ? nslots : 4 * kHotLabelsSingle);
-  const uint8_t* hc = reinterpret_cast<const uint8_t*>(hot);
-  for (u32 q = threadIdx.x; q < nc / 4; q += 1024) hot[q] = reinterpret_cast<const uint32_t*>(code8)[q];
+  const u32 nc = (u32)(nslots < 16 * kHotLabelsSingle ? nslots : 16 * kHotLabelsSingle);  // a multiple of 16
+  for (u32 q = threadIdx.x; q < nc / 16; q += 1024) hot[q] = code2[q];
   __syncthreads();
-  auto cp1 = [&](int c) -> u32 { return (u32)hc[(u32)c < nc ? (u32)c : nc - 1u]; };
+  auto cp1 = [&](int c) -> u32 {
+    const u32 cc = (u32)c < nc ? (u32)c : nc - 1u;
+    return (hot[cc >> 4] >> ((cc & 15u) * 2u)) & 3u;
+  };
   auto cp2 = [&](int c, u32 w) -> int32_t {
     const bool h = (u32)c < nc;
-    const u32 x = code8[h ? 0 : c];
-    return (int32_t)(h ? w : x);
+    const u32 x = code2[h ? 0u : ((u32)c >> 4)];
+    return (int32_t)(h ? w : ((x >> (((u32)c & 15u) * 2u)) & 3u));
   };
-  range_pipe(cp1, cp2,
-             [&](int64_t b, const int32_t (&r)[8]) {
-#pragma unroll
-               for (int k = 0; k < 8; ++k) al8[b + k * 64 + lane] = (uint8_t)r[k];
-             },
-             col, 0, bA);
+  range_pipe(cp1, cp2, [&](int64_t b, const int32_t (&r)[8]) { store_code2(al2, b, r, lane); }, col, 0, bA);
   // the partial last batch
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if ((nfull << 9) < arcs && wv == nfull % nw) {
+  const int64_t t0 = nfull << 9;
+  if (t0 < arcs && wv == nfull % nw) {
+    int32_t r[8];
+#pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int64_t i = (nfull << 9) + k * 64 + lane;
+      const int64_t i = t0 + k * 64 + lane;
+      r[k] = 0;
       if (i < arcs) {
-        const int32_t c = col[i];
-        const u32 x = (u32)Ln[c];
-        if (i < p64) al8[i] = (uint8_t)giant_code(x, G);
+        const u32 x = (u32)Ln[col[i]];
+        if (i < p64) r[k] = (int32_t)giant_code2(x, G);
         else al[i] = (int32_t)x;
+      }
+    }
+    if (t0 < p64) store_code2(al2, t0, r, lane);   // uniform; al2 covers this batch then
+  }
+}
+
+// k_lpa_units_giant on the 2-bit giant codes (the refresh took them: gsel[5]): ugc[u] = the
+// unit's code-0 (G) votes, umx[u] = its fullest of the three other buckets, by popcounts of
+// its <= 33 code words (lane l: word l).  Units in batches of 64 per wave (one descriptor
+// load per lane), the words of the next three units in flight.
+__global__ __launch_bounds__(256) void k_lpa_units_code2(const uint32_t* __restrict__ al2,
+                                                         const Segment* __restrict__ units, int64_t nunits,
+                                                         const int32_t* __restrict__ gsel,
+                                                         uint32_t* __restrict__ ugc, uint32_t* __restrict__ umx,
+                                                         int32_t* __restrict__ ndec) {
+  constexpr int D = 4;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) ndec[0] = ndec[2] = 0;  // unit list, block-row list
+  if (gsel[5] == 0) return;  // k_lpa_units_giant's turn (uniform)
+  if (gsel[1] == 0) return;  // no giant label worth trying: k_hub_decide lists every row
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t base = (int64_t)blockIdx.x * 4 + w; base < nunits; base += 64 * stride) {
+    const int64_t uk = base + (int64_t)lane * stride;
+    int64_t bk = 0;
+    int32_t lk = 0;
+    if (uk < nunits) {
+      const Segment sg = units[uk];
+      bk = sg.begin;
+      lk = sg.len & 1023;
+    }
+    const int64_t left = (nunits - base + stride - 1) / stride;
+    const int n = (int)(left < 64 ? left : 64);
+    auto ld = [&](int q) -> u32 {
+      const int64_t b = readlane_i64(bk, q);
+      const int64_t e = b + __builtin_amdgcn_readlane(lk, q);
+      const int64_t w0 = b >> 4, wl = e > b ? (e - 1) >> 4 : w0;
+      const int64_t wi = w0 + lane;
+      return al2[wi <= wl ? wi : wl];
+    };
+    u32 r[D];
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) r[k] = ld(k < n ? k : n - 1);
+    for (int q0 = 0; q0 < n; q0 += D) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const int q = q0 + k;
+        if (q >= n) break;  // uniform
+        r[(k + D - 1) % D] = ld(q + D - 1 < n ? q + D - 1 : n - 1);
+        const int64_t b = readlane_i64(bk, q);
+        const int64_t e = b + __builtin_amdgcn_readlane(lk, q);
+        u32 x = 0, y = 0;
+        code2_counts(r[k], code2_fmask((b >> 4) + lane, b, e), x, y);
+        x = wave_sum_u32(x);
+        y = wave_sum_u32(y);
+        if (lane == 0) {
+          const int64_t id = base + (int64_t)q * stride;
+          ugc[id] = x & 0xFFFFu;
+          umx[id] = max(x >> 16, max(y & 0xFFFFu, y >> 16));
+        }
       }
     }
   }
 }
 
 // The code settle of one bin (supersteps 2 and 3 after a giant-code refresh): a row is
-// decided for G from its al8 codes (G's votes above every bucket of a hash of its other
-// codes, as giant_decide) -- its label written, its dirty flag cleared -- or flagged (rdirty
-// = 1) for its bin's list mode.  Bodies take their share of the bin's rows as (bx, nbx): the
-// blocks of one merged launch (k_code_settle) are split over the seven bins by rows.
-//   wave bins (64 < deg <= 1024, NC chunks): one wave per row, 64 code buckets (LDS),
-//     k_lpa_wave's schedule -- row bounds by 64-row batches (span_batch), the codes of the
-//     next D - 1 rows in flight (branch-free byte loads at clamped positions)
-//   row bins G = 64 / 32 / 16 (8 < deg <= G): G lanes per row in 512-lane batches of
-//     RB = 512 / G rows (k_lpa_rows' layout, one row-offset load per batch), G's votes
-//     counted by ballot, the other codes into 16 buckets per row (LDS, as the row bins'
-//     giant test), the next batch's codes in flight.  Rows of <= 8 arcs keep their labels
-//     (the refresh wrote them; 16 buckets decide too few of them).
+// decided for G from its al2 codes (G's votes above each of the three buckets) -- its
+// label written, its dirty flag cleared -- or flagged (rdirty = 1) for its bin's list mode.
+// Bodies take their share of the bin's rows as (bx, nbx): the blocks of one merged launch
+// (k_code_settle) are split over the seven bins.
+//   wave bins (64 < deg <= 1024, NC chunks): one wave per row, lane l the row's l-th code
+//     word (NC = 16: and word l + 64), k_lpa_wave's schedule -- row bounds by 64-row
+//     batches (span_batch), the words of the next D - 1 rows in flight
+//   row bins of 8 < deg <= 64: one lane per row, its <= 5 words loaded at once
+// Rows of <= 8 arcs keep their labels (the refresh wrote them).
 template <int NC>
-__device__ __forceinline__ void code_settle_wave(const int64_t* __restrict__ rp, const uint8_t* __restrict__ al8,
+__device__ __forceinline__ void code_settle_wave(const int64_t* __restrict__ rp, const uint32_t* __restrict__ al2,
                                                  int64_t vbeg, int64_t vend, int32_t G, int32_t* __restrict__ Ln,
-                                                 uint8_t* __restrict__ rdirty, u32* hist, int64_t bx, int64_t nbx) {
-  constexpr int D = NC <= 4 ? 4 : 3;
+                                                 uint8_t* __restrict__ rdirty, int64_t bx, int64_t nbx) {
+  constexpr int NW = NC > 8 ? 2 : 1;   // a row of <= 64 NC arcs spans <= 4 NC + 1 words
+  constexpr int D = 4;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   BinRows br;
@@ -2759,20 +2860,19 @@ __device__ __forceinline__ void code_settle_wave(const int64_t* __restrict__ rp,
   const int64_t stride = nbx * 4;
   int64_t ib = bx * 4 + w;
   if (ib >= br.n) return;
-  auto load = [&](u32 (&x)[NC], const RowSpan& r) {
-    const int d = span_len(r);
-    const int last = d > 0 ? d - 1 : 0;
+  auto load = [&](u32 (&x)[NW], const RowSpan& r) {
+    const int64_t w0 = r.b >> 4, wl = r.e > r.b ? (r.e - 1) >> 4 : w0;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int off = c * 64 + lane;
-      x[c] = (u32)al8[r.b + (off < last ? off : last)];
+    for (int k = 0; k < NW; ++k) {
+      const int64_t wi = w0 + k * 64 + lane;
+      x[k] = al2[wi <= wl ? wi : wl];
     }
   };
   SpanBatch cur = span_batch(rp, br, ib, stride, lane), nxt;
   nxt.b = nxt.e = 0;
   nxt.v = 0;
   int p = 0;
-  u32 rl[D][NC];
+  u32 rl[D][NW];
 #pragma unroll
   for (int k = 0; k < D - 1; ++k) load(rl[k], span_at(cur, nxt, k));
   while (true) {
@@ -2781,15 +2881,15 @@ __device__ __forceinline__ void code_settle_wave(const int64_t* __restrict__ rp,
       load(rl[(k + D - 1) % D], span_at(cur, nxt, p + D - 1));
       const RowSpan sp = span_at(cur, nxt, p);
       const int64_t v = (int64_t)__builtin_amdgcn_readlane(cur.v, p);
-      const int d = span_len(sp);
-      u32 lab[NC];
+      u32 x = 0, y = 0;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) lab[c] = c * 64 + lane < d ? rl[k][c] : kNone;
-      const u32 cg = wave_sum_u32(giant_count<NC>(lab, NC, 0u, hist, kGiantLg));
-      __builtin_amdgcn_wave_barrier();  // no reordering across (LDS ops of a wave complete in order)
-      const u32 hb = hist[lane];
-      hist[lane] = 0u;
-      const bool settled = cg > wave_max_u32(hb);
+      for (int c = 0; c < NW; ++c) {
+        const int64_t wi = (sp.b >> 4) + c * 64 + lane;
+        code2_counts(rl[k][c], code2_fmask(wi, sp.b, sp.e), x, y);
+      }
+      x = wave_sum_u32(x);
+      y = wave_sum_u32(y);
+      const bool settled = code2_decided(x, y);
       if (lane == 0) {
         if (settled) Ln[v] = G;
         rdirty[v] = settled ? 0 : 1;
@@ -2806,70 +2906,21 @@ __device__ __forceinline__ void code_settle_wave(const int64_t* __restrict__ rp,
   }
 }
 
-template <int G>
-__device__ __forceinline__ void code_settle_rows(const int64_t* __restrict__ rp, const uint8_t* __restrict__ al8,
-                                                 int64_t vbeg, int64_t vend, int32_t Gl, int32_t* __restrict__ Ln,
-                                                 uint8_t* __restrict__ rdirty, u32* hist, int64_t bx, int64_t nbx) {
-  static_assert(G >= 16 && G <= 64, "16 buckets per row: G >= 16 lanes");
-  constexpr int RB = 512 / G;
-  constexpr int kGB = 16;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int gj = lane & (G - 1), gbase = lane & ~(G - 1);
-  const u64 gm = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
-  u32* hg = hist + (lane / G) * kGB;   // 64 / G groups x 16 buckets = the wave's 64 words
-  const int64_t nb = (vend - vbeg + RB - 1) / RB;
-  const int64_t stride = nbx * 4;
-  int64_t bi = bx * 4 + w;
-  if (bi >= nb) return;
-  auto load = [&](u32 (&lab)[kChunks], int64_t r0, int64_t rpl, int64_t rpe) {
+__device__ __forceinline__ void code_settle_rows(const int64_t* __restrict__ rp, const uint32_t* __restrict__ al2,
+                                                 int64_t vbeg, int64_t vend, int32_t G, int32_t* __restrict__ Ln,
+                                                 uint8_t* __restrict__ rdirty, int64_t bx, int64_t nbx) {
+  for (int64_t v = vbeg + bx * 256 + threadIdx.x; v < vend; v += nbx * 256) {
+    const int64_t b = rp[v], e = rp[v + 1];
+    const int64_t w0 = b >> 4, wl = e > b ? (e - 1) >> 4 : w0;
+    u32 wd[5];
 #pragma unroll
-    for (int c = 0; c < kChunks; ++c) {
-      const int rl = c * (64 / G) + lane / G;
-      const int64_t b = __shfl(rpl, rl, 64);
-      const int64_t en = __shfl(rpl, rl + 1 < 64 ? rl + 1 : 63, 64);
-      const int64_t e = rl + 1 < RB ? en : rpe;
-      int64_t a = b + gj < e ? b + gj : e - 1;
-      a = a > 0 ? a : 0;
-      const u32 x = (u32)al8[a];
-      lab[c] = (r0 + rl < vend && gj < e - b) ? x : kNone;
-    }
-  };
-  // batch bi's codes in flight while the previous batch is decided (rows_rp_nb clamps a
-  // batch past the bin to valid addresses)
-  int64_t rpl, rpe, rpl1, rpe1;
-  rows_rp_nb<G>(rp, vbeg + bi * RB, vend, lane, rpl, rpe);
-  u32 lab[kChunks], labn[kChunks];
-  load(lab, vbeg + bi * RB, rpl, rpe);
-  rows_rp_nb<G>(rp, vbeg + (bi + stride) * RB, vend, lane, rpl1, rpe1);
-  while (true) {
-    const int64_t bn = bi + stride;
-    load(labn, vbeg + bn * RB, rpl1, rpe1);
-    rows_rp_nb<G>(rp, vbeg + (bn + stride) * RB, vend, lane, rpl1, rpe1);
-    const int64_t r0 = vbeg + bi * RB;
+    for (int k = 0; k < 5; ++k) wd[k] = al2[w0 + k <= wl ? w0 + k : wl];
+    u32 x = 0, y = 0;
 #pragma unroll
-    for (int c = 0; c < kChunks; ++c) {
-      const u32 lb = lab[c];
-      const u32 cg = (u32)__popcll((__ballot(lb == 0u) >> gbase) & gm);
-      if (lb != 0u && lb != kNone) atomicAdd(&hg[lb & (kGB - 1)], 1u);
-      __builtin_amdgcn_wave_barrier();  // no reordering across (LDS ops of a wave complete in order)
-      u32 mx = 0u;
-      if (gj < kGB) {
-        mx = hg[gj];
-        hg[gj] = 0u;
-      }
-      for (int off = G >> 1; off > 0; off >>= 1) mx = max(mx, (u32)lane::lane_xor(mx, off, lane));
-      const int64_t row = r0 + c * (64 / G) + lane / G;
-      if (gj == 0 && row < vend) {
-        const bool settled = cg > mx;
-        if (settled) Ln[row] = Gl;
-        rdirty[row] = settled ? 0 : 1;
-      }
-    }
-    if (bn >= nb) return;
-    bi = bn;
-#pragma unroll
-    for (int c = 0; c < kChunks; ++c) lab[c] = labn[c];
+    for (int k = 0; k < 5; ++k) code2_counts(wd[k], code2_fmask(w0 + k, b, e), x, y);
+    const bool settled = code2_decided(x, y);
+    if (settled) Ln[v] = G;
+    rdirty[v] = settled ? 0 : 1;
   }
 }
 
@@ -2881,30 +2932,23 @@ struct CodeTasks {
   int64_t vbeg[7], vend[7];
   int32_t first[8];
 };
-__global__ __launch_bounds__(256) void k_code_settle(const int64_t* __restrict__ rp, const uint8_t* __restrict__ al8,
+__global__ __launch_bounds__(256) void k_code_settle(const int64_t* __restrict__ rp, const uint32_t* __restrict__ al2,
                                                      CodeTasks ct, int32_t* __restrict__ gword,
                                                      int32_t* __restrict__ Ln, uint8_t* __restrict__ rdirty) {
-  __shared__ u32 hist_all[4][64];
   const bool on = gword[5] != 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) gword[6] = on ? 0 : 1;
   if (!on) return;  // uniform
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  u32* hist = hist_all[w];
-  hist[lane] = 0u;
   const int32_t G = gword[0];
   int t = 0;
   while (t < 6 && (int32_t)blockIdx.x >= ct.first[t + 1]) ++t;
   const int64_t bx = (int64_t)blockIdx.x - ct.first[t], nbx = ct.first[t + 1] - ct.first[t];
   const int64_t vb = ct.vbeg[t], ve = ct.vend[t];
   switch (t) {
-    case 0: code_settle_wave<16>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
-    case 1: code_settle_wave<8>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
-    case 2: code_settle_wave<4>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
-    case 3: code_settle_wave<2>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
-    case 4: code_settle_rows<64>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
-    case 5: code_settle_rows<32>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
-    default: code_settle_rows<16>(rp, al8, vb, ve, G, Ln, rdirty, hist, bx, nbx); break;
+    case 0: code_settle_wave<16>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
+    case 1: code_settle_wave<8>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
+    case 2: code_settle_wave<4>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
+    case 3: code_settle_wave<2>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
+    default: code_settle_rows(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
   }
 }
 
@@ -2965,7 +3009,7 @@ __global__ __launch_bounds__(256) void k_code_partial_hub(const int32_t* __restr
 
 // Superstep 3 after a giant-code refresh (the refresh after superstep 2; Chung-Lu, where
 // L1 has no giant yet but L2 has one on the hubs): every hub row from its units' G counts
-// and bucket bounds (k_lpa_units_giant<uint8_t>), as k_hub_decide -- settled: the label, no
+// and bucket bounds (k_lpa_units_code2), as k_hub_decide -- settled: the label, no
 // dirty flag on the row or its units; otherwise every unit of the row is flagged (the
 // combine merges a dirty row's every unit) -- one wave per row
 __global__ __launch_bounds__(256) void k_code_settle_hubs(const int64_t* __restrict__ uoff,
@@ -3234,11 +3278,23 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
 // rows after the hub combine), overlapping most of the diff with the tally tail
 // the per-bin dirty-row lists of this superstep (zeroes the other parity's counts)
+// Converged supersteps tally by bin FAMILY (family_now): the wave bins w16..w2 by one
+// k_lpa_wave<16>, the row bins g64..g8 by one k_lpa_rows<64>, g4..g1 by one k_lpa_group<4>
+// -- three launches instead of eleven; each kernel takes any row up to its widest bin's
+// degree, and the family's dirty rows are listed together in its first bin's list
+// (flist[bin_begin[first], + fcnt[first]); the other bins' counts stay 0).  A converged
+// superstep walks a few lists: its time is mostly launch and drain, not work.
+bool family_now(const lpa_graph* g) { return g->since_reset >= kDenseSupersteps + 2; }
 int launch_frontier_lists(lpa_graph* g, hipStream_t st = nullptr, const int32_t* fr = nullptr) {
   if (!st) st = g->stream;
   if (!fr) fr = g->fr_all + g->par;
   BinBounds bnd;
   for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = g->bin_begin[b];
+  if (family_now(g)) {   // a family's later bins empty: their rows fall into its first bin
+    for (int b = BIN_W8; b <= BIN_W2; ++b) bnd.b[b] = g->bin_begin[BIN_G64];
+    for (int b = BIN_G32; b <= BIN_G8; ++b) bnd.b[b] = g->bin_begin[BIN_G4];
+    for (int b = BIN_G2; b <= BIN_G1; ++b) bnd.b[b] = g->bin_begin[BIN_ISO];
+  }
   const int64_t nbr = (g->slice + kListTile - 1) / kListTile;
   const int64_t nbu = (g->n_segs + kListTile - 1) / kListTile;
   hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, st, g->rdirty[g->par],
@@ -3283,12 +3339,13 @@ bool code_tally_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && 
 bool code_tally3_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset == 2 && g->code3; }
 
 // the code settle of the seven settled bins in one launch (k_code_settle; it returns at
-// once unless a giant-code refresh was taken): blocks split over the bins by rows, the
-// row bins' share counted in 512-lane batches
+// once unless a giant-code refresh was taken): blocks split over the bins by work (a
+// wave bin's row: a wave; a row bin's row: a lane and its <= 5 word loads), at most one
+// row per wave (wave bins) or lane (row bins)
 int launch_code_settle(lpa_graph* g, hipStream_t st, int32_t* Lown) {
   const int64_t* bb = g->bin_begin;
   const int bins[7] = {BIN_W16, BIN_W8, BIN_W4, BIN_W2, BIN_G64, BIN_G32, BIN_G16};
-  const int lanes[7] = {64, 64, 64, 64, 64, 32, 16};   // lanes per row
+  const int lanes[7] = {64, 64, 64, 64, 4, 4, 4};   // work per row: a wave; a lane's <= 5 loads
   CodeTasks ct;
   int64_t work[7], tot = 0;
   for (int t = 0; t < 7; ++t) {
@@ -3301,13 +3358,14 @@ int launch_code_settle(lpa_graph* g, hipStream_t st, int32_t* Lown) {
   ct.first[0] = 0;
   for (int t = 0; t < 7; ++t) {
     int64_t nb = tot > 0 ? (work[t] * kBlocks + tot - 1) / tot : 0;
-    const int64_t need = (work[t] + 255) / 256;   // no more blocks than 256 lanes of rows
+    const int64_t rows = ct.vend[t] - ct.vbeg[t];
+    const int64_t need = t < 4 ? (rows + 3) / 4 : (rows + 255) / 256;
     if (nb > need) nb = need;
     if (work[t] > 0 && nb < 1) nb = 1;
     ct.first[t + 1] = ct.first[t] + (int32_t)nb;
   }
   hipLaunchKernelGGL(k_code_settle, dim3((unsigned)(ct.first[7] > 0 ? ct.first[7] : 1)), dim3(256), 0, st, g->rp,
-                     g->al8, ct, g->gword, Lown, g->rdirty[g->par]);
+                     g->al2, ct, g->gword, Lown, g->rdirty[g->par]);
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -3389,8 +3447,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
       // hub rows from their units' code counts, wave-bin rows from their codes; the rest
       // listed (k_code_commit: list mode), their al[] entries gathered after the lists
       if (g->n_segs > 0) {
-        hipLaunchKernelGGL(k_lpa_units_giant<uint8_t>, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
-                           g->al8, g->segs, g->n_segs, g->gword, g->ugc, g->umx, g->gdec);
+        hipLaunchKernelGGL(k_lpa_units_code2, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
+                           g->al2, g->segs, g->n_segs, g->gword, g->ugc, g->umx, g->gdec);
         LPA_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_code_settle_hubs, dim3(cap_grid((g->n_hub + 3) / 4, 2048)), dim3(256), 0, s,
                            g->hub_uoff, g->ugc, g->umx, g->n_hub, g->gword, Lown, g->rdirty[g->par],
@@ -3517,8 +3575,8 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
                        g->al, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
     LPA_HIP(hipGetLastError());
     if (code_tally_now(g)) {  // the form on the giant codes (one of the two returns at once)
-      hipLaunchKernelGGL(k_lpa_units_giant<uint8_t>, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
-                         g->al8, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
+      hipLaunchKernelGGL(k_lpa_units_code2, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
+                         g->al2, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
       LPA_HIP(hipGetLastError());
     }
     LPA_TRY(launch_hub_decide(g, Lown, g->n_hub, gsel));
@@ -3585,6 +3643,36 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // row/group bins (round 4: superstep 2's tail bins g16 .. g1 on the main stream, ahead
   // of the hub combine, measured slower -- 2.08 -> 2.11 ms)
   hipStream_t st_tail = sc;
+  if (family_now(g)) {
+    // bin families (launch_frontier_lists): w16..w2 on aux0, g64..g8 then g4..g1 on aux1
+    const int64_t nw = bb[BIN_G64] - bb[BIN_W16], nr = bb[BIN_G4] - bb[BIN_G64], ng = bb[BIN_ISO] - bb[BIN_G4];
+    LPA_TRY(mark(2 * (BIN_W16 + 1), sb));
+    if (nw > 0) {
+      hipLaunchKernelGGL(k_lpa_wave<16>, dim3(cap_grid((nw + 3) / 4, 2048)), dim3(256), 0, sb, g->rp, g->al, Lown,
+                         bb[BIN_W16], bb[BIN_G64], g->flist, fcnt + BIN_W16, fr_wave, pmax, gsel);
+      LPA_HIP(hipGetLastError());
+    }
+    LPA_TRY(mark(2 * (BIN_W16 + 1) + 1, sb));
+    LPA_TRY(mark(2 * (BIN_G64 + 1), sc));
+    if (nr > 0) {
+      const int64_t nbat = (nr + 7) / 8;
+      hipLaunchKernelGGL(k_lpa_rows<64>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0, sc, g->rp, g->al, Lown,
+                         bb[BIN_G64], bb[BIN_G4], g->flist, fcnt + BIN_G64, fr_rows, sort_after, gsel);
+      LPA_HIP(hipGetLastError());
+    }
+    LPA_TRY(mark(2 * (BIN_G64 + 1) + 1, sc));
+    LPA_TRY(mark(2 * (BIN_G4 + 1), sc));
+    if (ng > 0) {
+      hipLaunchKernelGGL(k_lpa_group<4>, dim3((unsigned)((ng * 4 + 255) / 256)), dim3(256), 0, sc, g->rp, g->al,
+                         Lown, bb[BIN_G4], bb[BIN_ISO], g->flist, fcnt + BIN_G4, fr_rows);
+      LPA_HIP(hipGetLastError());
+    }
+    LPA_TRY(mark(2 * (BIN_G4 + 1) + 1, sc));
+    for (int b : {BIN_W8, BIN_W4, BIN_W2, BIN_G32, BIN_G16, BIN_G8, BIN_G2, BIN_G1}) {   // empty: 0 ms
+      LPA_TRY(mark(2 * (b + 1), sc));
+      LPA_TRY(mark(2 * (b + 1) + 1, sc));
+    }
+  } else {
   LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_wave)
@@ -3609,6 +3697,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)
     LPA_GROUP_LAUNCH(BIN_G1, 1, st_tail)
   }
+  }
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
@@ -3630,7 +3719,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     // label-dense supersteps only count the changed slots (launch_refresh decides)
     const int dm = dense_refresh(g) ? 1 : 0;
     // (the split between the two bin streams follows where w2 ran)
-    const int bw = code_tally_now(g) ? BIN_G64 : BIN_W2;
+    const int bw = (code_tally_now(g) || family_now(g)) ? BIN_G64 : BIN_W2;
     LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[bw], false, g->par, BIN_W16, bw, dm));
     // isolated slots (and the padding) never change: the diff stops at the isolated bin
     LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[bw], bb[BIN_ISO], false, g->par, bw, BIN_ISO, dm));
@@ -3727,11 +3816,11 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
 #undef LPA_HOT_LAUNCH
     if (code) {
       LPA_HIP(hipGetLastError());
-      hipLaunchKernelGGL(k_code_build, dim3(cap_grid((g->vpad / 4 + 255) / 256, 4096)), dim3(256), 0, s,
-                         (const int4*)L, g->vpad / 4, g->gword, (uint32_t*)g->code8);
+      hipLaunchKernelGGL(k_code_build, dim3(cap_grid((g->vpad / 16 + 255) / 256, 4096)), dim3(256), 0, s,
+                         (const int4*)L, g->vpad / 16, g->gword, g->code2);
       LPA_HIP(hipGetLastError());
       hipLaunchKernelGGL(k_code_rebuild, dim3(dev_cus), dim3(1024), 0, s, g->gword, g->col, g->arcs, L,
-                         g->vpad, g->code8, g->code_pcut, g->al8, g->al);
+                         g->vpad, g->code2, g->code_pcut, g->al2, g->al);
     }
   } else {
     const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
@@ -3969,9 +4058,12 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     // lpa_exchange_put (full vector + al[] rebuild) or lpa_exchange_put_delta
     // (changes + refresh); a refresh here would see a partial vector
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));  // stays if there is no refresh
+    // (P > 1 converged supersteps: the scatter folds the rare rebuild, as the P = 1
+    // graph does -- no giant pick / bits / hot-rebuild launches that return at once)
     if ((!exchanges(g) || has_collective(g)) && !early_graph && (last_refresh || t + 1 < n))
       LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par,
-                             bev ? bev[kTallyEv + 2] : nullptr));
+                             bev ? bev[kTallyEv + 2] : nullptr,
+                             exchanges(g) && g->since_reset >= eager));
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 3], s));
     // after the last block-mode superstep the next one tallies every row and unit:
     // the block rows' units staged nothing while k_lpa_block tallied them (set at the
