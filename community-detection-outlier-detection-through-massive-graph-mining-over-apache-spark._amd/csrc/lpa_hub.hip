@@ -194,7 +194,10 @@ __device__ __forceinline__ void queue_row(int64_t h, int T, int nu, int lane,
 // Superstep 2's giant-label decision for the hub rows [0, h_end) (after
 // k_lpa_units_giant): row h's G votes S_g = sum of its units' ugc, and any other
 // label's row count is at most S_m = sum of its units' umx (each unit's fullest
-// bucket).  S_g > S_m: G is the strict mode and is written.  Otherwise the row is
+// bucket).  On the 2-bit giant codes (gsel[5], k_lpa_units_code2) umx packs a unit's
+// three bucket counts (10 bits each) and S_m = the fullest of the three row sums -- the
+// row-level bucket test, not a sum of unit maxima.  S_g > S_m: G is the strict mode and
+// is written.  Otherwise the row is
 // tallied exactly: a unit-tallied row (h < hb2) gets wcount[h] = 0 and its units in
 // ulist2 (count ndec[0]), a block-tier row (h >= hb2, <= 16 units) goes to
 // glist (count ndec[2]); settled unit-tallied rows get wcount[h] = -1 (the combine's
@@ -216,18 +219,38 @@ __global__ __launch_bounds__(256) void k_hub_decide(int64_t h_end, const int64_t
   const bool on = gsel[1] != 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) ndec[3] = on ? 0 : 1;
   if (!on) return;  // uniform: k_lpa_units_giant counted nothing
+  const bool code = gsel[5] != 0;   // uniform
   const int64_t ha = hb2 < h_end ? hb2 : h_end;
   for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < ha; h += stride) {
     const int64_t u0 = uoff[h];
     const int nu = (int)(uoff[h + 1] - u0);
     u64 sg = 0, sm = 0;
-    for (int j = lane; j < nu; j += 64) {
-      sg += ugc[u0 + j];
-      sm += umx[u0 + j];
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      sg += __shfl_xor(sg, off, 64);
-      sm += __shfl_xor(sm, off, 64);
+    if (code) {
+      u64 s1 = 0, s2 = 0, s3 = 0;
+      for (int j = lane; j < nu; j += 64) {
+        const u32 m = umx[u0 + j];
+        sg += ugc[u0 + j];
+        s1 += m & 1023u;
+        s2 += (m >> 10) & 1023u;
+        s3 += m >> 20;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        sg += __shfl_xor(sg, off, 64);
+        s1 += __shfl_xor(s1, off, 64);
+        s2 += __shfl_xor(s2, off, 64);
+        s3 += __shfl_xor(s3, off, 64);
+      }
+      sm = s1 > s2 ? s1 : s2;
+      sm = sm > s3 ? sm : s3;
+    } else {
+      for (int j = lane; j < nu; j += 64) {
+        sg += ugc[u0 + j];
+        sm += umx[u0 + j];
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        sg += __shfl_xor(sg, off, 64);
+        sm += __shfl_xor(sm, off, 64);
+      }
     }
     if (sg > sm) {
       if (lane == 0) {
@@ -251,11 +274,16 @@ __global__ __launch_bounds__(256) void k_hub_decide(int64_t h_end, const int64_t
     if (h < h_end) {
       const int64_t u0 = uoff[h];
       const int nu = (int)(uoff[h + 1] - u0);
-      u32 sg = 0, sm = 0;
+      u32 sg = 0, sm = 0, s1 = 0, s2 = 0, s3 = 0;
       for (int j = 0; j < nu; ++j) {
+        const u32 m = umx[u0 + j];
         sg += ugc[u0 + j];
-        sm += umx[u0 + j];
+        sm += m;
+        s1 += m & 1023u;
+        s2 += (m >> 10) & 1023u;
+        s3 += m >> 20;
       }
+      if (code) sm = max(s1, max(s2, s3));
       if (sg > sm) Ln[h] = G;
       else open = true;
     }

@@ -525,10 +525,15 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
                                                    const int32_t* __restrict__ fcnt_b,
                                                    const int32_t* __restrict__ fr_all) {
   const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
-  const bool live = i < br.n;
-  group_row<G>(rp, al, Ln, live ? br.row(i) : 0, live, lane);
+  // 64 / G rows per wave; grid-stride by waves (the grid is sized to the range: one pass)
+  constexpr int64_t kRows = 64 / G;
+  for (int64_t wb = ((int64_t)blockIdx.x * 4 + w) * kRows; wb < br.n; wb += (int64_t)gridDim.x * 4 * kRows) {
+    const int64_t i = wb + lane / G;
+    const bool live = i < br.n;
+    group_row<G>(rp, al, Ln, live ? br.row(i) : 0, live, lane);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2777,7 +2782,8 @@ __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict
 }
 
 // k_lpa_units_giant on the 2-bit giant codes (the refresh took them: gsel[5]): ugc[u] = the
-// unit's code-0 (G) votes, umx[u] = its fullest of the three other buckets, by popcounts of
+// unit's code-0 (G) votes, umx[u] = its three other buckets' counts (k_hub_decide sums
+// each over the row and takes the fullest: the row-level bucket test), by popcounts of
 // its <= 33 code words (lane l: word l).  Units in batches of 64 per wave (one descriptor
 // load per lane), the words of the next three units in flight.
 __global__ __launch_bounds__(256) void k_lpa_units_code2(const uint32_t* __restrict__ al2,
@@ -2825,10 +2831,10 @@ __global__ __launch_bounds__(256) void k_lpa_units_code2(const uint32_t* __restr
         code2_counts(r[k], code2_fmask((b >> 4) + lane, b, e), x, y);
         x = wave_sum_u32(x);
         y = wave_sum_u32(y);
-        if (lane == 0) {
+        if (lane == 0) {   // umx: the three bucket counts (<= 512 each), 10 bits apiece
           const int64_t id = base + (int64_t)q * stride;
           ugc[id] = x & 0xFFFFu;
-          umx[id] = max(x >> 16, max(y & 0xFFFFu, y >> 16));
+          umx[id] = (x >> 16) | ((y & 0xFFFFu) << 10) | ((y >> 16) << 20);
         }
       }
     }
@@ -2952,8 +2958,9 @@ __global__ __launch_bounds__(256) void k_code_settle(const int64_t* __restrict__
   }
 }
 
-// al[i] = L[col[i]] over the arcs of the rows the code settle left (the wave bins' lists
-// [b0, b1) of this superstep), one wave per row
+// al[i] = L[col[i]] over the arcs of the rows the code settle left (the lists of bins
+// [b0, b1) of this superstep): a wave per row of the wave bins, 16 lanes per row of the
+// row bins (<= 64 arcs: a whole wave per row left 3/4 of its lanes idle)
 __global__ __launch_bounds__(256) void k_code_partial_rows(const int32_t* __restrict__ gword,
                                                            const int64_t* __restrict__ rp,
                                                            const int32_t* __restrict__ col,
@@ -2964,15 +2971,29 @@ __global__ __launch_bounds__(256) void k_code_partial_rows(const int32_t* __rest
   if (gword[5] == 0) return;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int64_t total = 0;
-  for (int b = b0; b < b1; ++b) total += fcnt[b];
-  for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < total; i += (int64_t)gridDim.x * 4) {
+  const int bm = b1 < BIN_G64 ? b1 : BIN_G64;   // [b0, bm): wave bins; [bm, b1): row bins
+  int64_t n1 = 0, n2 = 0;
+  for (int b = b0; b < bm; ++b) n1 += fcnt[b];
+  for (int b = bm; b < b1; ++b) n2 += fcnt[b];
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < n1; i += nw) {
     int64_t acc = 0;
     int b = b0;
     while (i >= acc + fcnt[b]) acc += fcnt[b++];
     const int64_t v = flist[bb.b[b] + (i - acc)];
     const int64_t e = rp[v + 1];
     for (int64_t p = rp[v] + lane; p < e; p += 64) al[p] = L[col[p]];
+  }
+  const int gq = lane >> 4, j = lane & 15;
+  for (int64_t i0 = ((int64_t)blockIdx.x * 4 + w) * 4; i0 < n2; i0 += nw * 4) {
+    const int64_t i = i0 + gq;
+    if (i >= n2) continue;
+    int64_t acc = 0;
+    int b = bm;
+    while (i >= acc + fcnt[b]) acc += fcnt[b++];
+    const int64_t v = flist[bb.b[b] + (i - acc)];
+    const int64_t e = rp[v + 1];
+    for (int64_t p = rp[v] + j; p < e; p += 16) al[p] = L[col[p]];
   }
 }
 
@@ -3023,16 +3044,21 @@ __global__ __launch_bounds__(256) void k_code_settle_hubs(const int64_t* __restr
   const int32_t G = gword[0];
   for (int64_t h = (int64_t)blockIdx.x * 4 + w; h < n_hub; h += (int64_t)gridDim.x * 4) {
     const int64_t u0 = uoff[h], u1 = uoff[h + 1];
-    u64 sg = 0, sm = 0;
+    u64 sg = 0, s1 = 0, s2 = 0, s3 = 0;   // umx: three bucket counts (k_lpa_units_code2)
     for (int64_t u = u0 + lane; u < u1; u += 64) {
+      const u32 m = umx[u];
       sg += ugc[u];
-      sm += umx[u];
+      s1 += m & 1023u;
+      s2 += (m >> 10) & 1023u;
+      s3 += m >> 20;
     }
     for (int off = 32; off > 0; off >>= 1) {
       sg += __shfl_xor(sg, off, 64);
-      sm += __shfl_xor(sm, off, 64);
+      s1 += __shfl_xor(s1, off, 64);
+      s2 += __shfl_xor(s2, off, 64);
+      s3 += __shfl_xor(s3, off, 64);
     }
-    const bool settled = sg > sm;
+    const bool settled = sg > s1 && sg > s2 && sg > s3;
     if (lane == 0) {
       if (settled) Ln[h] = G;
       rdirty[h] = settled ? 0 : 1;
@@ -3278,23 +3304,11 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
 // rows after the hub combine), overlapping most of the diff with the tally tail
 // the per-bin dirty-row lists of this superstep (zeroes the other parity's counts)
-// Converged supersteps tally by bin FAMILY (family_now): the wave bins w16..w2 by one
-// k_lpa_wave<16>, the row bins g64..g8 by one k_lpa_rows<64>, g4..g1 by one k_lpa_group<4>
-// -- three launches instead of eleven; each kernel takes any row up to its widest bin's
-// degree, and the family's dirty rows are listed together in its first bin's list
-// (flist[bin_begin[first], + fcnt[first]); the other bins' counts stay 0).  A converged
-// superstep walks a few lists: its time is mostly launch and drain, not work.
-bool family_now(const lpa_graph* g) { return g->since_reset >= kDenseSupersteps + 2; }
 int launch_frontier_lists(lpa_graph* g, hipStream_t st = nullptr, const int32_t* fr = nullptr) {
   if (!st) st = g->stream;
   if (!fr) fr = g->fr_all + g->par;
   BinBounds bnd;
   for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = g->bin_begin[b];
-  if (family_now(g)) {   // a family's later bins empty: their rows fall into its first bin
-    for (int b = BIN_W8; b <= BIN_W2; ++b) bnd.b[b] = g->bin_begin[BIN_G64];
-    for (int b = BIN_G32; b <= BIN_G8; ++b) bnd.b[b] = g->bin_begin[BIN_G4];
-    for (int b = BIN_G2; b <= BIN_G1; ++b) bnd.b[b] = g->bin_begin[BIN_ISO];
-  }
   const int64_t nbr = (g->slice + kListTile - 1) / kListTile;
   const int64_t nbu = (g->n_segs + kListTile - 1) / kListTile;
   hipLaunchKernelGGL(k_frontier_lists, dim3((unsigned)(nbr + nbu)), dim3(256), 0, st, g->rdirty[g->par],
@@ -3643,36 +3657,6 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // row/group bins (round 4: superstep 2's tail bins g16 .. g1 on the main stream, ahead
   // of the hub combine, measured slower -- 2.08 -> 2.11 ms)
   hipStream_t st_tail = sc;
-  if (family_now(g)) {
-    // bin families (launch_frontier_lists): w16..w2 on aux0, g64..g8 then g4..g1 on aux1
-    const int64_t nw = bb[BIN_G64] - bb[BIN_W16], nr = bb[BIN_G4] - bb[BIN_G64], ng = bb[BIN_ISO] - bb[BIN_G4];
-    LPA_TRY(mark(2 * (BIN_W16 + 1), sb));
-    if (nw > 0) {
-      hipLaunchKernelGGL(k_lpa_wave<16>, dim3(cap_grid((nw + 3) / 4, 2048)), dim3(256), 0, sb, g->rp, g->al, Lown,
-                         bb[BIN_W16], bb[BIN_G64], g->flist, fcnt + BIN_W16, fr_wave, pmax, gsel);
-      LPA_HIP(hipGetLastError());
-    }
-    LPA_TRY(mark(2 * (BIN_W16 + 1) + 1, sb));
-    LPA_TRY(mark(2 * (BIN_G64 + 1), sc));
-    if (nr > 0) {
-      const int64_t nbat = (nr + 7) / 8;
-      hipLaunchKernelGGL(k_lpa_rows<64>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0, sc, g->rp, g->al, Lown,
-                         bb[BIN_G64], bb[BIN_G4], g->flist, fcnt + BIN_G64, fr_rows, sort_after, gsel);
-      LPA_HIP(hipGetLastError());
-    }
-    LPA_TRY(mark(2 * (BIN_G64 + 1) + 1, sc));
-    LPA_TRY(mark(2 * (BIN_G4 + 1), sc));
-    if (ng > 0) {
-      hipLaunchKernelGGL(k_lpa_group<4>, dim3((unsigned)((ng * 4 + 255) / 256)), dim3(256), 0, sc, g->rp, g->al,
-                         Lown, bb[BIN_G4], bb[BIN_ISO], g->flist, fcnt + BIN_G4, fr_rows);
-      LPA_HIP(hipGetLastError());
-    }
-    LPA_TRY(mark(2 * (BIN_G4 + 1) + 1, sc));
-    for (int b : {BIN_W8, BIN_W4, BIN_W2, BIN_G32, BIN_G16, BIN_G8, BIN_G2, BIN_G1}) {   // empty: 0 ms
-      LPA_TRY(mark(2 * (b + 1), sc));
-      LPA_TRY(mark(2 * (b + 1) + 1, sc));
-    }
-  } else {
   LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_wave)
@@ -3697,7 +3681,6 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)
     LPA_GROUP_LAUNCH(BIN_G1, 1, st_tail)
   }
-  }
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
@@ -3719,7 +3702,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     // label-dense supersteps only count the changed slots (launch_refresh decides)
     const int dm = dense_refresh(g) ? 1 : 0;
     // (the split between the two bin streams follows where w2 ran)
-    const int bw = (code_tally_now(g) || family_now(g)) ? BIN_G64 : BIN_W2;
+    const int bw = code_tally_now(g) ? BIN_G64 : BIN_W2;
     LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[bw], false, g->par, BIN_W16, bw, dm));
     // isolated slots (and the padding) never change: the diff stops at the isolated bin
     LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[bw], bb[BIN_ISO], false, g->par, bw, BIN_ISO, dm));

@@ -1,9 +1,10 @@
 """Per-launch HBM traffic of the measured labelPropagation(10) call (the second call of
 tools/pmc_workload5.py) from the tools/pmc_r05.sh passes, per superstep: superstep t ends with its refresh -- the t-th k_giant_pick of the call and
 the rebuild launches right after it.  Summaries for the kernels with a byte model:
-  k_code_rebuild     the giant-code refresh (round 5): col 4 B/arc, a 1-B code per arc
-                     of the coded rows, a 4-B label per arc of the row bins, each slot's
-                     code (1 B) and label (4 B) once
+  k_code_rebuild     the giant-code refresh (round 5): col 4 B/arc, a 2-bit code per arc
+                     of the rows above 8 arcs, a 4-B label per arc of the others, the code
+                     array (1/4 B per slot) and the label vector (4 B per slot) once
+  k_code_build       each label once (4 B/slot) + its 2-bit code (1/4 B/slot)
   k_al_rebuild_hot   col 4 B/arc + al 4 B/arc + each label once (4 B/vertex)
   k_first_runs       al0 4 B/arc + row-start bits 1/8 B/arc + a label per row
 Read factor: the round-2 calibration (4 B/lane streams read FETCH_SIZE = half the bytes).
@@ -37,7 +38,7 @@ def launches(d, counter):
 info = json.load(open(f"{pre}_info.json"))
 A, V = info["arcs"], info["V"]
 bins = list(info["bin_arcs"].values())
-p64 = sum(bins[:5])     # arcs of the rows above the row bins (seg, w16, w8, w4, w2)
+p64 = sum(bins[:8])     # arcs of the coded rows: above 8 arcs (seg, w16..w2, g64, g32, g16)
 F = launches(f"{pre}_fetch", "FETCH_SIZE")
 W = launches(f"{pre}_write", "WRITE_SIZE")
 
@@ -49,7 +50,7 @@ def by_superstep(L):
     seg = L[firsts[1]:] if len(firsts) > 1 else L
     out, t, in_refresh = {}, 1, False
     for _, k, b in seg:
-        if in_refresh and k not in ("k_al_rebuild_hot", "k_code_rebuild"):
+        if in_refresh and k.split("<")[0] not in ("k_al_rebuild_hot", "k_code_rebuild", "k_code_build"):
             t += 1
             in_refresh = False
         out.setdefault(t, {}).setdefault(k, 0.0)
@@ -61,9 +62,10 @@ def by_superstep(L):
 
 fs, ws = by_superstep(F), by_superstep(W)
 model = {
-    "k_code_rebuild": (4 * A + p64 + 4 * (A - p64) + 5 * V,
-                       "col 4 B/arc + code 1 B/arc (rows above the row bins) + label 4 B/arc (row bins) + "
-                       "each slot's code and label once (5 B/vertex)"),
+    "k_code_rebuild": (4 * A + p64 // 4 + 4 * (A - p64) + V // 4 + 4 * V,
+                       "col 4 B/arc + 2-bit code per arc (rows above 8 arcs) + label 4 B/arc (the others) + "
+                       "the code array (1/4 B/slot) and the label vector (4 B/slot) once"),
+    "k_code_build": (4 * V + V // 4, "each label once + its 2-bit code"),
     "k_al_rebuild_hot": (8 * A + 4 * V, "col 4 B/arc + al 4 B/arc + each label once (4 B/vertex)"),
     "k_first_runs": (4 * A + A // 8 + 4 * V, "al0 4 B/arc + row-start bits 1/8 B/arc + a label per row"),
 }
@@ -72,10 +74,11 @@ for t in sorted(fs):
     for k, fb in fs[t].items():
         wb = ws.get(t, {}).get(k, 0.0)
         e = {"fetch_bytes": round(rf * fb), "write_bytes": round(wf * wb), "traffic_bytes": round(rf * fb + wf * wb)}
-        if k in model and e["traffic_bytes"] > 0.2 * model[k][0]:   # a launch that did the work
-            e["algorithmic_bytes"] = model[k][0]
-            e["traffic_over_algorithmic"] = round(e["traffic_bytes"] / model[k][0], 3)
-            e["algorithmic_note"] = model[k][1]
+        kb = k.split("<")[0]
+        if kb in model and e["traffic_bytes"] > 0.2 * model[kb][0]:   # a launch that did the work
+            e["algorithmic_bytes"] = model[kb][0]
+            e["traffic_over_algorithmic"] = round(e["traffic_bytes"] / model[kb][0], 3)
+            e["algorithmic_note"] = model[kb][1]
         rows.setdefault(k, {})[f"superstep_{t}"] = e
 print(json.dumps({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/pmc_r05.sh, "
                             "tools/pmc_workload5.py), the measured (second) labelPropagation(10) call",
