@@ -512,10 +512,12 @@ def main():
     ss1_rb_ms = max_over_ranks(statistics.median(ss1_rb))
     ss1_traffic, ss1_src = measured_traffic("k_al_rebuild_hot_superstep1", config_id)
     if ss1_code:
-        # the giant-code refresh: col 4 B/arc, a 2-bit code per arc of the rows of > 8 arcs,
-        # a 4-B label per arc of the rows of <= 8, the code array (1/4 B per slot) and the
-        # label vector once
-        pcut = sum(list(info["bin_arcs"].values())[:8])
+        # the giant-code refresh: col 4 B/arc, a 2-bit code per arc of the coded rows, a
+        # 4-B label per arc of the others, the code array (1/4 B per slot) and the label
+        # vector once
+        # the coded rows: above 64 arcs on a label vector of <= 64 MB, else above 8 (lpa_build)
+        lbin = 5 if 4 * info["slice"] * info["nranks"] <= 64 << 20 else 8
+        pcut = sum(list(info["bin_arcs"].values())[:lbin])
         ss1_bytes = 4 * info["arcs"] + pcut // 4 + 4 * (info["arcs"] - pcut) + info["V"] // 4 + 4 * info["V"]
     else:
         ss1_bytes = rb_bytes

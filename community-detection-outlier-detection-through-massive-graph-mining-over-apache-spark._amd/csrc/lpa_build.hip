@@ -653,7 +653,14 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
   g->code_ok = P == 1 && !g->pooled && !g->no_scatter && g->rebuild_hot && g->vpad >= kHotMinSlots &&
                g->arcs > 0 && (g->n_hub == 0 || g->hub_lane_begin < g->n_hub);
   if (g->code_ok) {
-    for (int b = 0; b < BIN_G8; ++b) g->code_pcut += g->bin_arcs[b];
+    // the rows of <= 64 arcs keep their labels when the label vector is small (C3: 64 MB,
+    // Infinity-Cache resident): three code buckets leave 10 % of their arcs undecided, whose
+    // gathers superstep 2 then pays, while their label gathers in the refresh cost little
+    // more than codes (C3 superstep 2 1.96 -> 1.78 ms, superstep 1 1.69 -> 1.82); a larger
+    // vector's label gathers miss (C4 superstep 1 8.0 -> 9.4 ms, C5's refresh after
+    // superstep 2 +5 ms): only the rows of <= 8 arcs keep labels there
+    g->code_lbin = 4 * g->vpad <= (int64_t(64) << 20) ? BIN_G64 : BIN_G8;
+    for (int b = 0; b < g->code_lbin; ++b) g->code_pcut += g->bin_arcs[b];
     LPA_TRY(dev_alloc(g, (void**)&g->code2, sizeof(uint32_t) * (size_t)(g->vpad / 16)));
     LPA_TRY(dev_alloc(g, (void**)&g->al2, sizeof(uint32_t) * (size_t)(((g->code_pcut + 511) / 512 * 512 + 512) / 16)));
     LPA_HIP(hipHostMalloc((void**)&g->h_flag, sizeof(int32_t), hipHostMallocDefault));

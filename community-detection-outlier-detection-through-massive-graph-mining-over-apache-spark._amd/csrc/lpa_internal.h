@@ -243,7 +243,9 @@ struct lpa_graph {
   uint32_t* code2 = nullptr;    // [vpad / 16] 2-bit code of every slot's label (16 per word)
   uint32_t* al2 = nullptr;      // [(code_pcut rounded up to 512 + 512) / 16] 2-bit code of every
                                 //   arc's column label (arc i: word i / 16, bits 2 (i % 16))
-  int64_t code_pcut = 0;        // first arc position of the rows of <= 8 arcs (they keep labels)
+  int32_t code_lbin = lpa::BIN_G8;   // first bin whose rows keep their labels in a code refresh
+                                //   (lpa_build: g64 when the label vector is <= 64 MB, else g8)
+  int64_t code_pcut = 0;        // its first arc position
   bool code3 = false;           // superstep 3 follows a giant-code refresh (read by the host
                                 //   before it: its schedule differs, see run_supersteps)
   int32_t* h_flag = nullptr;    // [1] pinned host word for that read

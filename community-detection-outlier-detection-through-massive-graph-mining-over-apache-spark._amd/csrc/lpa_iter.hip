@@ -1547,8 +1547,11 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
 // the consumed flags and zeroes the other parity's counts.  When every row is
 // tallied (*fr_all) the bin kernels take their ranges and the flags are left alone
 // (a stale flag only costs one redundant tally later).
-constexpr int kListSub = 8;            // 16-byte flag groups per thread, all loaded up front
-constexpr int kListTile = 256 * 16 * kListSub;  // flags per block (32 K: few global atomics per count)
+#ifndef LPA_LIST_SUB
+#define LPA_LIST_SUB 4
+#endif
+constexpr int kListSub = LPA_LIST_SUB;  // 16-byte flag groups per thread, all loaded up front
+constexpr int kListTile = 256 * 16 * kListSub;  // flags per block (16 K; 8 and 2 groups measured within 3 us per superstep)
 // bin of slot i from the block's bin bounds in LDS (binary search, 4 reads)
 __device__ __forceinline__ int flag_bin(const int64_t* sbb, int64_t i) {
   int b = 0;
@@ -2597,11 +2600,12 @@ __global__ __launch_bounds__(256) void k_al_rebuild_small(const unsigned long lo
 // 90 % of the 9-64-arc rows' arcs decided; 63 buckets: 100 / 100 / 99.4 %) -- so the
 // refresh writes 2-bit codes, 0 = (label == G), else 1 + a hash of the label mod 3:
 //   code2     per slot, 16 to a word (k_code_build): 4 MB at C3, one XCD's L2
-//   al2[i]    per arc of the rows above 8 arcs, code2[col[i]], 16 arcs to a word
+//   al2[i]    per arc of the rows above the cut, code2[col[i]], 16 arcs to a word
 //             (k_code_rebuild; the 655,360 hottest slots' codes in LDS)
-//   al[i]     per arc of the rows of <= 8 arcs, their labels
+//   al[i]     per arc of the rows below the cut (code_lbin: <= 64 arcs on a label vector
+//             of <= 64 MB, else <= 8), their labels
 // and superstep 2 decides the hub rows (k_lpa_units_code2 + k_hub_decide) and the rows of
-// the wave bins and of > 8 arcs (k_code_settle) by popcounts of the code words -- no
+// the other coded rows (k_code_settle) by popcounts of the code words -- no
 // table, no atomics; only the rows left undecided get their al[] entries gathered
 // (k_code_partial_*) and are tallied exactly, in list mode.  Exact for any G and any hash
 // (a label's count is at most its bucket's); gword[5] marks the refresh taken, so the
@@ -2716,7 +2720,7 @@ __device__ __forceinline__ void range_pipe(P1 p1, P2 p2, St st, const int32_t* _
 // al for [pB, arcs) (pB = code_pcut rounded down to a 512-arc batch) and al2 for [0, pA)
 // (pA = code_pcut rounded up, at most the full batches): the batch across code_pcut gets
 // both; the partial last batch (one wave) writes whichever applies.  One 1024-thread
-// block per CU, 160 KB of LDS: the rows of <= 8 arcs' labels first, with the 40,960
+// block per CU, 160 KB of LDS: the labelled rows (code_lbin) first, with the 40,960
 // hottest labels in LDS, then the codes, with the 655,360 hottest slots' codes in LDS --
 // the gathers are bound by their lane count, not their bytes, so the LDS share is the
 // lever -- and the others from the 2-bit code array (vpad / 4 bytes: L2-resident at C3).
@@ -2731,7 +2735,7 @@ __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict
   const int lane = threadIdx.x & 63;
   const int64_t nfull = arcs >> 9;
   const int64_t bA = min((p64 + 511) >> 9, nfull), bB = p64 >> 9;
-  // ---- the labels of the rows of <= 8 arcs ----
+  // ---- the labels of the rows below the cut ----
   const u32 nh = (u32)(nslots < kHotLabelsSingle ? nslots : kHotLabelsSingle);
   for (u32 i = threadIdx.x; i < nh; i += 1024) hot[i] = (u32)Ln[i];
   __syncthreads();
@@ -2850,7 +2854,8 @@ __global__ __launch_bounds__(256) void k_lpa_units_code2(const uint32_t* __restr
 //     word (NC = 16: and word l + 64), k_lpa_wave's schedule -- row bounds by 64-row
 //     batches (span_batch), the words of the next D - 1 rows in flight
 //   row bins of 8 < deg <= 64: one lane per row, its <= 5 words loaded at once
-// Rows of <= 8 arcs keep their labels (the refresh wrote them).
+//   row bins of 8 < deg <= 64 (a cut at g8): one lane per row, its <= 5 words loaded at once
+// Rows below the cut keep their labels (the refresh wrote them): their tasks are empty.
 template <int NC>
 __device__ __forceinline__ void code_settle_wave(const int64_t* __restrict__ rp, const uint32_t* __restrict__ al2,
                                                  int64_t vbeg, int64_t vend, int32_t G, int32_t* __restrict__ Ln,
@@ -3364,7 +3369,7 @@ int launch_code_settle(lpa_graph* g, hipStream_t st, int32_t* Lown) {
   int64_t work[7], tot = 0;
   for (int t = 0; t < 7; ++t) {
     ct.vbeg[t] = bb[bins[t]];
-    ct.vend[t] = bb[bins[t] + 1];
+    ct.vend[t] = bins[t] < g->code_lbin ? bb[bins[t] + 1] : bb[bins[t]];   // labelled bins: no rows
     work[t] = (ct.vend[t] - ct.vbeg[t]) * lanes[t];
     tot += work[t];
   }
@@ -3479,7 +3484,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
       BinBounds bnd;
       for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = bb[b];
       hipLaunchKernelGGL(k_code_partial_rows, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
-                         g->flist, fcnt, bnd, (int)BIN_W16, (int)BIN_G8);
+                         g->flist, fcnt, bnd, (int)BIN_W16, (int)g->code_lbin);
       LPA_HIP(hipGetLastError());
       hipLaunchKernelGGL(k_code_partial_hub, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
                          (const int32_t*)nullptr, (const int32_t*)nullptr, g->ulist, fcnt + kFcntUnits, g->segs);
@@ -3489,10 +3494,10 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // the wave bins' "fr_all": superstep 2 after a giant-code refresh walks the lists above;
   // the row bins': superstep 3's code commit keeps them in range mode (gword[7])
   const int32_t* fr_wave = code_tally_now(g) ? g->gword + 6 : fr_bins;
-  // the row bins of > 8 arcs settle from codes as the wave bins (superstep 2: gword[6];
-  // superstep 3: fr_all, 0 after k_code_commit); those of <= 8 arcs keep their ranges
-  const int32_t* fr_rows_hi = fr_wave;
+  // the labelled row bins of a code refresh (from code_lbin on) take their ranges (superstep
+  // 3 after one: gword[7], k_code_commit); coded row bins below it follow the wave bins
   const int32_t* fr_rows = code_tally3_now(g) ? g->gword + 7 : fr_bins;
+  auto fr_row = [&](int bin) { return bin < g->code_lbin ? fr_wave : fr_rows; };
   if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 5], s));
   if (sb != s) {
     LPA_HIP(hipEventRecord(g->ev_fork, s));
@@ -3510,10 +3515,10 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     BinBounds bnd;
     for (int b = 0; b <= LPA_NBINS; ++b) bnd.b[b] = bb[b];
     hipLaunchKernelGGL(k_code_partial_rows, dim3(2048), dim3(256), 0, sb, g->gword, g->rp, g->col, Lc, g->al,
-                       g->flist, fcnt, bnd, (int)BIN_W16, (int)BIN_G8);
+                       g->flist, fcnt, bnd, (int)BIN_W16, (int)g->code_lbin);
     LPA_HIP(hipGetLastError());
-    // the row bins of > 8 arcs (third stream) walk these lists too: they wait for them
-    if (sc != sb) LPA_HIP(hipEventRecord(g->ev_join2[2], sb));
+    // coded row bins (a cut below g64) on the third stream walk these lists: they wait
+    if (sc != sb && g->code_lbin > BIN_G64) LPA_HIP(hipEventRecord(g->ev_join2[2], sb));
   }
 
   auto mark = [&](int i, hipStream_t st) -> int {
@@ -3661,21 +3666,21 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W2, 2, code_tally_now(g) ? sb : sc, fr_wave)
-  if (code_tally_now(g)) {
-    // superstep 2 after a giant-code refresh: the bins of <= 8 arcs first (their ranges,
-    // labels written by the refresh), then, behind the code settle, the listed rows above
+  if (code_tally_now(g) && g->code_lbin > BIN_G64) {
+    // superstep 2 after a code refresh that coded the rows of 9-64 arcs: the labelled bins
+    // first (their ranges), then, behind the code settle's lists, the coded row bins
     LPA_ROWS_LAUNCH(BIN_G8, 8, fr_rows, st_tail)
     LPA_GROUP_LAUNCH(BIN_G4, 4, st_tail)
     LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)
     LPA_GROUP_LAUNCH(BIN_G1, 1, st_tail)
     if (sc != sb) LPA_HIP(hipStreamWaitEvent(sc, g->ev_join2[2], 0));
-    LPA_ROWS_LAUNCH(BIN_G64, 64, fr_rows_hi, sc)
-    LPA_ROWS_LAUNCH(BIN_G32, 32, fr_rows_hi, sc)
-    LPA_ROWS_LAUNCH(BIN_G16, 16, fr_rows_hi, st_tail)
+    LPA_ROWS_LAUNCH(BIN_G64, 64, fr_row(BIN_G64), sc)
+    LPA_ROWS_LAUNCH(BIN_G32, 32, fr_row(BIN_G32), sc)
+    LPA_ROWS_LAUNCH(BIN_G16, 16, fr_row(BIN_G16), st_tail)
   } else {
-    LPA_ROWS_LAUNCH(BIN_G64, 64, fr_rows_hi, sc)
-    LPA_ROWS_LAUNCH(BIN_G32, 32, fr_rows_hi, sc)
-    LPA_ROWS_LAUNCH(BIN_G16, 16, fr_rows_hi, st_tail)
+    LPA_ROWS_LAUNCH(BIN_G64, 64, fr_row(BIN_G64), sc)
+    LPA_ROWS_LAUNCH(BIN_G32, 32, fr_row(BIN_G32), sc)
+    LPA_ROWS_LAUNCH(BIN_G16, 16, fr_row(BIN_G16), st_tail)
     LPA_ROWS_LAUNCH(BIN_G8, 8, fr_rows, st_tail)
     LPA_GROUP_LAUNCH(BIN_G4, 4, st_tail)
     LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)

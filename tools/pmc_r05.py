@@ -2,7 +2,7 @@
 tools/pmc_workload5.py) from the tools/pmc_r05.sh passes, per superstep: superstep t ends with its refresh -- the t-th k_giant_pick of the call and
 the rebuild launches right after it.  Summaries for the kernels with a byte model:
   k_code_rebuild     the giant-code refresh (round 5): col 4 B/arc, a 2-bit code per arc
-                     of the rows above 8 arcs, a 4-B label per arc of the others, the code
+                     of the coded rows (above 64 or 8 arcs), a 4-B label per arc of the others, the code
                      array (1/4 B per slot) and the label vector (4 B per slot) once
   k_code_build       each label once (4 B/slot) + its 2-bit code (1/4 B/slot)
   k_al_rebuild_hot   col 4 B/arc + al 4 B/arc + each label once (4 B/vertex)
@@ -38,7 +38,8 @@ def launches(d, counter):
 info = json.load(open(f"{pre}_info.json"))
 A, V = info["arcs"], info["V"]
 bins = list(info["bin_arcs"].values())
-p64 = sum(bins[:8])     # arcs of the coded rows: above 8 arcs (seg, w16..w2, g64, g32, g16)
+# arcs of the coded rows: above 64 arcs on a label vector of <= 64 MB, else above 8 (lpa_build)
+p64 = sum(bins[:5]) if 4 * info["slice"] <= 64 << 20 else sum(bins[:8])
 F = launches(f"{pre}_fetch", "FETCH_SIZE")
 W = launches(f"{pre}_write", "WRITE_SIZE")
 
@@ -63,7 +64,7 @@ def by_superstep(L):
 fs, ws = by_superstep(F), by_superstep(W)
 model = {
     "k_code_rebuild": (4 * A + p64 // 4 + 4 * (A - p64) + V // 4 + 4 * V,
-                       "col 4 B/arc + 2-bit code per arc (rows above 8 arcs) + label 4 B/arc (the others) + "
+                       "col 4 B/arc + 2-bit code per arc (the coded rows) + label 4 B/arc (the others) + "
                        "the code array (1/4 B/slot) and the label vector (4 B/slot) once"),
     "k_code_build": (4 * V + V // 4, "each label once + its 2-bit code"),
     "k_al_rebuild_hot": (8 * A + 4 * V, "col 4 B/arc + al 4 B/arc + each label once (4 B/vertex)"),
