@@ -219,14 +219,24 @@ def test_vertex_order_invariance(gfa, oracle, monkeypatch, locality):
 
 def test_c2_sbm_full_size(gfa, oracle):
     """Config C2: planted partition, 1 M vertices / 20 M edges /
-    100 blocks, maxIter 10: bit-exact vs the oracle, and the communities recover the
-    planted blocks (NMI vs ground truth; oracle value at seed 20261015: 0.916)."""
+    100 blocks, maxIter 10: bit-exact vs the oracle at EVERY superstep (the shipped
+    schedule, then the frontier off), lpa_run(10) likewise, and the communities recover
+    the planted blocks (NMI vs ground truth; oracle value at seed 20261015: 0.916)."""
     from sklearn.metrics import normalized_mutual_info_score as nmi
     V, B, m = 1_000_000, 100, 20_000_000
     s, d = gfa.gen_sbm(V, B, m)
+    _, hist, _ = oracle.lpa(V, s.cpu().numpy(), d.cpu().numpy(), 10, per_iter=True)
+    ref = hist[9]
     with gfa.Graph(s, d, V) as g:
+        for frontier in (True, False):
+            g.set_frontier(frontier)
+            g.reset()
+            for t in range(10):
+                g.step(1)
+                bad = int((g.labels() != hist[t]).sum())
+                assert bad == 0, f"frontier={frontier} superstep {t + 1}: {bad} labels differ"
+        g.set_frontier(True)
         lab = g.run(10)
-    ref = oracle.lpa(V, s.cpu().numpy(), d.cpu().numpy(), 10)
     assert np.array_equal(lab, ref)
     truth = np.minimum(np.arange(V) // (V // B), B - 1)
     assert nmi(truth, lab) > 0.9
