@@ -68,6 +68,7 @@ class LpaGraphInfo(ctypes.Structure):
         ("graph_replays", ctypes.c_int64),
         ("exchanges_posted", ctypes.c_int64),
         ("exchanges_post_missed", ctypes.c_int64),
+        ("gather_mode", ctypes.c_int64),
     ]
 
     def to_dict(self):

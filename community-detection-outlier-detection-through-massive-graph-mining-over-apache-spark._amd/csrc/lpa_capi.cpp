@@ -580,6 +580,7 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->graph_replays = g->n_graph_replays;
   info->exchanges_posted = g->n_exch_posted;
   info->exchanges_post_missed = g->n_exch_post_missed;
+  info->gather_mode = g->gather ? 1 : 0;
   if (g->code_ok && g->gword) {
     int32_t w = 0;
     LPA_HIP(hipMemcpyAsync(&w, g->gword + 5, sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));

@@ -243,6 +243,8 @@ struct lpa_graph {
   uint32_t* code2 = nullptr;    // [vpad / 16] 2-bit code of every slot's label (16 per word)
   uint32_t* al2 = nullptr;      // [(code_pcut rounded up to 512 + 512) / 16] 2-bit code of every
                                 //   arc's column label (arc i: word i / 16, bits 2 (i % 16))
+  bool gather = false;          // gather mode: supersteps 1..kGatherSteps tally from L[col[i]] with
+                                //   no al[] refresh; the last of them rebuilds al (lpa_build)
   int32_t code_lbin = lpa::BIN_G8;   // first bin whose rows keep their labels in a code refresh
                                 //   (lpa_build: g64 when the label vector is <= 64 MB, else g8)
   int64_t code_pcut = 0;        // its first arc position
@@ -278,8 +280,9 @@ struct lpa_graph {
   int serial = 0;                           // LPA_SERIAL=1: all tally kernels on one stream (profiling)
   int use_graphs = 1;                       // LPA_GRAPHS=0: no captured superstep graphs
   // captured supersteps: [0, 4) converged per (cur, par); [4, 12) supersteps 2 and 3 per
-  // (superstep, cur, par); [12, 16) superstep 3 after a giant-code refresh
-  hipGraphExec_t gexec[16] = {};
+  // (superstep, cur, par); [12, 16) superstep 3 after a giant-code refresh; [16, 24) the
+  // converged supersteps of gather mode (5 and 6, cur, par)
+  hipGraphExec_t gexec[24] = {};
   int locality = 2;                         // LPA_LOCALITY: neighbour keys of the locality order (0: plain)
   unsigned long long* counters = nullptr;  // [2][4] per parity: [0] chunk count, [1] dirty arcs
 

@@ -476,11 +476,20 @@ __device__ __forceinline__ u64 decided_groups(u64 act, u64 my, u64 best, int gba
   return __ballot(my != 0ull && (u32)(best >> 32) > rem);
 }
 
+// A vote of arc i.  Gather mode (kG, lpa_build: one GPU, a label vector that stays in L2,
+// no row above 128 arcs -- C2): src is col and the vote is L[col[i]], read from the
+// current vector itself, so no al[] refresh runs at all; otherwise src is al[].
+template <bool kG>
+__device__ __forceinline__ u32 arc_vote(const int32_t* __restrict__ src, const int32_t* __restrict__ L, int64_t i) {
+  if constexpr (kG) return (u32)L[(int32_t)ld_stream(src + i)];
+  else return ld_stream(src + i);
+}
+
 // G lanes per row (G <= 64, all 64 lanes of the wave call it: ballot peel)
-template <int G>
+template <int G, bool kG = false>
 __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
                                           int32_t* __restrict__ Ln, int64_t v, bool live, int lane,
-                                          u64* tab = nullptr) {
+                                          u64* tab = nullptr, const int32_t* __restrict__ Lg = nullptr) {
   const int j = lane & (G - 1);
   int64_t b = 0;
   int d = 0;
@@ -488,7 +497,7 @@ __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const 
     b = rp[v];
     d = (int)(rp[v + 1] - b);
   }
-  const u32 lab = j < d ? ld_stream(al + b + j) : kNone;
+  const u32 lab = j < d ? arc_vote<kG>(al, Lg, b + j) : kNone;
   if constexpr (G == 1) {
     if (live) Ln[v] = (int32_t)lab;
   } else if constexpr (G == 2) {
@@ -517,13 +526,14 @@ __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const 
   }
 }
 
-template <int G>
+template <int G, bool kG = false>
 __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ rp,
                                                    const int32_t* __restrict__ al,
                                                    int32_t* __restrict__ Ln, int64_t vbeg,
                                                    int64_t vend, const int32_t* __restrict__ flist,
                                                    const int32_t* __restrict__ fcnt_b,
-                                                   const int32_t* __restrict__ fr_all) {
+                                                   const int32_t* __restrict__ fr_all,
+                                                   const int32_t* __restrict__ Lg) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
@@ -532,7 +542,7 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
   for (int64_t wb = ((int64_t)blockIdx.x * 4 + w) * kRows; wb < br.n; wb += (int64_t)gridDim.x * 4 * kRows) {
     const int64_t i = wb + lane / G;
     const bool live = i < br.n;
-    group_row<G>(rp, al, Ln, live ? br.row(i) : 0, live, lane);
+    group_row<G, kG>(rp, al, Ln, live ? br.row(i) : 0, live, lane, nullptr, Lg);
   }
 }
 
@@ -580,15 +590,15 @@ __device__ __forceinline__ void row_load(u32 (&raw)[NC], const int32_t* __restri
 
 // branch-free form (k_lpa_wave's ring): an empty span (past the bin's end) loads
 // al[0] and its labels are never read -- no control flow for the waitcnt pass to merge
-template <int NC>
+template <int NC, bool kG = false>
 __device__ __forceinline__ void row_load_nb(u32 (&raw)[NC], const int32_t* __restrict__ al,
-                                            const RowSpan& r, int lane) {
+                                            const RowSpan& r, int lane, const int32_t* __restrict__ Lg = nullptr) {
   const int d = span_len(r);
   const int last = d > 0 ? d - 1 : 0;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int off = c * 64 + lane;
-    raw[c] = ld_stream(al + r.b + (off < last ? off : last));
+    raw[c] = arc_vote<kG>(al, Lg, r.b + (off < last ? off : last));
   }
 }
 
@@ -678,14 +688,15 @@ constexpr int wave_ring_depth() { return NC <= 2 ? 6 : NC <= 4 ? 4 : 3; }
 // bins w2 / w4 / w8 / w16 (64 < deg <= 64 * NC): one wave per row, grid-stride; D
 // label register sets in an unrolled ring (labels D - 1 rows ahead), row bounds by
 // 64-row batches one batch ahead (span_batch).
-template <int NC>
+template <int NC, bool kG = false>
 __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp,
                                                   const int32_t* __restrict__ al,
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend, const int32_t* __restrict__ flist,
                                                   const int32_t* __restrict__ fcnt_b,
                                                   const int32_t* __restrict__ fr_all, int pmax,
-                                                  const int32_t* __restrict__ gsel) {
+                                                  const int32_t* __restrict__ gsel,
+                                                  const int32_t* __restrict__ Lg) {
   constexpr int kCap = 2 * 64 * NC;
   constexpr int D = wave_ring_depth<NC>();
   static_assert(D >= 2 && D <= 64, "ring depth");
@@ -712,11 +723,11 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
   int p = 0;  // current row: work item ib + p * stride
   u32 rl[D][NC];
 #pragma unroll
-  for (int k = 0; k < D - 1; ++k) row_load_nb<NC>(rl[k], al, span_at(cur, nxt, k), lane);
+  for (int k = 0; k < D - 1; ++k) row_load_nb<NC, kG>(rl[k], al, span_at(cur, nxt, k), lane, Lg);
   while (true) {
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-      row_load_nb<NC>(rl[(k + D - 1) % D], al, span_at(cur, nxt, p + D - 1), lane);
+      row_load_nb<NC, kG>(rl[(k + D - 1) % D], al, span_at(cur, nxt, p + D - 1), lane, Lg);
       const RowSpan s = span_at(cur, nxt, p);
       const int64_t v = (int64_t)__builtin_amdgcn_readlane(cur.v, p);
       row_tally<NC>(rl[k], s, v, Ln, tab, lst, lane, lt, pmax, giant, G);
@@ -880,10 +891,10 @@ __device__ __forceinline__ void rows_rp(const int64_t* __restrict__ rp, int64_t 
   rpe = rp[min(r0 + RB, vend)];
 }
 
-template <int G>
+template <int G, bool kG = false>
 __device__ __forceinline__ void rows_labels(u32 (&lab)[kChunks], const int32_t* __restrict__ al,
                                             int64_t r0, int64_t vend, int64_t rpl, int64_t rpe,
-                                            int lane) {
+                                            int lane, const int32_t* __restrict__ Lg = nullptr) {
   constexpr int RB = 512 / G;
 #pragma unroll
   for (int c = 0; c < kChunks; ++c) {
@@ -894,7 +905,7 @@ __device__ __forceinline__ void rows_labels(u32 (&lab)[kChunks], const int32_t* 
     const int64_t b = __shfl(rpl, rl, 64);
     const int64_t en = __shfl(rpl, rl + 1 < 64 ? rl + 1 : 63, 64);
     const int64_t e = rl + 1 < RB ? en : rpe;
-    lab[c] = (r0 + rl < vend && j < e - b) ? ld_stream(al + b + j) : kNone;
+    lab[c] = (r0 + rl < vend && j < e - b) ? arc_vote<kG>(al, Lg, b + j) : kNone;
   }
 }
 
@@ -913,10 +924,10 @@ __device__ __forceinline__ void rows_rp_nb(const int64_t* __restrict__ rp, int64
 
 // (vbits bit c: chunk c's label is a vote -- one register per set, applied when the set
 // is tallied, so nothing 64-bit stays live while the loads are in flight)
-template <int G>
+template <int G, bool kG = false>
 __device__ __forceinline__ void rows_labels_nb(u32 (&lab)[kChunks], u32& vbits, const int32_t* __restrict__ al,
                                                int64_t r0, int64_t vend, int64_t rpl, int64_t rpe,
-                                               int lane) {
+                                               int lane, const int32_t* __restrict__ Lg = nullptr) {
   constexpr int RB = 512 / G;
   vbits = 0u;
 #pragma unroll
@@ -928,20 +939,21 @@ __device__ __forceinline__ void rows_labels_nb(u32 (&lab)[kChunks], u32& vbits, 
     const int64_t e = rl + 1 < RB ? en : rpe;
     int64_t a = b + j < e ? b + j : e - 1;
     a = a > 0 ? a : 0;
-    lab[c] = ld_stream(al + a);
+    lab[c] = arc_vote<kG>(al, Lg, a);
     vbits |= (r0 + rl < vend && j < e - b) ? (1u << c) : 0u;
   }
   asm volatile("" : "+v"(vbits));  // computed here: not sunk to the tally (64-bit bounds would stay live)
 }
 
-template <int G>
+template <int G, bool kG = false>
 __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp,
                                                   const int32_t* __restrict__ al,
                                                   int32_t* __restrict__ Ln, int64_t vbeg,
                                                   int64_t vend, const int32_t* __restrict__ flist,
                                                   const int32_t* __restrict__ fcnt_b,
                                                   const int32_t* __restrict__ fr_all, int sort_after,
-                                                  const int32_t* __restrict__ gsel) {
+                                                  const int32_t* __restrict__ gsel,
+                                                  const int32_t* __restrict__ Lg) {
   static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "lane width");
   constexpr int RB = 512 / G;  // rows per batch
   constexpr int kGB = 16;      // giant-label histogram buckets per row (group)
@@ -960,7 +972,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
     for (int64_t i0 = ((int64_t)blockIdx.x * 4 + w) * per; i0 < br.n; i0 += nw * per) {
       const int64_t i = i0 + lane / G;
       const bool live = i < br.n;
-      group_row<G>(rp, al, Ln, live ? br.row(i) : 0, live, lane, htab);
+      group_row<G, kG>(rp, al, Ln, live ? br.row(i) : 0, live, lane, htab, Lg);
     }
     return;
   }
@@ -976,14 +988,14 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
   u32* hg = &ghist_all[w][(lane / G) * kGB];
   const int gj = lane & (G - 1);   // G >= kGB when giant: lane gj < kGB owns bucket gj
   if (gj < kGB) hg[gj] = 0u;
-  if constexpr (G == 64) {
+  if constexpr (G == 64 && !kG) {
     // g64 (33-64 arcs, eight rows per batch): the two-batch form -- the ring's extra
     // label set cost C2 (SBM, nearly every row here) 61.5 -> 57.6 GTEPS (same box)
     int64_t rpl0, rpe0, rpl1 = 0, rpe1 = 0;
     rows_rp<G>(rp, vbeg + bi * RB, vend, lane, rpl0, rpe0);
     if (bi + stride < nb) rows_rp<G>(rp, vbeg + (bi + stride) * RB, vend, lane, rpl1, rpe1);
     u32 lab[kChunks];
-    rows_labels<G>(lab, al, vbeg + bi * RB, vend, rpl0, rpe0, lane);
+    rows_labels<G, kG>(lab, al, vbeg + bi * RB, vend, rpl0, rpe0, lane, Lg);
     const int gbase = lane & ~(G - 1);
     const u64 gm = G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull);
     while (true) {
@@ -992,7 +1004,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       if (bn + stride < nb) rows_rp<G>(rp, vbeg + (bn + stride) * RB, vend, lane, rpl2, rpe2);
       u32 labn[kChunks];
       if (bn < nb) {
-        rows_labels<G>(labn, al, vbeg + bn * RB, vend, rpl1, rpe1, lane);
+        rows_labels<G, kG>(labn, al, vbeg + bn * RB, vend, rpl1, rpe1, lane, Lg);
       } else {
   #pragma unroll
         for (int c = 0; c < kChunks; ++c) labn[c] = kNone;
@@ -1094,6 +1106,37 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
       if ((lane & (G - 1)) == 0 && row < vend && best) Ln[row] = (int32_t)(~(u32)best);
     }
   };
+  if constexpr (kG) {
+    // gather mode (al = col): a vote is a column load and a dependent label gather, so
+    // the ring runs them a step apart -- at the tally of batch i the gathers of batch
+    // i + 1 (its columns arrived a step earlier) and the columns of batch i + 2 are in
+    // flight, and each wait is for loads issued a full step before
+    constexpr int D = kRowsRing;
+    static_assert(D == 3, "slot arithmetic below");
+    int64_t rpl[D], rpe[D];
+    u32 cc[D][kChunks], labg[D][kChunks], vb[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) rows_rp_nb<G>(rp, vbeg + (bi + k * stride) * RB, vend, lane, rpl[k], rpe[k]);
+    rows_labels_nb<G, false>(cc[0], vb[0], al, vbeg + bi * RB, vend, rpl[0], rpe[0], lane);
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) labg[0][c] = (u32)Lg[(int32_t)cc[0][c]];
+    rows_labels_nb<G, false>(cc[1], vb[1], al, vbeg + (bi + stride) * RB, vend, rpl[1], rpe[1], lane);
+    while (true) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const int k1 = (k + 1) % D, k2 = (k + 2) % D;
+        __builtin_amdgcn_sched_barrier(0);
+        rows_rp_nb<G>(rp, vbeg + (bi + D * stride) * RB, vend, lane, rpl[k], rpe[k]);
+#pragma unroll
+        for (int c = 0; c < kChunks; ++c) labg[k1][c] = (u32)Lg[(int32_t)cc[k1][c]];
+        rows_labels_nb<G, false>(cc[k2], vb[k2], al, vbeg + (bi + 2 * stride) * RB, vend, rpl[k2], rpe[k2], lane);
+        __builtin_amdgcn_sched_barrier(0);
+        tally_batch(labg[k], vb[k], vbeg + bi * RB);
+        bi += stride;
+        if (bi >= nb) return;
+      }
+    }
+  } else {
   // Ring of kRowsRing batches (batch j in slot j % kRowsRing): the offsets of batch
   // i + kRowsRing are issued before the labels of batch i + kRowsRing - 1, so the wait
   // for those labels' offsets (issued one batch earlier, ahead of the previous batch's
@@ -1106,19 +1149,20 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
 #pragma unroll
   for (int k = 0; k < D; ++k) rows_rp_nb<G>(rp, vbeg + (bi + k * stride) * RB, vend, lane, rpl[k], rpe[k]);
 #pragma unroll
-  for (int k = 0; k < D - 1; ++k) rows_labels_nb<G>(lab[k], vb[k], al, vbeg + (bi + k * stride) * RB, vend, rpl[k], rpe[k], lane);
+  for (int k = 0; k < D - 1; ++k) rows_labels_nb<G, kG>(lab[k], vb[k], al, vbeg + (bi + k * stride) * RB, vend, rpl[k], rpe[k], lane, Lg);
   while (true) {
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       __builtin_amdgcn_sched_barrier(0);
       rows_rp_nb<G>(rp, vbeg + (bi + D * stride) * RB, vend, lane, rpl[k], rpe[k]);
       const int kl = (k + D - 1) % D;
-      rows_labels_nb<G>(lab[kl], vb[kl], al, vbeg + (bi + (D - 1) * stride) * RB, vend, rpl[kl], rpe[kl], lane);
+      rows_labels_nb<G, kG>(lab[kl], vb[kl], al, vbeg + (bi + (D - 1) * stride) * RB, vend, rpl[kl], rpe[kl], lane, Lg);
       __builtin_amdgcn_sched_barrier(0);
       tally_batch(lab[k], vb[k], vbeg + bi * RB);
       bi += stride;
       if (bi >= nb) return;
     }
+  }
   }
   }
 }
@@ -1872,6 +1916,7 @@ static_assert(kSegArcs == 512, "unit of a position: (p - rp[row]) >> 9");
 __device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, const uint32_t* __restrict__ cpos,
                                              int32_t* __restrict__ al, bool all, const FrontierMarks& fm,
                                              int lane) {
+  if (al == nullptr && all) return;  // gather mode without marks: nothing to write (uniform)
   const int k = (n + 15) >> 4;
   int incl = k;
 #pragma unroll
@@ -1904,7 +1949,7 @@ __device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, cons
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           if (q + u < cnt) {
-            al[p[u]] = lv;
+            if (al) al[p[u]] = lv;   // gather mode: marks only
             if (!all) fm.mark(p[u]);
           }
       }
@@ -3309,6 +3354,14 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // produced right after them (aux0 w16..w4, aux1 w2..g1 + isolated, main the seg
 // rows after the hub combine), overlapping most of the diff with the tally tail
 // the per-bin dirty-row lists of this superstep (zeroes the other parity's counts)
+// Gather mode (lpa_build: small label vector, no row above 128 arcs -- C2) for the first
+// kGatherSteps supersteps: their tallies read L[col[i]] (arc_vote), no al[] is written
+// (the scatter only marks the frontier), and the last of them rebuilds al once, for the
+// later supersteps, whose cheaper tallies beat the gathers (C2, same box: label-dense
+// supersteps 0.42-0.49 -> 0.34-0.37 ms gathering, converged ones 0.16-0.22 ms from al[]
+// against 0.25-0.30 gathering)
+constexpr int kGatherSteps = 6;
+bool gather_now(const lpa_graph* g) { return g->gather && g->since_reset < kGatherSteps; }
 int launch_frontier_lists(lpa_graph* g, hipStream_t st = nullptr, const int32_t* fr = nullptr) {
   if (!st) st = g->stream;
   if (!fr) fr = g->fr_all + g->par;
@@ -3416,7 +3469,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // below the hubs then walk their unsettled rows' lists (fr_bins = gword[4])
   // (P > 1: each rank settles its owned rows from its own arc giant bits; G is the same
   // on every rank, k_giant_pick reads the replicated vector)
-  const bool settle4 = g->since_reset == 3 && g->abits != nullptr;
+  const bool settle4 = g->since_reset == 3 && g->abits != nullptr && !gather_now(g);  // its abits come from al
   const int32_t* fr_bins = settle4 ? g->gword + 4 : fr_all;
   if (settle4) {
     if (!g->serial) {
@@ -3623,13 +3676,21 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRACE_POINT("seg");
   }
   LPA_TRY(mark(1, s));
+  // gather mode (lpa_build): the votes are Lc[col[i]] -- the kernels read col and Lc
+  const bool gnow = gather_now(g);
+  const int32_t* vsrc = gnow ? g->col : g->al;
 #define LPA_WAVE_LAUNCH(BIN, NC, ST, FR)                                                          \
   {                                                                                           \
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                  \
     LPA_TRY(mark(2 * (BIN + 1), ST));                                                         \
     if (n > 0) {                                                                              \
-      hipLaunchKernelGGL(k_lpa_wave<NC>, dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, ST,  \
-                         g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, pmax, gsel); \
+      if (gnow)                                                                               \
+        hipLaunchKernelGGL((k_lpa_wave<NC, true>), dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, ST, \
+                           g->rp, vsrc, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, pmax, gsel, Lc); \
+      else                                                                                    \
+        hipLaunchKernelGGL((k_lpa_wave<NC, false>), dim3(cap_grid((n + 3) / 4, 2048)), dim3(256), 0, ST, \
+                           g->rp, vsrc, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, pmax, gsel, \
+                           (const int32_t*)nullptr);                                          \
       LPA_HIP(hipGetLastError());                                                             \
     }                                                                                         \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                     \
@@ -3639,8 +3700,13 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     const int64_t n = bb[BIN + 1] - bb[BIN];                                                 \
     LPA_TRY(mark(2 * (BIN + 1), ST));                                                        \
     if (n > 0) {                                                                             \
-      hipLaunchKernelGGL(k_lpa_group<G>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
-                         ST, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_rows); \
+      if (gnow)                                                                              \
+        hipLaunchKernelGGL((k_lpa_group<G, true>), dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
+                           ST, g->rp, vsrc, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_rows, Lc); \
+      else                                                                                   \
+        hipLaunchKernelGGL((k_lpa_group<G, false>), dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, \
+                           ST, g->rp, vsrc, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, fr_rows, \
+                           (const int32_t*)nullptr);                                         \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                    \
@@ -3651,9 +3717,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_TRY(mark(2 * (BIN + 1), ST));                                                        \
     if (n > 0) {                                                                             \
       const int64_t nbat = (n + 512 / G - 1) / (512 / G);                                    \
-      hipLaunchKernelGGL(k_lpa_rows<G>, dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0,   \
-                         ST, g->rp, g->al, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, \
-                         sort_after, gsel);                                                   \
+      if (gnow)                                                                              \
+        hipLaunchKernelGGL((k_lpa_rows<G, true>), dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0, \
+                           ST, g->rp, vsrc, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, \
+                           sort_after, gsel, Lc);                                             \
+      else                                                                                   \
+        hipLaunchKernelGGL((k_lpa_rows<G, false>), dim3(cap_grid((nbat + 3) / 4, 2048)), dim3(256), 0, \
+                           ST, g->rp, vsrc, Lown, bb[BIN], bb[BIN + 1], g->flist, fcnt + BIN, FR, \
+                           sort_after, gsel, (const int32_t*)nullptr);                        \
       LPA_HIP(hipGetLastError());                                                            \
     }                                                                                        \
     LPA_TRY(mark(2 * (BIN + 1) + 1, ST));                                                    \
@@ -3884,7 +3955,10 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
     hipLaunchKernelGGL(k_dense_decide, dim3(1), dim3(64), 0, s, ctr, INT64_MAX, g->gword);
     LPA_HIP(hipGetLastError());
   }
-  if (g->al_pending) {  // the column-run superstep after a lazy reset (al holds nothing)
+  // gather mode (lpa_build): no al[] to keep -- the scatter only marks the rows the next
+  // superstep re-tallies (and syncs the changed labels into Lc), no rebuild
+  const bool gnow = gather_now(g);
+  if (g->al_pending && !gnow) {  // the column-run superstep after a lazy reset (al holds nothing)
     hipLaunchKernelGGL(k_al_fill_unless_rebuild, dim3(cap_grid((g->arcs / 4 + 255) / 256, 8192)), dim3(256), 0, s,
                        ctr, thr, (const v4i*)g->al0, (v4i*)g->al, g->arcs);
     LPA_HIP(hipGetLastError());
@@ -3893,13 +3967,21 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   hipLaunchKernelGGL(k_al_scatter, dim3(2048), dim3(256), 0, s, g->chlist, (const uint4*)g->chflag,
                      (g->n_chunk_scan + 15) / 16, g->cowner, g->cch, ctr,
                      g->counters + 4 * (par ^ 1), g->cptr,
-                     g->cpos, Ln, g->al, thr, fm, g->fr_all + (par ^ 1), g->frontier,
-                     (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc),
-                     fold_rebuild ? g->col : (const int32_t*)nullptr, g->arcs, g->gword);
+                     g->cpos, Ln, gnow ? (int32_t*)nullptr : g->al, thr, fm, g->fr_all + (par ^ 1),
+                     g->frontier, (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc),
+                     (fold_rebuild && !gnow) ? g->col : (const int32_t*)nullptr, g->arcs, g->gword);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   if (ev_scatter) LPA_HIP(hipEventRecord(ev_scatter, s));  // profiling: scatter | rebuild
-  if (!fold_rebuild) LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
+  if (gnow && g->since_reset == kGatherSteps - 1) {
+    // the last gather-mode superstep: al[] for the supersteps after it, one plain rebuild
+    const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
+    hipLaunchKernelGGL(k_al_rebuild<false>, dim3(grid), dim3(256), 0, s, ctr, thr, g->col, g->arcs, Ln, g->al,
+                       g->gword);
+    LPA_HIP(hipGetLastError());
+  } else if (!fold_rebuild && !gnow) {
+    LPA_TRY(launch_rebuild(g, true, thr, Ln, ctr));
+  }
   LPA_HIP(hipGetLastError());
   return LPA_OK;
 }
@@ -3974,7 +4056,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
       LPA_HIP(hipStreamSynchronize(s));
       g->code3 = *g->h_flag != 0;
     }
-    if (!first) LPA_TRY(ensure_al(g));  // a lazy reset's al is needed by the hash tallies
+    if (!first && !gather_now(g)) LPA_TRY(ensure_al(g));  // a lazy reset's al is needed by the hash tallies
+    // the last gather-mode superstep's refresh rebuilds al (launched or in its graph)
+    const bool gather_switch = g->gather && g->since_reset == kGatherSteps - 1;
     const bool diff_in_tally = !exchanges(g) && !g->serial && !first;
     // converged supersteps on one GPU replay a captured HIP graph of the whole
     // superstep (tally on four streams + diff + refresh; ~25 kernels and the
@@ -3990,7 +4074,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     const bool early_graph = g->use_graphs && !exchanges(g) && !g->serial && !first && g->since_reset >= 1 &&
                              g->since_reset <= 2;
     if (g->use_graphs && !exchanges(g) && !g->serial && g->since_reset >= eager) {
-      const int key = g->cur * 2 + g->par;
+      // (gather mode's converged supersteps have their own graphs, keyed by the superstep)
+      const int key = gather_now(g) ? 16 + (g->since_reset - eager) * 4 + g->cur * 2 + g->par
+                                    : g->cur * 2 + g->par;
       if (!g->gexec[key])
         LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
           int rc = launch_tally(g, Lown, nullptr, Lc, Ln, true);
@@ -4000,6 +4086,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
       LPA_HIP(hipGraphLaunch(g->gexec[key], s));
       ++g->n_graph_replays;
       if (tt) LPA_HIP(hipEventRecord(g->ev[2 * t + 1], s));
+      if (gather_switch) g->al_pending = false;
       g->cur ^= 1;
       g->par ^= 1;
       ++g->since_reset;
@@ -4048,10 +4135,12 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 2], s));  // stays if there is no refresh
     // (P > 1 converged supersteps: the scatter folds the rare rebuild, as the P = 1
     // graph does -- no giant pick / bits / hot-rebuild launches that return at once)
-    if ((!exchanges(g) || has_collective(g)) && !early_graph && (last_refresh || t + 1 < n))
+    if ((!exchanges(g) || has_collective(g)) && !early_graph && (last_refresh || t + 1 < n)) {
       LPA_TRY(launch_refresh(g, Lc, Ln, diff_in_tally || changes_listed, g->par,
                              bev ? bev[kTallyEv + 2] : nullptr,
                              exchanges(g) && g->since_reset >= eager));
+      if (gather_switch) g->al_pending = false;
+    }
     if (bev) LPA_HIP(hipEventRecord(bev[kTallyEv + 3], s));
     // after the last block-mode superstep the next one tallies every row and unit:
     // the block rows' units staged nothing while k_lpa_block tallied them (set at the

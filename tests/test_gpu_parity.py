@@ -228,6 +228,7 @@ def test_c2_sbm_full_size(gfa, oracle):
     _, hist, _ = oracle.lpa(V, s.cpu().numpy(), d.cpu().numpy(), 10, per_iter=True)
     ref = hist[9]
     with gfa.Graph(s, d, V) as g:
+        assert g.info()["gather_mode"] == 1   # 4 MB label vector, rows <= 128 arcs
         for frontier in (True, False):
             g.set_frontier(frontier)
             g.reset()
@@ -267,7 +268,7 @@ def test_schedule_options_bit_exact(gfa, oracle, monkeypatch, env):
     """The switches read at graph creation (the serialized profiling
     schedule, superstep 1 by hash tallies, no captured graphs, the plain rebuild, no
     frontier, plain degree order): labels bit-exact per superstep on the degree mix
-    (both block tiers + a bucketed hub) and R-MAT-16."""
+    (both block tiers + a bucketed hub), R-MAT-16 and an SBM in gather mode."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     V, s, d = degree_mix(1)
@@ -281,6 +282,14 @@ def test_schedule_options_bit_exact(gfa, oracle, monkeypatch, env):
     got = _per_step(gfa, 1 << 16, rs, rd, 6)
     for t in range(6):
         assert np.array_equal(got[t], hist[t]), f"rmat16 {env} superstep {t + 1}"
+    # SBM 200 K / 4 M: gather mode (tallies read L[col[i]], no al[] refresh)
+    ss, sd = gfa.gen_sbm(200_000, 20, 4_000_000)
+    with gfa.Graph(ss, sd, 200_000) as gg:
+        assert gg.info()["gather_mode"] == 1
+    _, hist, _ = oracle.lpa(200_000, ss.cpu().numpy(), sd.cpu().numpy(), 8, per_iter=True)
+    got = _per_step(gfa, 200_000, ss, sd, 8)
+    for t in range(8):
+        assert np.array_equal(got[t], hist[t]), f"sbm {env} superstep {t + 1}"
 
 
 def test_chunglu_generator_matches_oracle(gfa, oracle):
