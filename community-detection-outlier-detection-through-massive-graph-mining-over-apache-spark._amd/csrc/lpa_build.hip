@@ -648,7 +648,7 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
     LPA_TRY(dev_alloc(g, (void**)&g->al0, sizeof(int32_t) * g->arcs));
     LPA_HIP(hipMemcpyAsync(g->al0, g->al, sizeof(int32_t) * g->arcs, hipMemcpyDeviceToDevice, s));
   }
-  // gather mode (lpa_iter.hip arc_vote): one GPU, a label vector that stays in L2 (<= 8 MB),
+  // gather mode (lpa_iter.hip arc_vote): one GPU, a label vector that stays in L2 (<= 4 MB),
   // every row in the bins of <= 128 arcs (no hub / unit / block tier, no wave bin above w2)
   // and the CSC index the scatter marks the frontier with.  The tallies then read L[col[i]]
   // and no al[] refresh runs: a label-dense superstep of C2 (SBM 1 M / 20 M) spent as long
@@ -656,7 +656,7 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
 #ifndef LPA_GATHER_OK
 #define LPA_GATHER_OK 1   // 0: a comparison build without gather mode (tools/ab_lib)
 #endif
-  g->gather = LPA_GATHER_OK && P == 1 && !g->pooled && !g->no_scatter && 4 * g->vpad <= (int64_t(8) << 20) && g->n_hub == 0 &&
+  g->gather = LPA_GATHER_OK && P == 1 && !g->pooled && !g->no_scatter && 4 * g->vpad <= (int64_t(4) << 20) && g->n_hub == 0 &&
               g->bin_begin[BIN_W2] == g->bin_begin[BIN_SEG] && g->arcs > 0;
   // giant codes (lpa_iter.hip): one GPU, the LDS hot-set rebuild's label vectors, and
   // a superstep 2 whose hub rows take the giant decision (block mode, or no hub rows)

@@ -93,7 +93,7 @@ typedef struct lpa_graph_info {
   int64_t exchanges_post_missed; /* ... posted ones whose counts exceeded the posted
                               capacity: exchanged again in the form that fits          */
   int64_t gather_mode;     /* 1: the tallies read L[col[i]] and no al[] refresh runs (one
-                              GPU, label vector <= 8 MB, no row above 128 arcs; since ABI 6) */
+                              GPU, label vector <= 4 MB, no row above 128 arcs; since ABI 6) */
 } lpa_graph_info;
 
 /* Outlier summary. */
