@@ -485,19 +485,12 @@ __device__ __forceinline__ u32 arc_vote(const int32_t* __restrict__ src, const i
   else return ld_stream(src + i);
 }
 
-// G lanes per row (G <= 64, all 64 lanes of the wave call it: ballot peel)
-template <int G, bool kG = false>
-__device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
-                                          int32_t* __restrict__ Ln, int64_t v, bool live, int lane,
-                                          u64* tab = nullptr, const int32_t* __restrict__ Lg = nullptr) {
+// the mode of each G-lane group's votes (kNone: no vote), written to Ln[v] by the group's
+// first lane when live
+template <int G>
+__device__ __forceinline__ void group_tally(u32 lab, int32_t* __restrict__ Ln, int64_t v, bool live, int lane,
+                                            u64* tab) {
   const int j = lane & (G - 1);
-  int64_t b = 0;
-  int d = 0;
-  if (live) {
-    b = rp[v];
-    d = (int)(rp[v + 1] - b);
-  }
-  const u32 lab = j < d ? arc_vote<kG>(al, Lg, b + j) : kNone;
   if constexpr (G == 1) {
     if (live) Ln[v] = (int32_t)lab;
   } else if constexpr (G == 2) {
@@ -524,6 +517,22 @@ __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const 
     }
     if (live && j == 0) Ln[v] = (int32_t)(~(u32)best);
   }
+}
+
+// G lanes per row (G <= 64, all 64 lanes of the wave call it: ballot peel)
+template <int G, bool kG = false>
+__device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
+                                          int32_t* __restrict__ Ln, int64_t v, bool live, int lane,
+                                          u64* tab = nullptr, const int32_t* __restrict__ Lg = nullptr) {
+  const int j = lane & (G - 1);
+  int64_t b = 0;
+  int d = 0;
+  if (live) {
+    b = rp[v];
+    d = (int)(rp[v + 1] - b);
+  }
+  const u32 lab = j < d ? arc_vote<kG>(al, Lg, b + j) : kNone;
+  group_tally<G>(lab, Ln, v, live, lane, tab);
 }
 
 template <int G, bool kG = false>
@@ -3010,7 +3019,9 @@ __global__ __launch_bounds__(256) void k_code_settle(const int64_t* __restrict__
 
 // al[i] = L[col[i]] over the arcs of the rows the code settle left (the lists of bins
 // [b0, b1) of this superstep): a wave per row of the wave bins, 16 lanes per row of the
-// row bins (<= 64 arcs: a whole wave per row left 3/4 of its lanes idle)
+// row bins (<= 64 arcs: a whole wave per row left 3/4 of its lanes idle); a row's rounds
+// are issued at once (the gathers are latency-bound: C4 superstep 2 9.01 -> 8.88 ms; a lane
+// per row with eight rounds measured worse -- its column loads no longer coalesce: +0.8 ms)
 __global__ __launch_bounds__(256) void k_code_partial_rows(const int32_t* __restrict__ gword,
                                                            const int64_t* __restrict__ rp,
                                                            const int32_t* __restrict__ col,
@@ -3031,9 +3042,24 @@ __global__ __launch_bounds__(256) void k_code_partial_rows(const int32_t* __rest
     int b = b0;
     while (i >= acc + fcnt[b]) acc += fcnt[b++];
     const int64_t v = flist[bb.b[b] + (i - acc)];
-    const int64_t e = rp[v + 1];
-    for (int64_t p = rp[v] + lane; p < e; p += 64) al[p] = L[col[p]];
+    const int64_t s0 = rp[v], e = rp[v + 1];
+    for (int64_t p0 = s0; p0 < e; p0 += 256) {   // uniform: four 64-arc rounds at once
+      int32_t c[4], x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t p = p0 + k * 64 + lane;
+        c[k] = col[p < e ? p : e - 1];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = L[c[k]];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t p = p0 + k * 64 + lane;
+        if (p < e) al[p] = x[k];
+      }
+    }
   }
+  // row bins: 16 lanes per row (coalesced column loads), its <= 4 rounds issued at once
   const int gq = lane >> 4, j = lane & 15;
   for (int64_t i0 = ((int64_t)blockIdx.x * 4 + w) * 4; i0 < n2; i0 += nw * 4) {
     const int64_t i = i0 + gq;
@@ -3042,8 +3068,21 @@ __global__ __launch_bounds__(256) void k_code_partial_rows(const int32_t* __rest
     int b = bm;
     while (i >= acc + fcnt[b]) acc += fcnt[b++];
     const int64_t v = flist[bb.b[b] + (i - acc)];
-    const int64_t e = rp[v + 1];
-    for (int64_t p = rp[v] + j; p < e; p += 16) al[p] = L[col[p]];
+    const int64_t s0 = rp[v], e = rp[v + 1];   // row bins hold 1..64 arcs
+    if (e == s0) continue;
+    int32_t c[4], x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t p = s0 + k * 16 + j;
+      c[k] = col[p < e ? p : e - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = L[c[k]];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t p = s0 + k * 16 + j;
+      if (p < e) al[p] = x[k];
+    }
   }
 }
 
@@ -3359,8 +3398,12 @@ int launch_diff(lpa_graph* g, hipStream_t st, const int32_t* Lc, const int32_t* 
 // (the scatter only marks the frontier), and the last of them rebuilds al once, for the
 // later supersteps, whose cheaper tallies beat the gathers (C2, same box: label-dense
 // supersteps 0.42-0.49 -> 0.34-0.37 ms gathering, converged ones 0.16-0.22 ms from al[]
-// against 0.25-0.30 gathering)
-constexpr int kGatherSteps = 6;
+// against 0.25-0.30 gathering; LPA_GATHER_STEPS=99, every superstep gathering, re-measured:
+// supersteps 2-10 2.84 against 2.65 ms)
+#ifndef LPA_GATHER_STEPS
+#define LPA_GATHER_STEPS 6
+#endif
+constexpr int kGatherSteps = LPA_GATHER_STEPS;
 bool gather_now(const lpa_graph* g) { return g->gather && g->since_reset < kGatherSteps; }
 int launch_frontier_lists(lpa_graph* g, hipStream_t st = nullptr, const int32_t* fr = nullptr) {
   if (!st) st = g->stream;
@@ -4074,8 +4117,9 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     const bool early_graph = g->use_graphs && !exchanges(g) && !g->serial && !first && g->since_reset >= 1 &&
                              g->since_reset <= 2;
     if (g->use_graphs && !exchanges(g) && !g->serial && g->since_reset >= eager) {
-      // (gather mode's converged supersteps have their own graphs, keyed by the superstep)
-      const int key = gather_now(g) ? 16 + (g->since_reset - eager) * 4 + g->cur * 2 + g->par
+      // (gather mode's converged supersteps have their own graphs: the plain ones and the
+      // switch superstep, whose refresh rebuilds al)
+      const int key = gather_now(g) ? 16 + (gather_switch ? 4 : 0) + g->cur * 2 + g->par
                                     : g->cur * 2 + g->par;
       if (!g->gexec[key])
         LPA_TRY(capture_graph(g, &g->gexec[key], [&]() -> int {
