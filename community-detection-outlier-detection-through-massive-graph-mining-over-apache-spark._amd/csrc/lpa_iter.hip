@@ -431,7 +431,13 @@ __device__ __forceinline__ u64 group_mode_hash(u32 v, int lane, u64* tab) {
   constexpr u32 kMask = (1u << kLg) - 1u;
   u64* gt = tab + (lane & ~(G - 1)) * 4;
   u64 w = 0ull;
+#if LPA_DIAG == 1
+  // diagnostic (timing only, wrong modes): no table, each vote counted once
+  if (v != kNone) w = (1ull << 32) | (u64)(u32)(~v);
+  if (false) {
+#else
   if (v != kNone) {
+#endif
     const u64 word = (1ull << 32) | (u64)(u32)(~v);
     u32 h = hash_slot(v, 32 - kLg);
     while (true) {
@@ -460,6 +466,12 @@ __device__ __forceinline__ u64 group_mode_hash(u32 v, int lane, u64* tab) {
   }
 }
 
+#if LPA_DIAG == 2
+#define LPA_GV(x) (x)
+#else
+#define LPA_GV(x) ((u32)Lg[(int32_t)(x)])
+#endif
+
 // peel rounds after which a chunk whose groups are still unresolved is hashed instead
 constexpr int kPeelSortAfter = 3;
 
@@ -481,7 +493,12 @@ __device__ __forceinline__ u64 decided_groups(u64 act, u64 my, u64 best, int gba
 // current vector itself, so no al[] refresh runs at all; otherwise src is al[].
 template <bool kG>
 __device__ __forceinline__ u32 arc_vote(const int32_t* __restrict__ src, const int32_t* __restrict__ L, int64_t i) {
+#if LPA_DIAG == 2
+  // diagnostic (timing only, wrong votes): the column itself, no label gather
+  if constexpr (kG) return ld_stream(src + i);
+#else
   if constexpr (kG) return (u32)L[(int32_t)ld_stream(src + i)];
+#endif
   else return ld_stream(src + i);
 }
 
@@ -1128,7 +1145,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
     for (int k = 0; k < D; ++k) rows_rp_nb<G>(rp, vbeg + (bi + k * stride) * RB, vend, lane, rpl[k], rpe[k]);
     rows_labels_nb<G, false>(cc[0], vb[0], al, vbeg + bi * RB, vend, rpl[0], rpe[0], lane);
 #pragma unroll
-    for (int c = 0; c < kChunks; ++c) labg[0][c] = (u32)Lg[(int32_t)cc[0][c]];
+    for (int c = 0; c < kChunks; ++c) labg[0][c] = LPA_GV(cc[0][c]);
     rows_labels_nb<G, false>(cc[1], vb[1], al, vbeg + (bi + stride) * RB, vend, rpl[1], rpe[1], lane);
     while (true) {
 #pragma unroll
@@ -1137,7 +1154,7 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
         __builtin_amdgcn_sched_barrier(0);
         rows_rp_nb<G>(rp, vbeg + (bi + D * stride) * RB, vend, lane, rpl[k], rpe[k]);
 #pragma unroll
-        for (int c = 0; c < kChunks; ++c) labg[k1][c] = (u32)Lg[(int32_t)cc[k1][c]];
+        for (int c = 0; c < kChunks; ++c) labg[k1][c] = LPA_GV(cc[k1][c]);
         rows_labels_nb<G, false>(cc[k2], vb[k2], al, vbeg + (bi + 2 * stride) * RB, vend, rpl[k2], rpe[k2], lane);
         __builtin_amdgcn_sched_barrier(0);
         tally_batch(labg[k], vb[k], vbeg + bi * RB);
