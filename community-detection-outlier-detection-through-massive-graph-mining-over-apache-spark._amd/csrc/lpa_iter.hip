@@ -3702,40 +3702,52 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_HIP(hipEventRecord(g->ev_join2[1], g->aux_stream[2]));
   }
   const int64_t n_units = blk ? g->unit_block2_begin : g->n_segs;
-  if (giant_units && g->n_segs > 0) {
-    hipLaunchKernelGGL(k_lpa_units_giant<int32_t>, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
-                       g->al, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
-    LPA_HIP(hipGetLastError());
-    if (code_tally_now(g)) {  // the form on the giant codes (one of the two returns at once)
-      hipLaunchKernelGGL(k_lpa_units_code2, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
-                         g->al2, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
+  // the main stream's unit work (the hub path's head): enqueued before the bins in the
+  // converged supersteps, after them in supersteps 2-4.  The streams share hardware queues
+  // (GPU_MAX_HW_QUEUES = 4), so the enqueue order decides what waits behind what: with
+  // the units last the row bins no longer queue behind the hub path in the label-dense
+  // supersteps (same box: C3 superstep 2 1.87 -> 1.71 ms, C4 9.28 -> 8.89, C5 28.75 ->
+  // 28.14), while the converged supersteps, whose critical path is the hub path, lost
+  // 8-15 us each that way
+  const bool units_last = !g->serial && g->since_reset >= 1 && g->since_reset <= 3;
+  auto launch_units = [&]() -> int {
+    if (giant_units && g->n_segs > 0) {
+      hipLaunchKernelGGL(k_lpa_units_giant<int32_t>, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
+                         g->al, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
       LPA_HIP(hipGetLastError());
+      if (code_tally_now(g)) {  // the form on the giant codes (one of the two returns at once)
+        hipLaunchKernelGGL(k_lpa_units_code2, dim3(cap_grid((g->n_segs + 3) / 4, 2048)), dim3(256), 0, s,
+                           g->al2, g->segs, g->n_segs, gsel, g->ugc, g->umx, g->gdec);
+        LPA_HIP(hipGetLastError());
+      }
+      LPA_TRY(launch_hub_decide(g, Lown, g->n_hub, gsel));
+      if (code_tally_now(g)) {  // the undecided hub rows' al[] entries (code refresh only)
+        hipLaunchKernelGGL(k_code_partial_hub, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
+                           g->glist, g->gdec + 2, g->ulist2, g->gdec, g->segs);
+        LPA_HIP(hipGetLastError());
+      }
+      // the wide tier's few undecided rows right here on the main stream (the fourth
+      // stream shares a hardware queue with aux1, whose row bins it would delay)
+      if (split) LPA_TRY(launch_block_wide(s));
     }
-    LPA_TRY(launch_hub_decide(g, Lown, g->n_hub, gsel));
-    if (code_tally_now(g)) {  // the undecided hub rows' al[] entries (code refresh only)
-      hipLaunchKernelGGL(k_code_partial_hub, dim3(2048), dim3(256), 0, s, g->gword, g->rp, g->col, Lc, g->al,
-                         g->glist, g->gdec + 2, g->ulist2, g->gdec, g->segs);
+    // serialized profiling: the block kernel bracketed on its own (stats kernel 16),
+    // ahead of the seg units' marks
+    if (blk && g->serial) LPA_TRY(launch_block(s));
+    LPA_TRY(mark(0, s));
+    if (n_units > 0 && giant_units) {
+      hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
+                         g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist2, g->gdec, g->gdec + 3, pmax);
       LPA_HIP(hipGetLastError());
+    } else if (n_units > 0) {
+      hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
+                         g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all, pmax);
+      LPA_HIP(hipGetLastError());
+      LPA_TRACE_POINT("seg");
     }
-    // the wide tier's few undecided rows right here on the main stream (the fourth
-    // stream shares a hardware queue with aux1, whose row bins it would delay)
-    if (split) LPA_TRY(launch_block_wide(s));
-  }
-  // serialized profiling: the block kernel bracketed on its own (stats kernel 16),
-  // ahead of the seg units' marks
-  if (blk && g->serial) LPA_TRY(launch_block(s));
-  LPA_TRY(mark(0, s));
-  if (n_units > 0 && giant_units) {
-    hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
-                       g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist2, g->gdec, g->gdec + 3, pmax);
-    LPA_HIP(hipGetLastError());
-  } else if (n_units > 0) {
-    hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
-                       g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist, fcnt + kFcntUnits, fr_all, pmax);
-    LPA_HIP(hipGetLastError());
-    LPA_TRACE_POINT("seg");
-  }
-  LPA_TRY(mark(1, s));
+    LPA_TRY(mark(1, s));
+    return LPA_OK;
+  };
+  if (!units_last) LPA_TRY(launch_units());
   // gather mode (lpa_build): the votes are Lc[col[i]] -- the kernels read col and Lc
   const bool gnow = gather_now(g);
   const int32_t* vsrc = gnow ? g->col : g->al;
@@ -3820,6 +3832,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
+  if (units_last) LPA_TRY(launch_units());
   // hub combine after the bins are queued: its tail kernels on the aux streams
   // run after those streams' bins
   LPA_TRY(mark(2, s));
