@@ -69,6 +69,7 @@ class LpaGraphInfo(ctypes.Structure):
         ("exchanges_posted", ctypes.c_int64),
         ("exchanges_post_missed", ctypes.c_int64),
         ("gather_mode", ctypes.c_int64),
+        ("host_allgathers", ctypes.c_int64),
     ]
 
     def to_dict(self):
@@ -100,6 +101,8 @@ _vp = ctypes.c_void_p
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
+# lpa_allgather_fn: (send, recv, bytes_per_rank, ctx) -> 0 on success
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 SIGNATURES = {
     "lpa_graph_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_uint32, ctypes.POINTER(_vp)]),
@@ -107,6 +110,9 @@ SIGNATURES = {
     "lpa_graph_create_dist": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "lpa_graph_create_hostcoll": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                                 ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ALLGATHER_FN,
+                                                 _vp, ctypes.POINTER(_vp)]),
     "lpa_set_stream": (ctypes.c_int, [_vp, _vp]),
     "lpa_set_serial": (ctypes.c_int, [_vp, ctypes.c_int32]),
     "lpa_set_frontier": (ctypes.c_int, [_vp, ctypes.c_int32]),

@@ -658,18 +658,22 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
 #endif
   g->gather = LPA_GATHER_OK && P == 1 && !g->pooled && !g->no_scatter && 4 * g->vpad <= (int64_t(4) << 20) && g->n_hub == 0 &&
               g->bin_begin[BIN_W2] == g->bin_begin[BIN_SEG] && g->arcs > 0;
-  // giant codes (lpa_iter.hip): one GPU, the LDS hot-set rebuild's label vectors, and
-  // a superstep 2 whose hub rows take the giant decision (block mode, or no hub rows)
-  g->code_ok = P == 1 && !g->gather && !g->pooled && !g->no_scatter && g->rebuild_hot && g->vpad >= kHotMinSlots &&
-               g->arcs > 0 && (g->n_hub == 0 || g->hub_lane_begin < g->n_hub);
+  // giant codes (lpa_iter.hip): the LDS hot-set rebuild's label vectors (one GPU, or the
+  // rank-strided form of a partitioned job: every rank codes its own arcs against the G
+  // of the replicated vector), and a superstep 2 whose hub rows take the giant decision
+  // (block mode, or no hub rows)
+  g->code_ok = (P == 1 || rebuild_ranked(g)) && !g->gather && !g->pooled && !g->no_scatter && g->rebuild_hot &&
+               g->vpad >= kHotMinSlots && g->arcs > 0 && (g->n_hub == 0 || g->hub_lane_begin < g->n_hub);
   if (g->code_ok) {
     // the rows of <= 64 arcs keep their labels when the label vector is small (C3: 64 MB,
     // Infinity-Cache resident): three code buckets leave 10 % of their arcs undecided, whose
     // gathers superstep 2 then pays, while their label gathers in the refresh cost little
     // more than codes (C3 superstep 2 1.96 -> 1.78 ms, superstep 1 1.69 -> 1.82); a larger
     // vector's label gathers miss (C4 superstep 1 8.0 -> 9.4 ms, C5's refresh after
-    // superstep 2 +5 ms): only the rows of <= 8 arcs keep labels there
+    // superstep 2 +5 ms): only the rows of <= 8 arcs keep labels there.  (The vector is
+    // the full replica at any P, so every rank takes the same cut.)
     g->code_lbin = 4 * g->vpad <= (int64_t(64) << 20) ? BIN_G64 : BIN_G8;
+    if (g->code_lbin_env == BIN_G64 || g->code_lbin_env == BIN_G8) g->code_lbin = g->code_lbin_env;
     for (int b = 0; b < g->code_lbin; ++b) g->code_pcut += g->bin_arcs[b];
     LPA_TRY(dev_alloc(g, (void**)&g->code2, sizeof(uint32_t) * (size_t)(g->vpad / 16)));
     LPA_TRY(dev_alloc(g, (void**)&g->al2, sizeof(uint32_t) * (size_t)(((g->code_pcut + 511) / 512 * 512 + 512) / 16)));
@@ -752,6 +756,17 @@ int build_graph(lpa_graph* g, const int32_t* src, const int32_t* dst, int64_t m,
   g->slice = ((int64_t)V + P - 1) / P;
   g->slice = (g->slice + 63) / 64 * 64;  // vector-aligned slices (k_diff reads int4)
   if (g->slice == 0) g->slice = 64;
+  // P > 1 (a power of two): power-of-two slices, the tail of each padded with isolated
+  // slots, so that the rank-strided LDS hot-set rebuild and the giant codes apply
+  // (rebuild_ranked): C5 over 8 ranks has 5 M vertices per slice, which otherwise took the
+  // plain labels-mode rebuild in every refresh.  The padding costs only label-vector
+  // bytes (C5: 160 -> 256 MB per replica) in the vector-sized passes (diff, full exchange).
+  // LPA_POW2_SLICES=0: the tight slices.
+  if (P > 1 && (P & (P - 1)) == 0 && g->rebuild_hot && g->pow2_slices) {
+    int64_t np2 = 64;
+    while (np2 < g->slice) np2 *= 2;
+    if (np2 * P <= (int64_t(1) << 30)) g->slice = np2;
+  }
   g->vpad = g->slice * P;
   g->own_begin = (int64_t)r * g->slice;
   const int64_t S = g->slice;

@@ -1,6 +1,7 @@
 // C ABI of liblpa_hip.so (include/lpa.h).  Handle lifetime, argument checks,
 // error reporting, RCCL communicator setup.
 #include <stdarg.h>
+#include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -102,6 +103,7 @@ void destroy(lpa_graph* g) {
       if (e) (void)hipEventDestroy(e);
   }
   if (g->host_pin) (void)hipHostFree(g->host_pin);
+  if (g->hc_buf) (void)hipHostFree(g->hc_buf);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   if (g->own_stream) (void)hipStreamDestroy(g->own_stream);
   delete g;
@@ -142,7 +144,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
                   int64_t m, int32_t V, uint32_t flags, int32_t rank, int32_t nranks,
                   const uint8_t* comm_id, Loopback* loop, lpa_graph** out,
                   const lpa_graph* borrow = nullptr, const lpa_graph* l2_parent = nullptr,
-                  const int32_t* l2_labels = nullptr, const uint8_t* l2_marks = nullptr) {
+                  const int32_t* l2_labels = nullptr, const uint8_t* l2_marks = nullptr,
+                  lpa_allgather_fn hc_fn = nullptr, void* hc_ctx = nullptr) {
   if (!out) {
     set_error("out must be non-null");
     return LPA_EINVAL;
@@ -169,6 +172,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_GRAPHS")) g->use_graphs = atoi(f);
   if (const char* f = getenv("LPA_FRONTIER")) g->frontier = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FIRST_RUNS")) g->first_runs = atoi(f) ? 1 : 0;
+  if (const char* f = getenv("LPA_CODE_LBIN")) g->code_lbin_env = atoi(f);
+  if (const char* f = getenv("LPA_POW2_SLICES")) g->pow2_slices = atoi(f) ? 1 : 0;
   // internal builds (the outlier stage's L2 sub-graph): the locality order is a
   // gather-locality heuristic worth its two atomic passes only on a graph that runs
   // many supersteps; labels do not depend on the vertex order
@@ -176,6 +181,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   g->pooled = (flags & kFlagPooled) && stream != nullptr;
   g->rank = rank;
   g->nranks = nranks;
+  g->hc_fn = hc_fn;
+  g->hc_ctx = hc_ctx;
   if (stream) {
     g->stream = stream;
   } else {
@@ -292,6 +299,17 @@ int lpa_graph_create_loopback(const int32_t* src, const int32_t* dst, int64_t m,
                        out);
 }
 
+int lpa_graph_create_hostcoll(const int32_t* src, const int32_t* dst, int64_t m, int32_t V, int32_t device,
+                              uint32_t flags, int32_t rank, int32_t nranks, lpa_allgather_fn allgather, void* ctx,
+                              lpa_graph** out) {
+  if (!allgather) {
+    set_error("lpa_graph_create_hostcoll: null allgather function");
+    return LPA_EINVAL;
+  }
+  return create_common(device, nullptr, src, dst, m, V, flags, rank, nranks, nullptr, nullptr, out, nullptr,
+                       nullptr, nullptr, nullptr, allgather, ctx);
+}
+
 int lpa_exchange_get(lpa_graph* g, int32_t* slice_out) {
   if (!g || !slice_out) {
     set_error("null handle or output");
@@ -313,7 +331,7 @@ int lpa_exchange_put(lpa_graph* g, const int32_t* full_in) {
   LPA_HIP(hipMemcpyAsync(g->lab[g->cur], full_in, sizeof(int32_t) * g->vpad, hipMemcpyHostToDevice,
                          g->stream));
   g->prev_delta_ok = false;
-  LPA_TRY(rebuild_arc_labels(g));
+  LPA_TRY(refresh_after_put(g));
   g->al_pending = false;
   LPA_TRY(frontier_all(g, g->par));
   LPA_HIP(hipStreamSynchronize(g->stream));
@@ -550,11 +568,11 @@ int lpa_degrees(lpa_graph* g, int32_t* deg_out) {
   return LPA_OK;
 }
 
-int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
-  if (!g || !info) {
-    set_error("null handle or info");
-    return LPA_EINVAL;
-  }
+}  // extern "C"
+
+namespace {
+// every field of this header's lpa_graph_info
+int fill_info(const lpa_graph* g, lpa_graph_info* info) {
   memset(info, 0, sizeof(*info));
   info->V = g->V;
   info->m = g->m;
@@ -581,7 +599,9 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   info->exchanges_posted = g->n_exch_posted;
   info->exchanges_post_missed = g->n_exch_post_missed;
   info->gather_mode = g->gather ? 1 : 0;
+  info->host_allgathers = g->n_host_allgathers;
   if (g->code_ok && g->gword) {
+    LPA_HIP(hipSetDevice(g->device));
     int32_t w = 0;
     LPA_HIP(hipMemcpyAsync(&w, g->gword + 5, sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));
     LPA_HIP(hipStreamSynchronize(g->stream));
@@ -589,16 +609,35 @@ int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
   }
   return LPA_OK;
 }
+}  // namespace
+
+extern "C" {
+
+// the unsized form is frozen at the ABI-5 struct (the fields up to blocked_pieces): a
+// caller compiled against that header passes a struct of that size
+int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info) {
+  if (!g || !info) {
+    set_error("null handle or info");
+    return LPA_EINVAL;
+  }
+  lpa_graph_info full;
+  LPA_TRY(fill_info(g, &full));
+  memcpy(info, &full, offsetof(lpa_graph_info, code_refresh));
+  return LPA_OK;
+}
 
 int lpa_abi_version(void) { return LPA_ABI_VERSION; }
 
 int lpa_graph_get_info_sized(const lpa_graph* g, lpa_graph_info* info, int64_t info_size) {
-  if (!info || info_size < 0) {
-    set_error("null info or negative size");
+  if (!g || !info || info_size < 0) {
+    set_error("null handle, null info or negative size");
     return LPA_EINVAL;
   }
   lpa_graph_info full;
-  LPA_TRY(lpa_graph_get_info(g, &full));
+  LPA_TRY(fill_info(g, &full));
+  // a caller's struct from a later header: the fields this library does not know read 0
+  if (info_size > (int64_t)sizeof(full)) memset(reinterpret_cast<char*>(info) + sizeof(full), 0,
+                                                (size_t)info_size - sizeof(full));
   memcpy(info, &full, (size_t)(info_size < (int64_t)sizeof(full) ? info_size : (int64_t)sizeof(full)));
   return LPA_OK;
 }

@@ -14,6 +14,11 @@
 //             This runs the library's exchange control flow -- dense/delta switch,
 //             host count read, in-place allgather offsets, delta chain -- on a
 //             one-GPU box, where RCCL refuses two ranks on one device.
+//   host      (round 6) the caller's host function (lpa_graph_create_hostcoll): the
+//             send bytes are staged to pinned host memory, the function gathers every
+//             rank's bytes in rank order (torch.distributed gloo, MPI, a Spark barrier
+//             stage ...), the result is copied back -- the library's exchange schedule,
+//             every form included, across real process boundaries without RCCL.
 #include <condition_variable>
 #include <chrono>
 #include <mutex>
@@ -170,9 +175,38 @@ int loop_allgather(lpa_graph* g, const void* send, void* recv, size_t bytes, hip
   return LPA_OK;
 }
 
+// The host collective: stream-ordered up to the staging copies, synchronous around the
+// caller's function (it runs on this host thread; the staging buffer is reused by the
+// next allgather, so the copy back completes before returning)
+int host_allgather(lpa_graph* g, const void* send, void* recv, size_t bytes, hipStream_t s) {
+  const int P = g->nranks;
+  const size_t need = bytes * (size_t)(P + 1) > 0 ? bytes * (size_t)(P + 1) : 1;
+  if (g->hc_bytes < need) {
+    if (g->hc_buf) LPA_HIP(hipHostFree(g->hc_buf));
+    g->hc_buf = nullptr;
+    g->hc_bytes = 0;
+    LPA_HIP(hipHostMalloc(&g->hc_buf, need, hipHostMallocDefault));
+    g->hc_bytes = need;
+  }
+  char* hs = static_cast<char*>(g->hc_buf);
+  char* hr = hs + bytes;
+  if (bytes > 0) LPA_HIP(hipMemcpyAsync(hs, send, bytes, hipMemcpyDeviceToHost, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  const int rc = g->hc_fn(hs, hr, (int64_t)bytes, g->hc_ctx);
+  if (rc != 0) {
+    set_error("host allgather function failed (returned %d) on rank %d, %zu bytes per rank", rc, g->rank, bytes);
+    return LPA_ERCCL;
+  }
+  ++g->n_host_allgathers;
+  if (bytes > 0) LPA_HIP(hipMemcpyAsync(recv, hr, bytes * (size_t)P, hipMemcpyHostToDevice, s));
+  LPA_HIP(hipStreamSynchronize(s));
+  return LPA_OK;
+}
+
 }  // namespace
 
 int coll_allgather(lpa_graph* g, const void* send, void* recv, size_t count, int elem, hipStream_t s) {
+  if (g->hc_fn) return host_allgather(g, send, recv, count * (size_t)elem, s);
   if (g->loop) {
     int rc = loop_allgather(g, send, recv, count * (size_t)elem, s);
     if (rc != LPA_OK && g->loop) g->loop->abort();

@@ -95,6 +95,7 @@ __global__ __launch_bounds__(256) void k_delta_compact(const int32_t* __restrict
 // slice; it writes no bitmap then and marks the giant form unavailable (a giant count
 // above any capacity in xpair[1]).
 constexpr int kCompactWords = 8;
+constexpr int kTriple = 3;   // per-rank words of the count exchange: delta, giant, posted request
 constexpr unsigned long long kNoGiantForm = 1ull << 62;
 struct ListBounds {
   int64_t b[LPA_NBINS + 1];
@@ -107,9 +108,13 @@ __global__ __launch_bounds__(256) void k_exch_compact(const int32_t* __restrict_
                                                       unsigned long long* __restrict__ bm_own,
                                                       const int32_t* __restrict__ flist,
                                                       const int32_t* __restrict__ fcnt,
-                                                      const int32_t* __restrict__ fr_all, ListBounds lb) {
+                                                      const int32_t* __restrict__ fr_all, ListBounds lb,
+                                                      long long post_req) {
   const int lane = threadIdx.x & 63;
   const u64 lt = (1ull << lane) - 1ull;
+  // this rank's posted-capacity request (lpa_set_posted) rides in the count triple, so
+  // every rank derives the next posted capacity from the same gathered values
+  if (blockIdx.x == 0 && threadIdx.x == 0) xpair[2] = (unsigned long long)post_req;
   if (flist != nullptr && *fr_all == 0 && fcnt[kFcntSettled] == 0) {   // uniform
     if (blockIdx.x == 0 && threadIdx.x == 0) xpair[1] = kNoGiantForm;
     int64_t total = 0;
@@ -307,8 +312,8 @@ int exchange_alloc(lpa_graph* g) {
   LPA_TRY(dev_alloc(g, (void**)&g->dcount, sizeof(unsigned long long) * (1 + P)));
   LPA_TRY(dev_alloc(g, (void**)&g->gsend, sizeof(u64) * g->slice));
   LPA_TRY(dev_alloc(g, (void**)&g->gbm, sizeof(unsigned long long) * (g->slice / 64) * P));
-  LPA_TRY(dev_alloc(g, (void**)&g->xpair, sizeof(unsigned long long) * (2 + 2 * P)));
-  LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * 2 * P, hipHostMallocDefault));
+  LPA_TRY(dev_alloc(g, (void**)&g->xpair, sizeof(unsigned long long) * kTriple * (1 + P)));
+  LPA_HIP(hipHostMalloc((void**)&g->h_dcounts, sizeof(unsigned long long) * kTriple * P, hipHostMallocDefault));
   LPA_HIP(hipEventCreateWithFlags(&g->cnt_ev, hipEventDisableTiming));
   g->prev_delta_ok = false;
   return LPA_OK;
@@ -370,6 +375,18 @@ static int64_t posted_cap(const lpa_graph* g, int64_t capd) {
   while (c < 2 * capd) c *= 2;
   return c <= kPostMax && c <= g->dcap ? c : 0;
 }
+// ... agreed over the ranks: every rank's request (its lpa_set_posted value, gathered
+// with the counts: < 0 adaptive, 0 off, > 0 fixed) gives a capacity, the smallest wins.
+// Computed from gathered values only, so every rank posts the same allgather size even
+// when one rank alone calls lpa_set_posted, or calls it with another value
+static int64_t agreed_post_cap(const lpa_graph* g, int64_t capd) {
+  int64_t c = INT64_MAX;
+  for (int k = 0; k < g->nranks; ++k) {
+    const int64_t req = (int64_t)g->h_dcounts[kTriple * k + 2];
+    c = std::min(c, req < 0 ? posted_cap(g, capd) : std::min(req, g->dcap));
+  }
+  return c == INT64_MAX ? 0 : c;
+}
 
 // In-library exchange of one superstep (P > 1, RCCL communicator or loopback group):
 // Lown = Ln + own_begin holds the new owned labels; on return Ln holds the full new
@@ -382,7 +399,7 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
   const int64_t S = g->slice, wpr = S / 64;   // bitmap words per rank
   *changes_listed = false;
   if (!first) {
-    LPA_HIP(hipMemsetAsync(g->xpair, 0, 2 * sizeof(unsigned long long), s));
+    LPA_HIP(hipMemsetAsync(g->xpair, 0, 2 * sizeof(unsigned long long), s));   // [2]: the kernel
     // converged supersteps: the frontier lists of this superstep's tally (g->par)
     const bool list_mode = g->since_reset >= kDenseSupersteps + 2;
     ListBounds lbd;
@@ -390,35 +407,36 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
     hipLaunchKernelGGL(k_exch_compact, dim3(grid_of(S / kCompactWords, 4096)), dim3(256), 0, s, Lc + g->own_begin,
                        Lown, S,
                        g->gword, g->dsend, g->gsend, g->xpair, g->gbm + (int64_t)g->rank * wpr,
-                       list_mode ? g->flist : (const int32_t*)nullptr, g->fcnt + 16 * g->par, g->fr_all + g->par, lbd);
+                       list_mode ? g->flist : (const int32_t*)nullptr, g->fcnt + 16 * g->par, g->fr_all + g->par, lbd,
+                       (long long)g->post_fixed);
     LPA_HIP(hipGetLastError());
-    LPA_TRY(coll_allgather(g, g->xpair, g->xpair + 2, 2, 8, s));
-    const unsigned long long* pairs = g->xpair + 2;   // rank r: (delta, giant) counts at 2r, 2r + 1
-    LPA_HIP(hipMemcpyAsync(g->h_dcounts, pairs, sizeof(unsigned long long) * 2 * P, hipMemcpyDeviceToHost, s));
+    LPA_TRY(coll_allgather(g, g->xpair, g->xpair + kTriple, kTriple, 8, s));
+    // rank r: (delta count, giant count, posted request) at 3r, 3r + 1, 3r + 2
+    const unsigned long long* pairs = g->xpair + kTriple;
+    LPA_HIP(hipMemcpyAsync(g->h_dcounts, pairs, sizeof(unsigned long long) * kTriple * P, hipMemcpyDeviceToHost, s));
     LPA_HIP(hipEventRecord(g->cnt_ev, s));
     // Posted delta (converged supersteps, after a delta exchange of few entries): the
-    // entries go out at a capacity fixed from the last counts (the same on every rank),
-    // and their apply + the refresh's change chunks are queued behind them BEFORE the
-    // host waits for the counts, so the GPU keeps working through the host's read.  A
-    // count above the capacity makes the queued kernel stand down; the host then sees
-    // the same counts and exchanges again below in the form that fits.
-    const int64_t post = !g->prev_delta_ok      ? 0
-                         : g->post_fixed < 0    ? g->post_cap
-                                                : std::min(g->post_fixed, g->dcap);
+    // entries go out at a capacity fixed from the last counts and requests (the same on
+    // every rank: agreed_post_cap), and their apply + the refresh's change chunks are
+    // queued behind them BEFORE the host waits for the counts, so the GPU keeps working
+    // through the host's read.  A count above the capacity makes the queued kernel stand
+    // down; the host then sees the same counts and exchanges again below in the form that
+    // fits.
+    const int64_t post = g->prev_delta_ok ? g->post_cap : 0;
     if (post > 0) {
       LPA_TRY(coll_allgather(g, g->dsend, exchange_recv_buf(g), (size_t)post, 8, s));
-      LPA_TRY(exchange_finish_delta(g, const_cast<int32_t*>(Lc), Ln, post, g->par, pairs, 2, true));
+      LPA_TRY(exchange_finish_delta(g, const_cast<int32_t*>(Lc), Ln, post, g->par, pairs, kTriple, true));
     }
     LPA_HIP(hipEventSynchronize(g->cnt_ev));
     int64_t capd = 0, capg = 0;
     for (int k = 0; k < P; ++k) {
-      capd = std::max(capd, (int64_t)g->h_dcounts[2 * k]);
-      capg = std::max(capg, (int64_t)g->h_dcounts[2 * k + 1]);
+      capd = std::max(capd, (int64_t)g->h_dcounts[kTriple * k]);
+      capg = std::max(capg, (int64_t)g->h_dcounts[kTriple * k + 1]);
     }
     if (post > 0) {
       if (capd <= post) {
         g->last_exchange_delta = capd;
-        g->post_cap = posted_cap(g, capd);
+        g->post_cap = agreed_post_cap(g, capd);
         ++g->n_exch_delta;
         ++g->n_exch_posted;
         *changes_listed = true;
@@ -433,10 +451,10 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
     if (delta_b <= giant_b && delta_b < full_b) {
       if (capd > 0) LPA_TRY(coll_allgather(g, g->dsend, exchange_recv_buf(g), (size_t)capd, 8, s));
       g->last_exchange_delta = capd;
-      g->post_cap = posted_cap(g, capd);
+      g->post_cap = agreed_post_cap(g, capd);
       ++g->n_exch_delta;
       *changes_listed = true;
-      return exchange_finish_delta(g, const_cast<int32_t*>(Lc), Ln, capd, g->par, pairs, 2);
+      return exchange_finish_delta(g, const_cast<int32_t*>(Lc), Ln, capd, g->par, pairs, kTriple);
     }
     if (giant_b < full_b) {
       // in place: rank r's bitmap words at gbm + r * wpr
@@ -448,7 +466,7 @@ int exchange_collective(lpa_graph* g, const int32_t* Lc, int32_t* Ln, bool first
                          g->gbm, n4, g->own_begin / 4, (g->own_begin + S) / 4, g->gword);
       LPA_HIP(hipGetLastError());
       if (capg > 0) {
-        hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(capg * P, 8192)), dim3(256), 0, s, ent, pairs + 1, 2, capg,
+        hipLaunchKernelGGL(k_delta_apply, dim3(grid_of(capg * P, 8192)), dim3(256), 0, s, ent, pairs + 1, kTriple, capg,
                            P, g->rank, S, Ln);
         LPA_HIP(hipGetLastError());
       }

@@ -850,6 +850,9 @@ __global__ __launch_bounds__(64 * kW) void k_hub_mid_all(const int32_t* __restri
 // The producer side leans on gfx950 behaviour (device atomics on hipMalloc memory
 // complete at the memory side once vmcnt drains), so the library is built for gfx950
 // only:
+#ifndef LPA_HUB_RELEASE
+#define LPA_HUB_RELEASE 0
+#endif
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "lpa_hub.hip: the fused last-block hand-off is validated on gfx950 only"
 #endif
@@ -867,9 +870,19 @@ __device__ __forceinline__ bool last_block(uint32_t* tk) {
     uint32_t* t1 = tk + gi * kTicketStride;
     uint32_t* t2 = tk + kTicketGroups * kTicketStride;
     last = 0;
-    if (__hip_atomic_fetch_add(t1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1) {
+    // LPA_HUB_RELEASE (A/B build): the tickets as agent-scope acq_rel RMWs -- the C++ /
+    // HSA-model form (every block's ticket a release, each winner an acquire).  gfx950
+    // lowers each release to `buffer_wbl2 sc1; s_waitcnt vmcnt(0)` before the atomic
+    // (hipcc -S, round 6): a write-back of this XCD's dirty L2 lines, none of which hold
+    // hand-off data
+#if LPA_HUB_RELEASE
+    constexpr int kTicketOrder = __ATOMIC_ACQ_REL;
+#else
+    constexpr int kTicketOrder = __ATOMIC_RELAXED;
+#endif
+    if (__hip_atomic_fetch_add(t1, 1u, kTicketOrder, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1) {
       __hip_atomic_store(t1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (__hip_atomic_fetch_add(t2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+      if (__hip_atomic_fetch_add(t2, 1u, kTicketOrder, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
         __hip_atomic_store(t2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the winner alone acquires at agent scope (one block per launch, not every
         // ticket): gfx950 emits `buffer_inv sc1` -- the CU's vector L1 and this XCD's

@@ -133,12 +133,21 @@ struct lpa_graph {
   // each); neither = the caller-driven exchange (lpa_exchange_get/put)
   ncclComm_t comm = nullptr;
   lpa::Loopback* loop = nullptr;
+  // host-staged collective (lpa_graph_create_hostcoll): each allgather is handed to the
+  // caller's host function (MPI, torch.distributed gloo, a Spark barrier stage ...),
+  // staged through a pinned host buffer (hc_buf: send + nranks * recv bytes, grown on use)
+  lpa_allgather_fn hc_fn = nullptr;
+  void* hc_ctx = nullptr;
+  void* hc_buf = nullptr;
+  size_t hc_bytes = 0;
+  int64_t n_host_allgathers = 0;               // allgathers served by hc_fn (lpa_graph_info)
   hipEvent_t loop_ev[2] = {nullptr, nullptr};  // loopback: send-ready / copies-done marks
   int64_t n_exch_full = 0, n_exch_delta = 0;   // exchanges by mode (lpa_graph_info)
   int64_t n_graph_replays = 0;                 // supersteps replayed from a captured graph
 
   int64_t V = 0, m = 0;
-  int64_t slice = 0;      // vertex slots per rank
+  int64_t slice = 0;      // vertex slots per rank (P > 1: a power of two, lpa_build)
+  int pow2_slices = 1;    // LPA_POW2_SLICES=0: tight slices (ceil(V / P) rounded to 64)
   int64_t vpad = 0;       // nranks * slice
   int64_t own_begin = 0;  // rank * slice
   int64_t n_own = 0;      // real (non-padding) vertices owned
@@ -235,18 +244,23 @@ struct lpa_graph {
                                 //     giant-bit count (k_giant_bits), [4] superstep 4 bins: 0 = lists,
                                 //     [5] giant-code refresh taken (superstep 2 settles from al2),
                                 //     [6] superstep 2's wave bins: 0 = lists of the unsettled rows
-  // giant codes (round 5, lpa_iter.hip "Giant codes"): the refresh after superstep 1 on
-  // a single GPU, when one label G carries the hubs but not half the hot slots (R-MAT),
-  // writes a 1-byte code per arc instead of al[] (code 0 = G, else an 8-bit label hash)
-  // for the rows of > 8 arcs, and al[] only for the positions of the rows of <= 8
-  bool code_ok = false;         // the handle can take that refresh (P = 1, hot-set rebuild)
+  // giant codes (round 5, lpa_iter.hip "Giant codes"): the refresh after superstep 1 (or
+  // 2), when one label G carries the hubs but not half the hot slots (R-MAT), writes a
+  // 2-bit code per arc instead of al[] (code 0 = G, else 1 + a label hash mod 3; 16 arcs
+  // to a word of al2) for the rows above the cut (code_lbin), and al[] only for the
+  // positions of the rows below it.  Round 6: every rank of a partitioned job too (G is
+  // picked from the replicated vector, the same on every rank; each rank codes its own arcs)
+  bool code_ok = false;         // the handle can take that refresh (the LDS hot-set rebuild:
+                                //   P = 1, or P > 1 with power-of-two slices, rebuild_ranked)
   uint32_t* code2 = nullptr;    // [vpad / 16] 2-bit code of every slot's label (16 per word)
   uint32_t* al2 = nullptr;      // [(code_pcut rounded up to 512 + 512) / 16] 2-bit code of every
                                 //   arc's column label (arc i: word i / 16, bits 2 (i % 16))
   bool gather = false;          // gather mode: supersteps 1..kGatherSteps tally from L[col[i]] with
                                 //   no al[] refresh; the last of them rebuilds al (lpa_build)
   int32_t code_lbin = lpa::BIN_G8;   // first bin whose rows keep their labels in a code refresh
-                                //   (lpa_build: g64 when the label vector is <= 64 MB, else g8)
+                                //   (lpa_build: g64 when the label vector is <= 64 MB, else g8;
+                                //   LPA_CODE_LBIN=5|8 forces either, for tests)
+  int32_t code_lbin_env = -1;   // LPA_CODE_LBIN at create time (-1: by size)
   int64_t code_pcut = 0;        // its first arc position
   bool code3 = false;           // superstep 3 follows a giant-code refresh (read by the host
                                 //   before it: its schedule differs, see run_supersteps)
@@ -290,19 +304,22 @@ struct lpa_graph {
   lpa::u64* dsend = nullptr;                 // [slice] this rank's (slot << 32 | label)
   lpa::u64* drecv = nullptr;                 // [nranks * dcap] gathered deltas
   unsigned long long* dcount = nullptr;      // [1 + nranks] own count, then every rank's (caller-driven)
-  unsigned long long* h_dcounts = nullptr;   // [2 nranks] pinned host copy of the count pairs
+  unsigned long long* h_dcounts = nullptr;   // [3 nranks] pinned host copy of the count triples
   // giant-compressed exchange (lpa_exchange.hip): the giant-label bitmap of every slice
   // ([nranks][slice / 64] words, own slice in place) and the changed non-G entries
   lpa::u64* gsend = nullptr;                 // [slice] this rank's changed non-G (slot << 32 | label)
   unsigned long long* gbm = nullptr;         // [nranks * slice / 64] bit = (label == G)
-  unsigned long long* xpair = nullptr;       // [2 + 2 nranks] own (delta, giant) counts, then every rank's
+  unsigned long long* xpair = nullptr;       // [3 + 3 nranks] own (delta count, giant count, posted
+                                             //   request), then every rank's
   int64_t n_exch_giant = 0;                  // exchanges done in the giant-compressed form
   int64_t dcap = 0;                          // delta entries per rank (slice / 4)
   int64_t last_exchange_delta = -1;          // entries per rank of the last exchange (-1 full)
   bool prev_delta_ok = false;                // the last exchange was a delta: the two label
                                              //   buffers agree outside the own slice
-  int64_t post_cap = 0;                      // posted delta capacity of the next exchange (0: none)
-  int64_t post_fixed = -1;                   // lpa_set_posted: -1 adaptive (post_cap), 0 off, > 0 fixed
+  int64_t post_cap = 0;                      // posted delta capacity of the next exchange (0: none),
+                                             //   agreed over the ranks from the gathered triples
+  int64_t post_fixed = -1;                   // lpa_set_posted: this rank's request, -1 adaptive, 0 off,
+                                             //   > 0 fixed (the smallest capacity requested wins)
   int64_t n_exch_posted = 0;                 // delta exchanges that went out before the count read
   int64_t n_exch_post_missed = 0;            // posted exchanges whose counts exceeded the capacity
   hipEvent_t cnt_ev = nullptr;               // the count pairs reached h_dcounts
@@ -379,6 +396,18 @@ int launch_hub_decide(lpa_graph* g, int32_t* Lown, int64_t h_end, const int32_t*
 bool block_mode_now(const lpa_graph* g);  // lpa_iter.hip
 int64_t block_rows_begin(const lpa_graph* g);  // first row of the block tiers (lpa_iter.hip)
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
+// the caller-driven full exchange (lpa_exchange_put) completes the superstep just run:
+// its refresh rebuilds every arc label, and may take the giant codes as the in-library
+// refresh of that superstep would
+int refresh_after_put(lpa_graph* g);
+// P > 1: the LDS hot-set rebuild's rank-strided form applies (power-of-two rank count and
+// slice, each slice holding its share of the kHotRankedLabels hottest labels)
+constexpr int kHotRankedLabels = 32768;
+inline bool rebuild_ranked(const lpa_graph* g) {
+  const auto pow2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
+  return g->nranks > 1 && pow2(g->nranks) && pow2(g->slice) && g->nranks <= kHotRankedLabels &&
+         g->slice >= kHotRankedLabels / g->nranks;
+}
 int ensure_al(lpa_graph* g);           // al valid (copies al0 after a lazy reset)
 int frontier_all(lpa_graph* g, int par);  // next tally of parity `par` takes every row
 
@@ -391,11 +420,13 @@ int gather_labels(lpa_graph* g, int32_t* out_dense_dev);
 // collective backend (lpa_comm.cpp): allgather of `count` elements of `elem` bytes
 // per rank in rank order (in place when send == recv + rank * count * elem),
 // stream-ordered on s, on the handle's RCCL communicator or loopback group
-inline bool has_collective(const lpa_graph* g) { return g->comm != nullptr || g->loop != nullptr; }
-// the superstep has a label-exchange step: P > 1, or an RCCL communicator at any P (a
-// one-rank job of the distributed path runs the same exchange code, ncclAllGather of
-// one rank included)
-inline bool exchanges(const lpa_graph* g) { return g->nranks > 1 || g->comm != nullptr; }
+inline bool has_collective(const lpa_graph* g) {
+  return g->comm != nullptr || g->loop != nullptr || g->hc_fn != nullptr;
+}
+// the superstep has a label-exchange step: P > 1, or an RCCL communicator / host
+// collective at any P (a one-rank job of the distributed path runs the same exchange
+// code, its allgather of one rank included)
+inline bool exchanges(const lpa_graph* g) { return g->nranks > 1 || g->comm != nullptr || g->hc_fn != nullptr; }
 int coll_allgather(lpa_graph* g, const void* send, void* recv, size_t count, int elem, hipStream_t s);
 int loopback_attach(lpa_graph* g, Loopback* lb);  // registers the handle's rank slot
 int loopback_ranks(const Loopback* lb);

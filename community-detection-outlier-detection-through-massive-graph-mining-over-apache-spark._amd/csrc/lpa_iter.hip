@@ -44,6 +44,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "lpa_internal.h"
@@ -2153,7 +2154,7 @@ __global__ __launch_bounds__(256) void k_al_rebuild(const unsigned long long* __
 // own label is not (Chung-Lu superstep 2: the mode holds 43 % of the arcs' columns, the
 // top hub's label 0.3 %).  One block, a 2K-slot LDS table.  The choice of G only
 // affects speed: every use of it is exact for any G.
-constexpr int kHotLabels = 32768;          // rank-strided label set (P > 1: power-of-two shares)
+constexpr int kHotLabels = kHotRankedLabels;  // rank-strided label set (P > 1: power-of-two shares)
 constexpr int kHotLabelsSingle = 40960;    // P = 1: the whole 160 KB of LDS
 // bits mode: 1,310,688 slots' bits (the last LDS word counts the set bits first)
 constexpr int64_t kHotBits = 32ll * (kHotLabelsSingle - 1);
@@ -2187,12 +2188,16 @@ __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__
 
 // (abits / nzero: the class-blocked rebuild that follows ORs the arc giant bits of its
 // pieces into abits[0, nzero): zeroed here, one launch ahead)
+// gword[3] counts the set bits of the hot slots, slot i with (i & hmask) < hlim: the first
+// kHotBits slots at P = 1 (hmask all ones), the first hlim slots of every slice of a
+// rank-strided vector (hmask = slice - 1) -- the degree-ranked top set either way
 template <bool kIfWanted>
 __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __restrict__ counters, int64_t thr,
                                                     const int32_t* __restrict__ L, int64_t n,
                                                     int32_t* __restrict__ gword,
                                                     unsigned long long* __restrict__ bits,
-                                                    unsigned long long* __restrict__ abits, int64_t nzero) {
+                                                    unsigned long long* __restrict__ abits, int64_t nzero,
+                                                    uint64_t hmask, int64_t hlim) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += (int64_t)gridDim.x * blockDim.x)
     abits[i] = 0ull;
@@ -2213,9 +2218,12 @@ __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __
       if (lane == k) mine = m;
     }
     if (lane < 8 && g0 + lane * 64 < n) bits[(g0 >> 6) + lane] = mine;
-    // the hot slots' set bits (the rebuild's bits-mode test without an LDS fill)
-    if (g0 < kHotBits) {
-      const u32 c = wave_sum_u32(lane < 8 && g0 + lane * 64 < kHotBits ? (u32)__popcll(mine) : 0u);
+    // the hot slots' set bits (the rebuild's bits-mode test without an LDS fill); hlim
+    // and the slice are multiples of 64, so a bit word is hot or cold as a whole
+    const int64_t wi = g0 + lane * 64;
+    const bool hot = lane < 8 && wi < n && (int64_t)((uint64_t)wi & hmask) < hlim;
+    if (__ballot(hot)) {
+      const u32 c = wave_sum_u32(hot ? (u32)__popcll(mine) : 0u);
       if (lane == 0 && c) atomicAdd(&gword[3], (int32_t)c);
     }
   }
@@ -2795,24 +2803,49 @@ __device__ __forceinline__ void range_pipe(P1 p1, P2 p2, St st, const int32_t* _
 // hottest labels in LDS, then the codes, with the 655,360 hottest slots' codes in LDS --
 // the gathers are bound by their lane count, not their bytes, so the LDS share is the
 // lever -- and the others from the 2-bit code array (vpad / 4 bytes: L2-resident at C3).
+// kRanked (a partitioned job's rank, round 6): the hot sets are the first 2^hot_lg labels
+// and the first 2^hc_lg codes of EVERY slice (degree rank k lives at slot (k mod P) S +
+// k / P, so these are the global top degree ranks), at LDS index (c / S) H + c mod S as in
+// k_al_rebuild_hot's ranked form; at P = 1 they are the first slots.
+template <bool kRanked>
 __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict__ gword,
                                                        const int32_t* __restrict__ col, int64_t arcs,
                                                        const int32_t* __restrict__ Ln, int64_t nslots,
                                                        const uint32_t* __restrict__ code2, int64_t p64,
-                                                       uint32_t* __restrict__ al2, int32_t* __restrict__ al) {
+                                                       uint32_t* __restrict__ al2, int32_t* __restrict__ al,
+                                                       int slice_lg, int hot_lg, int hc_lg) {
   if (gword[5] == 0) return;
   __shared__ u32 hot[kHotLabelsSingle];
   const u32 G = (u32)gword[0];
   const int lane = threadIdx.x & 63;
   const int64_t nfull = arcs >> 9;
   const int64_t bA = min((p64 + 511) >> 9, nfull), bB = p64 >> 9;
+  const u32 smask = kRanked ? (1u << slice_lg) - 1u : 0u;
+  // slot c -> its hot-set index (h: whether it has one) for a set of 2^lg per slice
+  auto hot_at = [&](int c, int lg, u32 nflat, bool& h) -> u32 {
+    if constexpr (kRanked) {
+      const u32 j = (u32)c & smask;
+      h = j < (1u << lg);
+      return (((u32)c >> slice_lg) << lg) + j;
+    } else {
+      h = (u32)c < nflat;
+      return (u32)c;
+    }
+  };
   // ---- the labels of the rows below the cut ----
-  const u32 nh = (u32)(nslots < kHotLabelsSingle ? nslots : kHotLabelsSingle);
-  for (u32 i = threadIdx.x; i < nh; i += 1024) hot[i] = (u32)Ln[i];
+  const u32 nh = kRanked ? (u32)((nslots >> slice_lg) << hot_lg)
+                         : (u32)(nslots < kHotLabelsSingle ? nslots : kHotLabelsSingle);
+  for (u32 i = threadIdx.x; i < nh; i += 1024)
+    hot[i] = (u32)Ln[kRanked ? ((int64_t)(i >> hot_lg) << slice_lg) + (i & ((1u << hot_lg) - 1u)) : (int64_t)i];
   __syncthreads();
-  range_pipe([&](int c) -> u32 { return hot[(u32)c < nh ? (u32)c : nh - 1u]; },
+  range_pipe([&](int c) -> u32 {
+               bool h;
+               const u32 k = hot_at(c, hot_lg, nh, h);
+               return hot[h ? k : nh - 1u];
+             },
              [&](int c, u32 w) -> int32_t {
-               const bool h = (u32)c < nh;
+               bool h;
+               (void)hot_at(c, hot_lg, nh, h);
                const int32_t x = Ln[h ? 0 : c];
                return h ? (int32_t)w : x;
              },
@@ -2823,15 +2856,22 @@ __global__ __launch_bounds__(1024) void k_code_rebuild(const int32_t* __restrict
              col, bB, nfull);
   // ---- the codes of the rows above ----
   __syncthreads();
-  const u32 nc = (u32)(nslots < 16 * kHotLabelsSingle ? nslots : 16 * kHotLabelsSingle);  // a multiple of 16
-  for (u32 q = threadIdx.x; q < nc / 16; q += 1024) hot[q] = code2[q];
+  // (a multiple of 16 either way: ranked, 2^hc_lg >= 16 codes per slice)
+  const u32 nc = kRanked ? (u32)((nslots >> slice_lg) << hc_lg)
+                         : (u32)(nslots < 16 * kHotLabelsSingle ? nslots : 16 * kHotLabelsSingle);
+  for (u32 q = threadIdx.x; q < nc / 16; q += 1024)
+    hot[q] = code2[kRanked ? ((int64_t)(q >> (hc_lg - 4)) << (slice_lg - 4)) + (q & ((1u << (hc_lg - 4)) - 1u))
+                           : (int64_t)q];
   __syncthreads();
   auto cp1 = [&](int c) -> u32 {
-    const u32 cc = (u32)c < nc ? (u32)c : nc - 1u;
-    return (hot[cc >> 4] >> ((cc & 15u) * 2u)) & 3u;
+    bool h;
+    const u32 k = hot_at(c, hc_lg, nc, h);
+    const u32 cc = h ? k : nc - 1u;
+    return (hot[cc >> 4] >> (((u32)c & 15u) * 2u)) & 3u;   // (k = c mod 16 where hot)
   };
   auto cp2 = [&](int c, u32 w) -> int32_t {
-    const bool h = (u32)c < nc;
+    bool h;
+    (void)hot_at(c, hc_lg, nc, h);
     const u32 x = code2[h ? 0u : ((u32)c >> 4)];
     return (int32_t)(h ? w : ((x >> (((u32)c & 15u) * 2u)) & 3u));
   };
@@ -3462,13 +3502,15 @@ int launch_first(lpa_graph* g, int32_t* Lown) {
   return LPA_OK;
 }
 
-// the refresh after superstep 1 of a single-GPU handle may take the giant codes
-// (after superstep 1 on R-MAT, after superstep 2 on Chung-Lu: the first label vector
-// whose giant carries the hubs without holding half the hot slots)
-bool code_refresh_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset <= 1; }
+// the refresh after superstep 1 or 2 may take the giant codes (after superstep 1 on
+// R-MAT, after superstep 2 on Chung-Lu: the first label vector whose giant carries the
+// hubs without holding half the hot slots).  Round 6: on every rank of a partitioned job
+// too -- the refresh follows the exchange, so it codes the replicated vector, and G (picked
+// from it) is the same on every rank; each rank codes and settles its own rows
+bool code_refresh_now(const lpa_graph* g) { return g->code_ok && g->since_reset <= 1; }
 // ... and superstep 2 (block mode) or 3 then settles from them
-bool code_tally_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset == 1; }
-bool code_tally3_now(const lpa_graph* g) { return g->code_ok && !exchanges(g) && g->since_reset == 2 && g->code3; }
+bool code_tally_now(const lpa_graph* g) { return g->code_ok && g->since_reset == 1; }
+bool code_tally3_now(const lpa_graph* g) { return g->code_ok && g->since_reset == 2 && g->code3; }
 
 // the code settle of the seven settled bins in one launch (k_code_settle; it returns at
 // once unless a giant-code refresh was taken): blocks split over the bins by work (a
@@ -3880,20 +3922,24 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     hipLaunchKernelGGL(k_giant_pick, dim3(1), dim3(kPickK), 0, s, L, g->V, g->slice, g->nranks, g->gword);
     LPA_HIP(hipGetLastError());
   }
-  const auto pow2 = [](int64_t x) { return x > 0 && (x & (x - 1)) == 0; };
-  const bool ranked = g->nranks > 1 && pow2(g->nranks) && pow2(g->slice) && g->nranks <= kHotLabels &&
-                      g->slice >= kHotLabels / g->nranks;
+  const bool ranked = rebuild_ranked(g);
+  // hot slots of the bits-mode / code-mode test (k_giant_bits' count in gword[3]): the
+  // first kHotBits slots at P = 1, the first kHotBits / P (whole bit words) of every slice
+  // of a rank-strided vector -- the same degree-ranked top set
+  const uint64_t hmask = ranked ? (uint64_t)(g->slice - 1) : ~0ull;
+  const int64_t hlim = ranked ? std::min<int64_t>(g->slice, kHotBits / g->nranks / 64 * 64) : kHotBits;
+  const int64_t nhot_bits = ranked ? g->nranks * hlim : std::min<int64_t>(g->vpad, kHotBits);
   if (g->rebuild_hot && g->nranks == 1 && g->vpad < kHotMinSlots) {
     const int64_t ngrp = (g->vpad + 511) / 512;
     const unsigned gb = cap_grid((ngrp + 3) / 4, 4096), gr = cap_grid((g->arcs + 2047) / 2048, 8192);
     if (if_wanted) {
       hipLaunchKernelGGL(k_giant_bits<true>, dim3(gb), dim3(256), 0, s, ctr, thr, L, g->vpad, g->gword,
-                         (unsigned long long*)g->gbits, g->abits, (int64_t)0);
+                         (unsigned long long*)g->gbits, g->abits, (int64_t)0, hmask, hlim);
       hipLaunchKernelGGL(k_al_rebuild_small<true>, dim3(gr), dim3(256), 0, s, ctr, thr, g->col, g->arcs, L, g->al,
                          g->gbits, g->vpad, g->gword, g->abits);
     } else {
       hipLaunchKernelGGL(k_giant_bits<false>, dim3(gb), dim3(256), 0, s, ctr, thr, L, g->vpad, g->gword,
-                         (unsigned long long*)g->gbits, g->abits, (int64_t)0);
+                         (unsigned long long*)g->gbits, g->abits, (int64_t)0, hmask, hlim);
       hipLaunchKernelGGL(k_al_rebuild_small<false>, dim3(gr), dim3(256), 0, s, ctr, thr, g->col, g->arcs, L, g->al,
                          g->gbits, g->vpad, g->gword, g->abits);
     }
@@ -3920,10 +3966,10 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     const int64_t nzero = blk ? g->blk_a0 / 64 : 0;
     if (if_wanted)
       hipLaunchKernelGGL(k_giant_bits<true>, dim3(cap_grid((ngrp + 3) / 4, 4096)), dim3(256), 0, s, ctr, thr, L,
-                         g->vpad, g->gword, (unsigned long long*)g->gbits, g->abits, nzero);
+                         g->vpad, g->gword, (unsigned long long*)g->gbits, g->abits, nzero, hmask, hlim);
     else
       hipLaunchKernelGGL(k_giant_bits<false>, dim3(cap_grid((ngrp + 3) / 4, 4096)), dim3(256), 0, s, ctr, thr, L,
-                         g->vpad, g->gword, (unsigned long long*)g->gbits, g->abits, nzero);
+                         g->vpad, g->gword, (unsigned long long*)g->gbits, g->abits, nzero, hmask, hlim);
     LPA_HIP(hipGetLastError());
     // ranked without a usable bit share: nbits 0 keeps every block in labels mode
     const int64_t nbits = (ranked && hb_lg == 0) ? 0 : g->vpad;
@@ -3936,8 +3982,7 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
                      g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \
                      blk ? g->blk_pieces : nullptr, binfo, code ? g->gword + 5 : nullptr)
     if (code) {
-      hipLaunchKernelGGL(k_code_mode, dim3(1), dim3(64), 0, s, ctr, thr,
-                         (int64_t)(g->vpad < kHotBits ? g->vpad : kHotBits), g->gword);
+      hipLaunchKernelGGL(k_code_mode, dim3(1), dim3(64), 0, s, ctr, thr, nhot_bits, g->gword);
       LPA_HIP(hipGetLastError());
     }
     if (if_wanted) {
@@ -3951,8 +3996,17 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
       hipLaunchKernelGGL(k_code_build, dim3(cap_grid((g->vpad / 16 + 255) / 256, 4096)), dim3(256), 0, s,
                          (const int4*)L, g->vpad / 16, g->gword, g->code2);
       LPA_HIP(hipGetLastError());
-      hipLaunchKernelGGL(k_code_rebuild, dim3(dev_cus), dim3(1024), 0, s, g->gword, g->col, g->arcs, L,
-                         g->vpad, g->code2, g->code_pcut, g->al2, g->al);
+      // ranked: 2^hc_lg codes of every slice in LDS (P << hc_lg <= 16 kHotLabelsSingle)
+      int hc_lg = 4;
+      while (ranked && (int64_t(g->nranks) << (hc_lg + 1)) <= 16ll * kHotLabelsSingle &&
+             (int64_t(1) << (hc_lg + 1)) <= g->slice)
+        ++hc_lg;
+      if (ranked)
+        hipLaunchKernelGGL(k_code_rebuild<true>, dim3(dev_cus), dim3(1024), 0, s, g->gword, g->col, g->arcs, L,
+                           g->vpad, g->code2, g->code_pcut, g->al2, g->al, slice_lg, hot_lg, hc_lg);
+      else
+        hipLaunchKernelGGL(k_code_rebuild<false>, dim3(dev_cus), dim3(1024), 0, s, g->gword, g->col, g->arcs, L,
+                           g->vpad, g->code2, g->code_pcut, g->al2, g->al, 0, 0, 0);
     }
   } else {
     const unsigned grid = cap_grid((g->arcs / 4 + 511) / 512, 8192);
@@ -4009,8 +4063,15 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
     hipLaunchKernelGGL(k_dense_decide, dim3(1), dim3(64), 0, s, ctr, nd, g->gword);
     LPA_HIP(hipGetLastError());
     LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, true, par, 0, 0, 2));
-  } else if (!diff_done) {
-    LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, true, par));
+  } else {
+    if (!diff_done) LPA_TRY(launch_diff(g, s, Lc, Ln, 0, nd, true, par));
+    // P > 1, superstep 2 after a giant-code refresh, its changes exchanged as a delta
+    // (the change chunks are queued): the rows it settled from codes have no al[] entries,
+    // so this refresh rebuilds whatever the change count (k_dense_decide's code clause)
+    if (code_tally_now(g)) {
+      hipLaunchKernelGGL(k_dense_decide, dim3(1), dim3(64), 0, s, ctr, INT64_MAX, g->gword);
+      LPA_HIP(hipGetLastError());
+    }
   }
   LPA_TRACE_POINT("diff");
   // (a handle without the CSC position index rebuilds every time: counters[1] >= 0 > -1)
@@ -4061,8 +4122,15 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
 
 }  // namespace
 
+// (the caller-driven delta exchange, lpa_exchange_put_delta: the refresh of the superstep
+// lpa_step just ran, which since_reset already counts -- it is seen as the in-library
+// refresh of that superstep sees it: dense / code-settled supersteps, code refresh allowed)
 int launch_refresh_ext(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff_done, int par) {
-  return launch_refresh(g, Lc, Ln, diff_done, par);
+  const bool back = g->since_reset > 0;
+  if (back) --g->since_reset;
+  const int rc = launch_refresh(g, Lc, Ln, diff_done, par);
+  if (back) ++g->since_reset;
+  return rc;
 }
 
 // Capture `body` (launches on the handle's stream and the streams it forks) into an
@@ -4124,7 +4192,7 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     // before superstep 3 on a code-capable handle: did the refresh after superstep 2 take
     // the giant codes?  One host read (~20 us of idle GPU) instead of ~10 kernels that
     // return at once in the other case (C3: ~0.1 ms of superstep 3's 0.47)
-    if (g->code_ok && !exchanges(g) && g->since_reset == 2) {
+    if (g->code_ok && g->since_reset == 2) {
       LPA_HIP(hipMemcpyAsync(g->h_flag, g->gword + 5, sizeof(int32_t), hipMemcpyDeviceToHost, s));
       LPA_HIP(hipStreamSynchronize(s));
       g->code3 = *g->h_flag != 0;
@@ -4285,6 +4353,18 @@ int frontier_all(lpa_graph* g, int par) {
 int rebuild_arc_labels(lpa_graph* g) {
   if (g->arcs == 0) return LPA_OK;
   return launch_rebuild(g, false, 0, g->lab[g->cur], g->counters);
+}
+
+int refresh_after_put(lpa_graph* g) {
+  if (g->arcs == 0) return LPA_OK;
+  if (g->since_reset == 0) return rebuild_arc_labels(g);   // no superstep ran since L0
+  // the refresh of the superstep lpa_step just ran (since_reset counted it already): an
+  // unconditional rebuild (thr = -1: every rebuild_wanted test passes), the giant codes
+  // allowed after superstep 1 or 2 as in the in-library schedule
+  --g->since_reset;
+  const int rc = launch_rebuild(g, true, -1, g->lab[g->cur], g->counters + 4 * (g->par ^ 1));
+  ++g->since_reset;
+  return rc;
 }
 
 int ensure_al(lpa_graph* g) {

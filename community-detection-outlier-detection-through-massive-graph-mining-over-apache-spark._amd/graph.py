@@ -50,19 +50,45 @@ class Graph:
     rank r of an in-process ``Loopback`` group (P handles on one device, one host
     thread each, the same exchange code with D2D copies for the allgather);
     ``comm_id=None`` with ``nranks > 1`` selects the caller-driven exchange
-    (``exchange_get`` / ``exchange_put``).
+    (``exchange_get`` / ``exchange_put``); ``allgather=fn`` the host-staged collective
+    (``lpa_graph_create_hostcoll``): the library's own exchange schedule with every
+    allgather done by ``fn(send: np.ndarray[uint8]) -> bytes-like of nranks * send.size``
+    (e.g. torch.distributed gloo between processes).
     """
 
     def __init__(self, src, dst, num_vertices: int, device: int = 0, rank: int = 0,
-                 nranks: int = 1, comm_id: bytes | None = None, loopback: "Loopback | None" = None):
+                 nranks: int = 1, comm_id: bytes | None = None, loopback: "Loopback | None" = None,
+                 allgather=None):
         lib = _lib.load()
         self._lib = lib
         self._h = ctypes.c_void_p()
+        self._allgather_cb = None
+        self._allgather_err = None
         sp, dp, m, flags, keep = _edge_ptrs(src, dst)
         V = int(num_vertices)
         if V < 0 or V > np.iinfo(np.int32).max:
             raise ValueError(f"num_vertices out of range: {V}")
-        if loopback is not None:
+        if allgather is not None:
+            P = int(nranks)
+
+            def _cb(send, recv, nbytes, _ctx):
+                try:
+                    n = int(nbytes)
+                    src_b = np.ctypeslib.as_array((ctypes.c_uint8 * max(n, 1)).from_address(send))[:n]
+                    out = np.frombuffer(memoryview(allgather(src_b.copy())), dtype=np.uint8)
+                    if out.size != P * n:
+                        raise ValueError(f"allgather returned {out.size} bytes, expected {P * n}")
+                    if n > 0:
+                        ctypes.memmove(recv, out.ctypes.data, P * n)
+                    return 0
+                except BaseException as e:  # noqa: BLE001 -- reported after the failed call
+                    self._allgather_err = e
+                    return -1
+
+            self._allgather_cb = _lib.ALLGATHER_FN(_cb)   # kept alive with the handle
+            rc = lib.lpa_graph_create_hostcoll(sp, dp, m, V, device, flags, rank, P, self._allgather_cb, None,
+                                               ctypes.byref(self._h))
+        elif loopback is not None:
             nranks = loopback.nranks
             rc = lib.lpa_graph_create_loopback(sp, dp, m, V, device, flags, rank, loopback._handle(),
                                                ctypes.byref(self._h))
@@ -106,6 +132,13 @@ class Graph:
             raise ValueError("graph handle is closed")
         return self._h
 
+    def _check(self, rc: int):
+        """check() that re-raises a host allgather function's own exception as the cause."""
+        err, self._allgather_err = self._allgather_err, None
+        if rc != _lib.LPA_OK and err is not None:
+            raise _lib.LpaError(rc, _lib.last_error()) from err
+        _lib.check(rc)
+
     # -- LPA ----------------------------------------------------------------
     def info(self) -> dict:
         info = _lib.LpaGraphInfo()
@@ -117,7 +150,7 @@ class Graph:
 
     def step(self, n: int = 1, stats: bool = False):
         st = _lib.LpaStats() if stats else None
-        _lib.check(self._lib.lpa_step(self._handle(), int(n), ctypes.byref(st) if stats else None))
+        self._check(self._lib.lpa_step(self._handle(), int(n), ctypes.byref(st) if stats else None))
         return st.to_dict() if stats else None
 
     def labels(self, out=None) -> np.ndarray:
@@ -140,8 +173,8 @@ class Graph:
         else:
             lab = np.empty(self.num_vertices, dtype=np.int32)
             ptr, on_dev = lab.ctypes.data, 0
-        _lib.check(self._lib.lpa_run(self._handle(), int(max_iter), ptr, on_dev,
-                                     ctypes.byref(st) if stats else None))
+        self._check(self._lib.lpa_run(self._handle(), int(max_iter), ptr, on_dev,
+                                      ctypes.byref(st) if stats else None))
         return (lab, st.to_dict()) if stats else lab
 
     def degrees(self) -> np.ndarray:

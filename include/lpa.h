@@ -83,9 +83,10 @@ typedef struct lpa_graph_info {
   int64_t blocked_rows;    /* P = 1: rows whose columns are in (class, column) order for
                               the class-blocked al[] rebuild (0: off, LPA_BLOCK_DEG)  */
   int64_t blocked_pieces;  /* ... and the rebuild's piece-list length                */
-  int64_t code_refresh;    /* 1: the last refresh took the giant codes (P = 1: superstep 2
-                              settles rows from 1-byte label codes) -- read
-                              after a superstep-1 step; 0 otherwise (since ABI 6)      */
+  int64_t code_refresh;    /* 1: the last refresh took the giant codes (the next superstep
+                              settles rows from 2-bit label codes; every
+                              rank of a partitioned job since ABI 7) -- read after a
+                              superstep-1 step; 0 otherwise (since ABI 6)              */
   int64_t graph_replays;   /* supersteps run by replaying a captured HIP graph (the
                               converged ones, P = 1 also supersteps 2-3; since ABI 6)  */
   int64_t exchanges_posted; /* P > 1: delta exchanges sent at a capacity fixed before the
@@ -94,6 +95,8 @@ typedef struct lpa_graph_info {
                               capacity: exchanged again in the form that fits          */
   int64_t gather_mode;     /* 1: the tallies read L[col[i]] and no al[] refresh runs (one
                               GPU, label vector <= 4 MB, no row above 128 arcs; since ABI 6) */
+  int64_t host_allgathers; /* allgathers served by the host collective's function
+                              (lpa_graph_create_hostcoll; since ABI 7)                 */
 } lpa_graph_info;
 
 /* Outlier summary. */
@@ -147,6 +150,25 @@ int lpa_graph_create_dist(const int32_t* src, const int32_t* dst, int64_t m, int
  * (each then fails with LPA_ERCCL); a rank whose peers never arrive fails the
  * same way after 300 s.
  */
+/*
+ * Host-staged collective (round 6): the same in-library exchange as the RCCL path --
+ * full / delta / giant-compressed forms, the posted delta and its stand-down, the
+ * per-rank count triple -- with every allgather handed to the caller's host function:
+ *   allgather(send, recv, bytes_per_rank, ctx) gathers every rank's `bytes_per_rank`
+ *   bytes from `send` into `recv` in rank order (nranks * bytes_per_rank bytes) and
+ *   returns 0 (non-zero: the superstep fails with LPA_ERCCL).
+ * Both buffers are pinned host memory owned by the library, valid during the call; the
+ * function runs on the thread that called lpa_step / lpa_run, once per allgather, and
+ * every rank calls it the same number of times with the same size.  For clusters
+ * without RCCL between the ranks: MPI_Allgather, torch.distributed (gloo), a Spark
+ * barrier stage moving the bytes through the driver.  PCIe-staged: the RCCL build
+ * (lpa_graph_create_dist with a comm id) is the fast path between MI355X GPUs.
+ */
+typedef int (*lpa_allgather_fn)(const void* send, void* recv, int64_t bytes_per_rank, void* ctx);
+int lpa_graph_create_hostcoll(const int32_t* src, const int32_t* dst, int64_t m, int32_t V,
+                              int32_t device, uint32_t flags, int32_t rank, int32_t nranks,
+                              lpa_allgather_fn allgather, void* ctx, lpa_graph** out);
+
 typedef struct lpa_loopback lpa_loopback;
 int lpa_loopback_create(int32_t nranks, lpa_loopback** out);
 void lpa_loopback_abort(lpa_loopback* group);
@@ -195,8 +217,11 @@ int lpa_set_frontier(lpa_graph* g, int32_t on);
  * host's read; a count above it makes the queued apply stand down and the host exchange
  * again in the form that fits).  cap < 0: adaptive (default: twice the last largest
  * count, 1024..131072 entries); 0: off (the host reads the counts first); > 0: that
- * fixed capacity (testing: 1 exercises the stand-down path).  Labels are identical
- * either way.  Since ABI 6. */
+ * fixed capacity (testing: 1 exercises the stand-down path).  The value is this rank's
+ * REQUEST: it travels with the next per-rank count exchange and every rank posts the
+ * smallest capacity requested by any rank (0 if any rank turned posting off), from the
+ * superstep after that exchange on -- so ranks never disagree on the allgather size,
+ * whichever ranks call this and when.  Labels are identical either way.  Since ABI 6. */
 int lpa_set_posted(lpa_graph* g, int64_t cap);
 /* Run on a caller-provided hipStream_t (NULL = the handle's own stream). */
 int lpa_set_stream(lpa_graph* g, void* hip_stream);
@@ -266,12 +291,14 @@ int lpa_quality(lpa_graph* g, const int32_t* labels, int32_t labels_on_device, l
 int lpa_degrees(lpa_graph* g, int32_t* deg_out);
 
 /* lpa_graph_info has grown across header versions (it carries no size field of its
- * own): lpa_graph_get_info writes the whole struct of THIS header (LPA_ABI_VERSION);
- * a caller compiled against another header passes its struct size to
- * lpa_graph_get_info_sized, which writes only the first min(info_size, sizeof)
- * bytes (the fields are only ever appended).  lpa_abi_version() returns the
- * library's LPA_ABI_VERSION, so a binding can check the header it was built for. */
-#define LPA_ABI_VERSION 6
+ * own; fields are only ever appended).  lpa_graph_get_info is frozen at the ABI-5
+ * struct: it writes the fields up to blocked_pieces, never more, so a caller built
+ * against that header is not overrun.  lpa_graph_get_info_sized(g, info, sizeof *info)
+ * writes min(info_size, sizeof) bytes of this header's struct and zeroes the rest of a
+ * larger caller struct: use it for the later fields.  lpa_abi_version() returns the
+ * library's LPA_ABI_VERSION, so a binding can check the header it was built for.
+ * ABI 7: lpa_graph_create_hostcoll, host_allgathers, the frozen unsized get_info. */
+#define LPA_ABI_VERSION 7
 int lpa_abi_version(void);
 int lpa_graph_get_info(const lpa_graph* g, lpa_graph_info* info);
 int lpa_graph_get_info_sized(const lpa_graph* g, lpa_graph_info* info, int64_t info_size);

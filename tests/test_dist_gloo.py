@@ -267,3 +267,96 @@ def test_gloo_library_delta_exchange_two_processes(oracle):
         p.join(timeout=60)
     assert all(res[r][0] for r in range(P)), res
     assert set(res[0][1]) == {"full", "delta"}, res[0][1]
+
+
+# ---------------------------------------------------------------------------
+# The library's IN-LIBRARY exchange (lpa_exchange.hip exchange_collective -- the code an
+# RCCL rank runs: the per-rank count triple, the full / delta / giant-compressed forms,
+# the posted delta and its stand-down) across two real processes: each handle is built
+# with lpa_graph_create_hostcoll and its allgathers are done by torch.distributed gloo
+# on the host (the giant and posted forms across a
+# process boundary, and a posted capacity set on ONE rank only).
+# ---------------------------------------------------------------------------
+HC_STEPS = 10
+
+
+def _gloo_allgather_bytes(send):
+    """Every rank's `send` bytes in rank order (gloo all_gather on int32 words)."""
+    n = send.size
+    x = torch.from_numpy(send.view(np.int32) if n % 4 == 0 else send)
+    parts = _gather(x)
+    return b"".join(p.numpy().tobytes() for p in parts)
+
+
+def _hostcoll_worker(rank, P, port, V, s, d, ref, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=P)
+    try:
+        import graphframes_amd as gfa
+
+        out = {}
+        with gfa.Graph(s, d, V, rank=rank, nranks=P, allgather=_gloo_allgather_bytes) as g:
+            ok = True
+            for t in range(HC_STEPS):
+                g.step(1)
+                ok = ok and bool(np.array_equal(g.labels(), ref[t]))
+            out["steps_ok"] = ok
+            out["forms"] = {k: g.info()[k] for k in ("exchanges_full", "exchanges_delta", "exchanges_giant",
+                                                     "exchanges_posted", "exchanges_post_missed",
+                                                     "host_allgathers")}
+            # a posted capacity of 1 requested by rank 0 ONLY: the ranks agree on the
+            # smallest request (it travels with the count triple), so both post the same
+            # allgather size and the queued apply stands down on both
+            before = g.info()
+            if rank == 0:
+                g.set_posted(1)
+            runs_ok = bool(np.array_equal(g.run(HC_STEPS), ref[HC_STEPS - 1]))
+            after = g.info()
+            out["missed_p1"] = after["exchanges_post_missed"] - before["exchanges_post_missed"]
+            # back to adaptive on rank 0: posted exchanges that fit
+            if rank == 0:
+                g.set_posted(-1)
+            before = g.info()
+            runs_ok = runs_ok and bool(np.array_equal(g.run(HC_STEPS), ref[HC_STEPS - 1]))
+            after = g.info()
+            out["posted_adaptive"] = after["exchanges_posted"] - before["exchanges_posted"]
+            out["runs_ok"] = runs_ok
+        q.put((rank, out))
+    except BaseException as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gloo_host_collective_in_library_exchange_two_processes(oracle):
+    """Two processes, one hostcoll rank handle each (R-MAT-16 on the one GPU): every
+    superstep bit-exact on both ranks through the library's own exchange schedule with
+    gloo as the transport; the full, delta, giant and posted forms all ran, a posted
+    capacity set on one rank alone stood down identically on both, and lpa_run(10)
+    is bit-exact after each setting."""
+    P = 2
+    s, d = oracle.gen_rmat(16, 16, 3, True)
+    V = 1 << 16
+    _, ref, _ = oracle.lpa(V, s, d, HC_STEPS, per_iter=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 35500 + (os.getpid() % 2000)
+    procs = [ctx.Process(target=_hostcoll_worker, args=(r, P, port, V, s, d, ref, q)) for r in range(P)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(P):
+        r, out = q.get(timeout=240)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+    assert all("error" not in res[r] for r in range(P)), res
+    assert all(res[r]["steps_ok"] and res[r]["runs_ok"] for r in range(P)), res
+    f = res[0]["forms"]
+    assert f == res[1]["forms"], res            # every rank took the same forms
+    assert f["exchanges_full"] >= 1 and f["exchanges_delta"] >= 1 and f["exchanges_giant"] >= 1, f
+    assert f["exchanges_posted"] >= 1 and f["host_allgathers"] > 0, f
+    assert res[0]["missed_p1"] == res[1]["missed_p1"] >= 1, res
+    assert res[0]["posted_adaptive"] == res[1]["posted_adaptive"] >= 1, res

@@ -38,11 +38,15 @@ def _host(t):
     return t.cpu().numpy()
 
 
-def _mismatch_per_step(g, hist, n):
-    """Steps the handle n times; the number of labels that differ at each superstep."""
+def _mismatch_per_step(g, hist, n, codes=None):
+    """Steps the handle n times; the number of labels that differ at each superstep.
+    codes (a list): gets code_refresh after supersteps 1 and 2 (whether that refresh
+    took the giant codes)."""
     bad = []
     for t in range(n):
         g.step(1)
+        if codes is not None and t < 2:
+            codes.append(int(g.info()["code_refresh"]))
         bad.append(int((g.labels() != hist[t]).sum()))
     return bad
 
@@ -80,10 +84,12 @@ def _empty_cache():
     torch.cuda.empty_cache()
 
 
-def _partitioned_every_superstep(gfa, cfg, P, what):
+def _partitioned_every_superstep(gfa, cfg, P, what, code_after):
     """A loopback group of P ranks on the one GPU, built from the same edge list (as
     P processes of `bench.py --gpus P` build theirs), every rank checked against the
-    oracle at every superstep 1..10, then lpa_run(10) on every rank concurrently."""
+    oracle at every superstep 1..10, then lpa_run(10) on every rank concurrently.
+    code_after (1 or 2): every rank's refresh after that superstep took the giant codes
+    (round 6: the code refresh and settle on every rank of a partitioned job)."""
     import torch
 
     lb = gfa.Loopback(P)
@@ -97,10 +103,12 @@ def _partitioned_every_superstep(gfa, cfg, P, what):
         _empty_cache()
         infos = [g.info() for g in ranks]
         assert sum(i["arcs"] for i in infos) == 2 * cfg.src.size
-        bad = gfa.run_ranks(ranks, lambda r, g: _mismatch_per_step(g, cfg.hist, MAX_ITER))
+        codes = [[] for _ in range(P)]
+        bad = gfa.run_ranks(ranks, lambda r, g: _mismatch_per_step(g, cfg.hist, MAX_ITER, codes[r]))
         for r in range(P):
             for t in range(MAX_ITER):
                 assert bad[r][t] == 0, f"{what} P={P} rank {r} superstep {t + 1}: {bad[r][t]} labels differ"
+        assert all(c[code_after - 1] == 1 for c in codes), f"{what} P={P} code refresh per rank: {codes}"
         infos = [g.info() for g in ranks]
         # full slices after L0, giant-compressed (bitmap + changed non-giant labels) once
         # G dominates, changed-label deltas when converged: one exchange per superstep
@@ -152,15 +160,17 @@ def test_c4_rmat26_every_superstep(gfa, c4):
         assert g.info()["arcs"] == 2 * (16 << 26)   # > 2^31: int64 row offsets
         del dev_s, dev_d
         _empty_cache()
-        bad = _mismatch_per_step(g, c4.hist, MAX_ITER)
+        codes = []
+        bad = _mismatch_per_step(g, c4.hist, MAX_ITER, codes)
     _empty_cache()
     assert bad == [0] * MAX_ITER, f"C4 one GPU: labels differing per superstep {bad}"
+    assert codes[0] == 1, codes
 
 
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_c4_rmat26_partitioned_every_superstep(gfa, c4, P):
     """BASELINE C4 as configured: R-MAT-26 vertex-partitioned over P ranks."""
-    _partitioned_every_superstep(gfa, c4, P, "C4")
+    _partitioned_every_superstep(gfa, c4, P, "C4", code_after=1)
 
 
 def test_c5_chunglu_every_superstep(gfa, c5):
@@ -174,16 +184,18 @@ def test_c5_chunglu_every_superstep(gfa, c5):
         assert g.info()["max_degree"] > 1_000_000   # the hub-bin spill path is exercised
         del dev_s, dev_d
         _empty_cache()
-        bad = _mismatch_per_step(g, c5.hist, MAX_ITER)
+        codes = []
+        bad = _mismatch_per_step(g, c5.hist, MAX_ITER, codes)
         run10 = int((g.run(MAX_ITER) != c5.hist[MAX_ITER - 1]).sum())
     _empty_cache()
     assert bad == [0] * MAX_ITER, f"C5 one GPU: labels differing per superstep {bad}"
+    assert codes[1] == 1, codes   # Chung-Lu: L2 is the first vector with a giant on the hubs
     assert run10 == 0, f"C5 lpa_run(10): {run10} labels differ"
 
 
 def test_c5_chunglu_partitioned_p8_every_superstep(gfa, c5):
     """BASELINE C5 as configured: the heavy-hub graph over 8 ranks."""
-    _partitioned_every_superstep(gfa, c5, 8, "C5")
+    _partitioned_every_superstep(gfa, c5, 8, "C5", code_after=2)
 
 
 def test_c2_outlier_l1_l2_vs_oracle(gfa, oracle):

@@ -15,7 +15,7 @@ import time
 import numpy as np
 import pytest
 
-from graphs import degree_mix
+from graphs import code_mix, degree_mix
 
 pytestmark = pytest.mark.gpu
 
@@ -185,3 +185,67 @@ def test_loopback_close_before_graphs(gfa):
     lb.close()
     for g in ranks:
         g.close()
+
+
+@pytest.fixture(scope="module")
+def codemix22(gfa, oracle):
+    s, d = gfa.gen_rmat(22, 16, seed=11)
+    V, sn, dn = code_mix(s.cpu().numpy(), d.cpu().numpy(), 1 << 22)
+    _, hist, _ = oracle.lpa(V, sn, dn, 5, per_iter=True)
+    return V, sn, dn, hist
+
+
+@pytest.mark.parametrize("P,lbin", [(2, None), (4, None), (2, "8")])
+def test_loopback_giant_codes_every_rank(gfa, codemix22, monkeypatch, P, lbin):
+    """Round 6: the giant-code refresh after superstep 1 and superstep 2's settle from the
+    2-bit codes on EVERY rank of a partitioned job (each rank codes its own arcs against
+    the G of the replicated vector, the rank-strided LDS hot sets), with every exact
+    fallback populated (tests/graphs.py code_mix: wave-bin rows, block-tier hub rows and
+    > 8192-arc hub rows whose mode is not G) -- bit-exact on every rank at supersteps 1..5,
+    the code refresh asserted on every rank.  lbin "8": the cut that codes the rows of
+    9-64 arcs too (LPA_CODE_LBIN; C4 / C5 take it by size), whose coded row bins walk
+    the code settle's lists on the third stream."""
+    if lbin:
+        monkeypatch.setenv("LPA_CODE_LBIN", lbin)
+    V, sn, dn, hist = codemix22
+    lb, ranks = _group(gfa, sn, dn, V, P)
+    try:
+        assert all(g.info()["slice"] & (g.info()["slice"] - 1) == 0 for g in ranks)   # power-of-two slices
+
+        def work(r, g):
+            out, codes = [], []
+            for t in range(5):
+                g.step(1)
+                if t == 0:
+                    codes.append(g.info()["code_refresh"])
+                out.append(int((g.labels() != hist[t]).sum()))
+            return out, codes
+
+        res = gfa.run_ranks(ranks, work)
+        for r in range(P):
+            assert res[r][0] == [0] * 5, f"P={P} rank {r} labels differing per superstep {res[r][0]}"
+            assert res[r][1] == [1], f"P={P} rank {r}: the giant-code refresh was not taken"
+        runs = gfa.run_ranks(ranks, lambda r, g: g.run(5))
+        for r in range(P):
+            assert np.array_equal(runs[r], hist[4]), f"P={P} rank {r} lpa_run(5)"
+    finally:
+        _close(lb, ranks)
+
+
+def test_code_cut_g8_single_gpu(gfa, codemix22, monkeypatch):
+    """the code_lbin = g8 schedule (the rows of 9-64 arcs coded; their row
+    bins walk the code settle's lists after ev_join2[2], k_code_partial_rows fills their
+    al[]) on a graph small enough for the fast suite -- forced by LPA_CODE_LBIN=8 --
+    bit-exact at supersteps 1..5, then lpa_run(5) twice (replayed graphs)."""
+    monkeypatch.setenv("LPA_CODE_LBIN", "8")
+    V, sn, dn, hist = codemix22
+    with gfa.Graph(sn, dn, V) as g:
+        for t in range(5):
+            g.step(1)
+            if t == 0:
+                assert g.info()["code_refresh"] == 1
+            bad = int((g.labels() != hist[t]).sum())
+            assert bad == 0, f"g8 cut superstep {t + 1}: {bad} labels differ"
+        for _ in range(2):
+            g.reset()
+            assert np.array_equal(g.run(5), hist[4])
