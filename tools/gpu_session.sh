@@ -56,6 +56,25 @@ for st in $STEPS; do
       fi ;;
     tally) timeout -k 10 400 python3 -u tools/rank_tally.py C4 8 > "gpurun_out/${TAG}_tally.json" 2> "gpurun_out/${TAG}_tally.err" || exit 1
            cat "gpurun_out/${TAG}_tally.json" ;;
+    refresh)   # per-rank superstep-1 refresh at C4 / P = 8 against the single GPU (kernel trace)
+      cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+      timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/${TAG}_rr" -o run \
+        -- python3 tools/rank_refresh.py C4 8 > "gpurun_out/${TAG}_rr_run.json" 2> "gpurun_out/${TAG}_rr.err" || exit 1
+      python3 tools/refresh_trace.py "gpurun_out/${TAG}_rr" 8 3 > "gpurun_out/${TAG}_rr.json" || exit 1
+      cat "gpurun_out/${TAG}_rr_run.json" "gpurun_out/${TAG}_rr.json" ;;
+    ab)   # bench A/B of the default library against VLIB (LPA_LIB_PATH) on CONFIGS (default "C3 C5")
+      for c in ${CONFIGS:-C3 C5}; do
+        for v in default variant; do
+          if [ $v = default ]; then
+            timeout -k 10 400 python3 -u bench.py --config $c --no-cpu-baseline --no-outlier --no-quality --steps 5 \
+              > "gpurun_out/${TAG}_ab_${c}_$v.json" 2> "gpurun_out/${TAG}_ab_${c}_$v.err" || exit 1
+          else
+            LPA_LIB_PATH="$VLIB" timeout -k 10 400 python3 -u bench.py --config $c --no-cpu-baseline --no-outlier \
+              --no-quality --steps 5 > "gpurun_out/${TAG}_ab_${c}_$v.json" 2> "gpurun_out/${TAG}_ab_${c}_$v.err" || exit 1
+          fi
+          python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], d['run_maxiter10_ms'], d['baseline_method']['median_ms_per_superstep_2_to_10'])" "gpurun_out/${TAG}_ab_${c}_$v.json"
+        done
+      done ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
