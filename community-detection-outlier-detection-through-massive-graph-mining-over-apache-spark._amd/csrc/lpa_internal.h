@@ -261,6 +261,7 @@ struct lpa_graph {
                                 //   (lpa_build: g64 when the label vector is <= 64 MB, else g8;
                                 //   LPA_CODE_LBIN=5|8 forces either, for tests)
   int32_t code_lbin_env = -1;   // LPA_CODE_LBIN at create time (-1: by size)
+  int codes_env = 1;            // LPA_GIANT_CODES=0: no giant-code refresh (A/B, tests)
   int64_t code_pcut = 0;        // its first arc position
   bool code3 = false;           // superstep 3 follows a giant-code refresh (read by the host
                                 //   before it: its schedule differs, see run_supersteps)

@@ -62,6 +62,13 @@ for st in $STEPS; do
         -- python3 tools/rank_refresh.py C4 8 > "gpurun_out/${TAG}_rr_run.json" 2> "gpurun_out/${TAG}_rr.err" || exit 1
       python3 tools/refresh_trace.py "gpurun_out/${TAG}_rr" 8 3 > "gpurun_out/${TAG}_rr.json" || exit 1
       cat "gpurun_out/${TAG}_rr_run.json" "gpurun_out/${TAG}_rr.json" ;;
+    conv)   # kernel trace of C3's timed calls (tools/step_trace.py): converged-superstep timelines
+      cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/${TAG}_conv" -o run \
+        -- python3 tools/step_trace.py ${CONV_CFG:-C3} > "gpurun_out/${TAG}_conv.txt" 2>&1 || exit 1
+      f=$(ls gpurun_out/${TAG}_conv/*/*kernel_trace.csv gpurun_out/${TAG}_conv/*kernel_trace.csv 2>/dev/null | head -1)
+      python3 tools/timeline2.py "$f" > "gpurun_out/${TAG}_conv_timeline.txt" || exit 1
+      head -3 "gpurun_out/${TAG}_conv_timeline.txt" ;;
     ab)   # bench A/B of the default library against VLIB (LPA_LIB_PATH) on CONFIGS (default "C3 C5")
       for c in ${CONFIGS:-C3 C5}; do
         for v in default variant; do

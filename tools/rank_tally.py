@@ -68,6 +68,7 @@ def exchange():
 
 
 per_rank = [[0.0] * (MAX_ITER - 1) for _ in range(P)]
+conv_k = [dict() for _ in range(P)]   # per-kernel ms summed over the converged supersteps 5..10
 modes = []
 for g in ranks:
     g.step(1)   # superstep 1 (column runs; not serialized)
@@ -76,7 +77,11 @@ for g in ranks:
     g.set_serial(True)
 for t in range(MAX_ITER - 1):
     for r, g in enumerate(ranks):
-        per_rank[r][t] = tally_ms(g.step(1, stats=True))
+        st = g.step(1, stats=True)
+        per_rank[r][t] = tally_ms(st)
+        if t >= 3:
+            for k in TALLY:
+                conv_k[r][k] = conv_k[r].get(k, 0.0) + st["kernel_ms"][k]
     modes.append(exchange())
 # every rank's replica equals the single-GPU labels after superstep 10
 ok = all(np.array_equal(g.labels(), ref) for g in ranks)
@@ -92,4 +97,7 @@ print(json.dumps(dict(
     single_tally_ms=round(one_sum, 4), single_over_P_ms=round(one_sum / P, 4),
     rank_max_tally_ms=round(sum(rank_max), 4),
     ratio_rank_max_over_single_div_P=round(sum(rank_max) / (one_sum / P), 3),
-    per_rank_tally_ms=[round(sum(x), 4) for x in per_rank])))
+    per_rank_tally_ms=[round(sum(x), 4) for x in per_rank],
+    # converged supersteps 5..10, per kernel: the single GPU and the slowest rank
+    single_converged_kernel_ms={k: round(sum(st["kernel_ms"][k] for st in one[3:]), 4) for k in TALLY},
+    rank_converged_kernel_ms={k: round(v, 4) for k, v in conv_k[max(range(P), key=lambda r: sum(per_rank[r][3:]))].items()})))

@@ -32,12 +32,17 @@ for s, e, n in rows:
         cur["kernels"][base] = round(cur["kernels"].get(base, 0.0) + ms, 4)
     elif cur is not None and base not in GROUP:
         cur = None
-single = groups[:REPS]
-ranks = groups[REPS:REPS + REPS * P]
+# layout (tools/rank_refresh.py): the single handle's build refresh, REPS superstep-1
+# refreshes, one superstep-2 refresh; the P rank handles' build refreshes, REPS x P
+# superstep-1 refreshes (rank order), P superstep-2 refreshes
+single = groups[1:1 + REPS]
+r0 = 1 + REPS + 1 + P
+ranks = groups[r0:r0 + REPS * P]
+assert len(groups) == r0 + REPS * P + P, (len(groups), r0 + REPS * P + P)
 per_rank = [statistics.median(ranks[k * P + r]["total_ms"] for k in range(REPS)) for r in range(P)]
 one = statistics.median(g["total_ms"] for g in single)
 print(json.dumps(dict(
     groups_found=len(groups), single_gpu_refresh_ms=round(one, 4), single_gpu_kernels=single[-1]["kernels"],
     per_rank_refresh_ms=[round(x, 4) for x in per_rank], rank_max_refresh_ms=round(max(per_rank), 4),
     single_over_P_ms=round(one / P, 4), ratio_rank_max_over_single_div_P=round(max(per_rank) / (one / P), 3),
-    rank0_kernels=ranks[-P]["kernels"] if ranks else None)))
+    rank_kernels_last_rep=[ranks[(REPS - 1) * P + r]["kernels"] for r in range(P)])))
