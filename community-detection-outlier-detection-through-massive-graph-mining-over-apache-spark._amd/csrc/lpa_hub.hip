@@ -845,6 +845,17 @@ __global__ __launch_bounds__(64 * kW) void k_hub_mid_all(const int32_t* __restri
 //     leaves no dirty line there -- it is written only by device atomics, which execute
 //     at the memory side -- so the write-back has nothing to do for it; 2048 blocks
 //     issuing it cost ~90 us per launch.
+//     Round 6 re-checked both forms.  ISA (hipcc -O3 -S, gfx950): an
+//     agent-scope release -- a `__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")` before
+//     the ticket, or the ticket RMW itself as release / acq_rel, with or without the
+//     "global" address-space qualifier -- lowers to `buffer_wbl2 sc1; s_waitcnt vmcnt(0)`
+//     ahead of the atomic in every form; no release form omits the L2 write-back.  The
+//     relaxed form keeps each wave's `s_waitcnt vmcnt(0)` (every wave's own atomics
+//     acknowledged: for device-scope atomics that is their completion at the memory side)
+//     and the workgroup barrier before thread 0's ticket.  Measured, same box, bench
+//     (profiles/r06/b_release_ab/, LPA_HUB_RELEASE=1 build, tickets acq_rel): C3 666.0 ->
+//     634.9 GTEPS (converged supersteps +15-28 us each: the write-backs flush the label
+//     stores of the concurrent bin kernels), C5 263.4 -> 262.3.  The relaxed form stays.
 // Tickets are two-level (kTicketGroups counters, one 64-B line each, then one for the
 // groups): returning atomics on ONE address serialise at ~88 M/s, 2048 of them ~23 us.
 // The producer side leans on gfx950 behaviour (device atomics on hipMalloc memory

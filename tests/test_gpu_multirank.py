@@ -249,3 +249,31 @@ def test_code_cut_g8_single_gpu(gfa, codemix22, monkeypatch):
         for _ in range(2):
             g.reset()
             assert np.array_equal(g.run(5), hist[4])
+
+
+@pytest.mark.parametrize("env", [{"LPA_GIANT_CODES": "0"}, {"LPA_POW2_SLICES": "0"}])
+def test_round6_switches_bit_exact(gfa, codemix22, monkeypatch, env):
+    """The round-6 switches: no giant-code refresh (LPA_GIANT_CODES=0:
+    the labels- / bits-mode rebuilds only), and tight slices at P > 1 (LPA_POW2_SLICES=0:
+    ceil(V / P) slots per rank, so the plain rebuild and no codes) -- bit-exact at
+    supersteps 1..5 on one GPU and on a P = 2 loopback group."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    V, sn, dn, hist = codemix22
+    with gfa.Graph(sn, dn, V) as g:
+        for t in range(5):
+            g.step(1)
+            if t == 0 and "LPA_GIANT_CODES" in env:
+                assert g.info()["code_refresh"] == 0
+            assert np.array_equal(g.labels(), hist[t]), f"{env} one GPU superstep {t + 1}"
+    lb, ranks = _group(gfa, sn, dn, V, 2)
+    try:
+        S = ranks[0].info()["slice"]
+        assert (S & (S - 1) == 0) == ("LPA_POW2_SLICES" not in env), S
+        got = _per_step_all_ranks(gfa, ranks, 5)
+        for r in range(2):
+            for t in range(5):
+                assert np.array_equal(got[r][t], hist[t]), f"{env} P=2 rank {r} superstep {t + 1}"
+        assert all(g.info()["code_refresh"] == 0 for g in ranks)
+    finally:
+        _close(lb, ranks)
