@@ -289,7 +289,6 @@ struct lpa_graph {
                                             //   but C3 (64 MB of labels) 0.9 ms slower
   lpa::u64* blk_pieces = nullptr;           // [n] (len << 32 | first position)
   int blk_classes = 8;                      // 8 x phases (kMaxBlkClasses at most)
-  int blk_bits = 0;                         // LPA_BLOCK_BITS=1: the bits-mode rebuild takes the pieces too
   int64_t blk_off[lpa::kMaxBlkClasses + 1] = {}; // class x: pieces [blk_off[x], blk_off[x + 1])
   int64_t blk_a0 = 0;                       // arcs [0, blk_a0) are listed (a multiple of 512)
   int64_t blk_rows = 0;                     // rows in (class, column) order

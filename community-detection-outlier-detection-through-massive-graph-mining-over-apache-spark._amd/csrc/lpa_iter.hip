@@ -2436,7 +2436,6 @@ struct BlkInfo {
   int64_t off[kMaxBlkClasses + 1];  // class x: pieces [off[x], off[x + 1]), multiples of 8
   int64_t a0;                       // listed arcs [0, a0) (0: no blocked part)
   int phases;                       // classes / 8: group x streams x, x + 8, ...
-  int bits_too;                     // the bits mode takes the pieces too (LPA_BLOCK_BITS)
 };
 template <typename P1, typename P2>
 __device__ __forceinline__ void rebuild_pieces(P1 p1, P2 p2, int32_t G, bool bits, const u64* __restrict__ pieces,
@@ -2591,10 +2590,10 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
     // wave's lanes then share one line)
     const u32 nhbu = (u32)nhb;
     auto run = [&](auto p1, auto p2, bool wbits) {
-      // uniform: labels / hybrid mode of a blocked handle (and, bits_too, the bits mode:
-      // its cold columns' bit words come from gbits, vpad / 8 bytes -- 5 MB at C5, past
-      // one XCD's L2 -- and a class's share of them stays resident)
-      if (pieces && (!bits || blk.bits_too)) {
+      // uniform: labels / hybrid mode of a blocked handle (the bits mode through the
+      // pieces measured slower, round 6: C5 superstep 3 13.4 -> 17.4 ms, C4 superstep 2
+      // 8.9 -> 12.8 ms -- its lookups hit LDS / L2 anyway, the split arc ranges cost)
+      if (!bits && pieces) {
         const int grp = blockIdx.x & 7;
         const int64_t nwv = (int64_t)(gridDim.x >> 3) * (blockDim.x >> 6);
         const int64_t wi = (int64_t)(blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -3981,7 +3980,6 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     for (int x = 0; x <= kMaxBlkClasses; ++x) binfo.off[x] = g->blk_off[x];
     binfo.a0 = blk ? g->blk_a0 : 0;
     binfo.phases = g->blk_classes / 8;
-    binfo.bits_too = g->blk_bits;
 #define LPA_HOT_LAUNCH(W, R)                                                                     \
   hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
                      g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \

@@ -660,8 +660,7 @@ def rmat22(gfa, oracle):
 
 @pytest.mark.parametrize("env", [{"LPA_BLOCK_DEG": "0"}, {"LPA_BLOCK_DEG": "8"}, {"LPA_BLOCK_DEG": "64"},
                                  {"LPA_BLOCK_DEG": "1000"}, {"LPA_BLOCK_DEG": "64", "LPA_LOCALITY": "0"},
-                                 {"LPA_BLOCK_DEG": "64", "LPA_BLOCK_BITS": "1"},
-                                 {"LPA_BLOCK_DEG": "64", "LPA_BLOCK_BITS": "1", "LPA_GIANT_CODES": "0"}])
+                                 {"LPA_BLOCK_DEG": "64", "LPA_GIANT_CODES": "0"}])
 def test_class_blocked_rebuild_bit_exact(gfa, rmat22, monkeypatch, env):
     """The class-blocked labels-mode al[] rebuild (rows of degree > LPA_BLOCK_DEG in
     (class, column) order, per-XCD class pieces -- 8 classes at this size, one phase per 8;
