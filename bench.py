@@ -469,7 +469,8 @@ def main():
     rb_work = [x for x in rb if x > 0.1]
     rb_bytes = 8 * info["arcs"] + 4 * info["V"]
     rb_traffic, rb_src = measured_traffic("k_al_rebuild_hot", config_id)
-    S = info["slice"]
+    # this rank's vertices (the slice is padded to a power of two at P > 1, lpa_build.hip)
+    S = -(-info["V"] // info["nranks"])
     iter_bytes = 8 * info["arcs"] + 12 * S + 8     # SURVEY §8(d) contract, this rank's share
     moved = moved_bytes_converged(info)
     # contract roofline of the whole job: every rank moves its share at 8 TB/s at once

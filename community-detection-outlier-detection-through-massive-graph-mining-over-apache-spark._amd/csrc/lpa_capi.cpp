@@ -91,6 +91,7 @@ void destroy(lpa_graph* g) {
                   g->glist, g->code2, g->al2};
   for (void* p : bufs) dev_free(g, p);
   if (g->h_flag) (void)hipHostFree(g->h_flag);
+  if (g->h_err) (void)hipHostFree(g->h_err);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : g->bin_ev)

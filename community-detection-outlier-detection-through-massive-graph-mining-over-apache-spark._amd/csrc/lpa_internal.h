@@ -266,6 +266,7 @@ struct lpa_graph {
   bool code3 = false;           // superstep 3 follows a giant-code refresh (read by the host
                                 //   before it: its schedule differs, see run_supersteps)
   int32_t* h_flag = nullptr;    // [1] pinned host word for that read
+  int32_t* h_err = nullptr;     // [1] pinned host copy of dev_err (read at the end of a call)
   unsigned long long* abits = nullptr;  // [arcs / 64] bit i = (al[i] == G): the bits-mode rebuild's by-product
   int64_t* cptr = nullptr;      // [vpad + 1] CSC: arcs of this rank whose column is u ...
   uint32_t* cpos = nullptr;     // [arcs]      ... are at positions cpos[cptr[u] .. cptr[u+1])

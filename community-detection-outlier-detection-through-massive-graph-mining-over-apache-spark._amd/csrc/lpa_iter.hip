@@ -4304,10 +4304,15 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
     ++g->since_reset;
   }
   if (timed) LPA_HIP(hipEventRecord(g->ev[2 * LPA_STATS_MAX_ITERS + 1], s));
+  // the kernel-side error word rides the final synchronisation (a stream-ordered copy
+  // into pinned memory instead of a blocking hipMemcpy after it: one round trip fewer)
+  if (n > 0) {
+    if (!g->h_err) LPA_HIP(hipHostMalloc((void**)&g->h_err, sizeof(int32_t), hipHostMallocDefault));
+    LPA_HIP(hipMemcpyAsync(g->h_err, g->dev_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  }
   LPA_HIP(hipStreamSynchronize(s));
   if (n > 0) {
-    int32_t err = 0;
-    LPA_HIP(hipMemcpy(&err, g->dev_err, sizeof(err), hipMemcpyDeviceToHost));
+    const int32_t err = *g->h_err;
     if (err) {
       // reported once per call: a later call on this handle starts clean
       LPA_HIP(hipMemset(g->dev_err, 0, sizeof(int32_t)));
