@@ -90,11 +90,6 @@ __device__ __forceinline__ u32 degree_bin(int32_t d) {
   return (u32)(11 - j);
 }
 
-__global__ void k_iota_i32(int32_t* __restrict__ out, int64_t n) {
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
-    out[k] = (int32_t)k;
-}
-
 __global__ void k_rank_of(const u64* __restrict__ keys, int64_t V, int32_t* __restrict__ rank_of) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < V;
        k += (int64_t)gridDim.x * blockDim.x)
@@ -498,18 +493,7 @@ int vertex_order(lpa_graph* g, int32_t V, int64_t m, bool locality) {
     for (int b = 0; b < blo; b += 8) shifts[ns++] = b;
     for (int b = 0; b < bhi; b += 8) shifts[ns++] = 32 + b;
     LPA_TRY(radix_sort_u64(vk, vk + V, V, shifts, ns, s));
-    if (locality && m > 0 && V < (1 << 28) && g->locality == 9) {
-      // (experiment) LPA_LOCALITY=9: within each bin below the hubs, input-id order
-      int32_t* idk = nullptr;
-      LPA_TRY(scratch_alloc(g, (void**)&idk, sizeof(int32_t) * (size_t)V));
-      hipLaunchKernelGGL(k_iota_i32, dim3(grid_for(V)), dim3(256), 0, s, idk, (int64_t)V);
-      hipLaunchKernelGGL(k_locality_keys, dim3(grid_for(V)), dim3(256), 0, s, vk, (int64_t)V, g->deg, idk,
-                         g->max_degree, 1, 1);
-      const int hi[4] = {32, 40, 48, 56};
-      LPA_TRY(radix_sort_u64(vk, vk + V, V, hi, 4, s));
-      LPA_HIP(hipGetLastError());
-      scratch_free(g, idk);
-    } else if (locality && m > 0 && V < (1 << 28)) {
+    if (locality && m > 0 && V < (1 << 28)) {
       const int K = g->locality < 4 ? g->locality : 4;  // neighbour keys (LPA_LOCALITY)
       int32_t* rank_of = nullptr;
       LPA_TRY(scratch_alloc(g, (void**)&rank_of, sizeof(int32_t) * (1 + K) * (size_t)V));
