@@ -662,7 +662,9 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
   // rank-strided form of a partitioned job: every rank codes its own arcs against the G
   // of the replicated vector), and a superstep 2 whose hub rows take the giant decision
   // (block mode, or no hub rows)
-  g->code_ok = g->codes_env && (P == 1 || rebuild_ranked(g)) && !g->gather && !g->pooled && !g->no_scatter && g->rebuild_hot &&
+  // (round 6: the outlier stage's pooled, rebuild-only L2 sub-graph too -- its second LPA
+  // from L0 collapses like the first, and every refresh there rebuilds anyway)
+  g->code_ok = g->codes_env && (P == 1 || rebuild_ranked(g)) && !g->gather && g->rebuild_hot &&
                g->vpad >= kHotMinSlots && g->arcs > 0 && (g->n_hub == 0 || g->hub_lane_begin < g->n_hub);
   if (g->code_ok) {
     // the rows of <= 64 arcs keep their labels when the label vector is small (C3: 64 MB,

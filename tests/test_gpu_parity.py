@@ -436,7 +436,7 @@ def test_outlier_vs_oracle(gfa, oracle, seed):
         assert o2["summary"]["n_flagged"] == summ2["n_flagged"]
 
 
-@pytest.mark.parametrize("case", ["mix_run", "mix_random_labels", "reciprocal_loops", "rmat_coarse"])
+@pytest.mark.parametrize("case", ["mix_run", "mix_random_labels", "reciprocal_loops", "rmat_coarse", "rmat22_codes"])
 def test_outlier_l2_subgraph_and_device(gfa, oracle, case):
     """The L2 sub-graph built straight from the distinct-edge orders (no arc sort):
     reciprocal pairs (u, v) + (v, u) (two arcs of the same column in a row), self-loops,
@@ -454,6 +454,11 @@ def test_outlier_l2_subgraph_and_device(gfa, oracle, case):
         loops = rng.integers(0, V - 200, size=300)
         s = np.concatenate([a, b, loops, a[:500]]).astype(np.int32)     # (a, b), (b, a), loops, dups
         d = np.concatenate([b, a, loops, b[:500]]).astype(np.int32)
+    elif case == "rmat22_codes":
+        # round 6: a sub-graph of >= 4 M slots, whose second LPA takes the giant-code
+        # refresh and settles (the main LPA's schedule on the pooled, rebuild-only handle)
+        ts, td = gfa.gen_rmat(22, 16, seed=9)
+        V, s, d = 1 << 22, ts.cpu().numpy(), td.cpu().numpy()
     else:
         ts, td = gfa.gen_rmat(15, 16, seed=4)
         V, s, d = 1 << 15, ts.cpu().numpy(), td.cpu().numpy()
@@ -462,6 +467,8 @@ def test_outlier_l2_subgraph_and_device(gfa, oracle, case):
             lab = rng.integers(0, 40, size=V).astype(np.int32)        # 40 arbitrary communities
         elif case == "rmat_coarse":
             lab = (g.run(2) % 97).astype(np.int32)
+        elif case == "rmat22_codes":
+            lab = g.run(10)
         else:
             lab = g.run(3)
         o1 = g.outlier(lab, "L1")
