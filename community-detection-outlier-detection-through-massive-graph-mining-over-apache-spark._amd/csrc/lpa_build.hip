@@ -405,19 +405,22 @@ __global__ void k_l2_degree(const int64_t* __restrict__ out_off, const int64_t* 
     deg[v] = o + n;
   }
 }
+// (al: each arc's L0 label -- its column's dense id -- written with the arc (round 6), so
+// the handle starts with al = L0[col] and init_labels runs no gather pass: 2.5 ms at C3)
 // arcs of row s from its intra out-edges, in place: row s's first dout[s] positions
 // (rows are the runs of the (s, d) order, so the per-row terms are cached loads; the
 // column's slot is one gather from new_of, 4 B per vertex, cache-resident)
 __global__ void k_l2_emit_out(const u64* __restrict__ ek, int64_t md, const uint8_t* __restrict__ mark,
                               const uint32_t* __restrict__ pos_out, const int64_t* __restrict__ out_off,
                               const int32_t* __restrict__ new_of, const int64_t* __restrict__ rp,
-                              int32_t* __restrict__ col) {
+                              int32_t* __restrict__ col, int32_t* __restrict__ al) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < md; i += (int64_t)gridDim.x * blockDim.x) {
     if (!mark[i]) continue;
     const u64 k = ek[i];
     const int32_t sv = (int32_t)(k >> 32);
     const int64_t p = rp[new_of[sv]] + (int64_t)(pos_out[i] - pos_out[out_off[sv]]);
     col[p] = new_of[(int32_t)(u32)k];
+    al[p] = (int32_t)(u32)k;   // the arc's L0 label: the column's dense id
   }
 }
 // arcs of row d from its intra in-edges, after its out-edges (de_t: d << 32 | index into
@@ -426,12 +429,14 @@ __global__ void k_l2_emit_in(const u64* __restrict__ et, const uint32_t* __restr
                              const uint8_t* __restrict__ mark, const uint32_t* __restrict__ pos_in,
                              const int64_t* __restrict__ in_off, const int32_t* __restrict__ dout,
                              const int32_t* __restrict__ new_of, const int64_t* __restrict__ rp,
-                             int32_t* __restrict__ col) {
+                             int32_t* __restrict__ col, int32_t* __restrict__ al) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < md; j += (int64_t)gridDim.x * blockDim.x) {
     if (!mark[j]) continue;
     const int32_t dv = (int32_t)(et[j] >> 32);
     const int64_t q = rp[new_of[dv]] + dout[dv] + (int64_t)(pos_in[j] - pos_in[in_off[dv]]);
-    col[q] = new_of[(int32_t)ets[j]];
+    const int32_t sv = (int32_t)ets[j];
+    col[q] = new_of[sv];
+    al[q] = sv;
   }
 }
 
@@ -467,6 +472,10 @@ int init_labels(lpa_graph* g) {
   g->prev_delta_ok = false;  // the exchange's delta chain restarts from L0
   if (g->al0) {              // al = L0[col] is al0: nothing to gather (lazy, see al0)
     g->al_pending = true;
+    return LPA_OK;
+  }
+  if (g->al_is_l0) {         // the L2 sub-graph's build wrote al = L0[col] with the arcs
+    g->al_is_l0 = false;
     return LPA_OK;
   }
   return rebuild_arc_labels(g);
@@ -530,7 +539,7 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
   const int32_t P = g->nranks, r = g->rank;
   const int64_t S = g->slice;
   const int64_t arcs = g->arcs;
-  LPA_TRY(dev_alloc(g, (void**)&g->al, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
+  if (!g->al) LPA_TRY(dev_alloc(g, (void**)&g->al, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
   {
     const int64_t nfl = (g->n_chunks + 16) / 16 * 16;
     LPA_TRY(dev_alloc(g, (void**)&g->chflag, nfl));
@@ -1024,15 +1033,17 @@ int build_graph_l2(lpa_graph* g, const lpa_graph* parent, const int32_t* L, cons
   // instantiation and destruction (~8 ms of host time at C3) for ~1 ms of launches
   g->use_graphs = 0;
   LPA_TRY(dev_alloc(g, (void**)&g->col, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
+  LPA_TRY(dev_alloc(g, (void**)&g->al, sizeof(int32_t) * (arcs > 0 ? arcs : 1)));
   LPA_TRY(dev_alloc(g, (void**)&g->cptr, sizeof(int64_t) * (g->vpad + 1)));
   LPA_HIP(hipMemcpyAsync(g->cptr, g->rp, sizeof(int64_t) * (S + 1), hipMemcpyDeviceToDevice, s));
   if (md > 0) {
     hipLaunchKernelGGL(k_l2_emit_out, dim3(grid_for(md)), dim3(256), 0, s, parent->de_keys, md, mo_c, pos_out,
-                       parent->de_out_off, g->new_of, g->rp, g->col);
+                       parent->de_out_off, g->new_of, g->rp, g->col, g->al);
     hipLaunchKernelGGL(k_l2_emit_in, dim3(grid_for(md)), dim3(256), 0, s, parent->de_t, parent->de_ts, md, mi,
-                       pos_in, parent->de_in_off, dout, g->new_of, g->rp, g->col);
+                       pos_in, parent->de_in_off, dout, g->new_of, g->rp, g->col, g->al);
     LPA_HIP(hipGetLastError());
   }
+  g->al_is_l0 = true;   // init_labels (finish_build) needs no rebuild
   if (mo) scratch_free(g, mo);
   scratch_free(g, mi);
   scratch_free(g, pos_out);

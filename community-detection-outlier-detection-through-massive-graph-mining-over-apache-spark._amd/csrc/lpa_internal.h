@@ -238,6 +238,7 @@ struct lpa_graph {
   // when it only scatters; any other first use copies al0 first (ensure_al).
   int32_t* al0 = nullptr;       // [arcs] or nullptr
   bool al_pending = false;
+  bool al_is_l0 = false;        // al holds L0[col] already (the L2 sub-graph's build writes it)
   uint32_t* gbits = nullptr;    // [vpad / 32] rebuild: bit u = (L[u] == G), the giant label
   int32_t* gword = nullptr;     // [8] G of the last refreshed vector (k_giant_pick), worth-trying flag,
                                 //     abits valid (bits-mode rebuild, no scatter since), [3] hot-slot
