@@ -688,8 +688,12 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
     for (int b = 0; b < g->code_lbin; ++b) g->code_pcut += g->bin_arcs[b];
     LPA_TRY(dev_alloc(g, (void**)&g->code2, sizeof(uint32_t) * (size_t)(g->vpad / 16)));
     LPA_TRY(dev_alloc(g, (void**)&g->al2, sizeof(uint32_t) * (size_t)(((g->code_pcut + 511) / 512 * 512 + 512) / 16)));
-    LPA_HIP(hipHostMalloc((void**)&g->h_flag, sizeof(int32_t), hipHostMallocDefault));
+    if (!g->h_flag) LPA_HIP(hipHostMalloc((void**)&g->h_flag, sizeof(int32_t), hipHostMallocDefault));
   }
+  // pinned words every handle reads through (the code-refresh flag, the kernel-error word
+  // at the end of a call); a handle that may parent an L2 sub-graph lends them to it
+  if (!g->h_flag) LPA_HIP(hipHostMalloc((void**)&g->h_flag, sizeof(int32_t), hipHostMallocDefault));
+  if (!g->h_err) LPA_HIP(hipHostMalloc((void**)&g->h_err, sizeof(int32_t), hipHostMallocDefault));
   LPA_HIP(hipStreamSynchronize(s));
   // the kept edge list serves the outlier stage (single-GPU handles) and lpa_quality,
   // which a distributed job runs on rank 0: the other ranks release it (at C5 over 8

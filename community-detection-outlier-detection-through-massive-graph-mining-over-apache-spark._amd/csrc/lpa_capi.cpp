@@ -23,8 +23,59 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+// carve bytes (256-B aligned) from the arena of the handle g allocates from; a block of
+// max(bytes, 256 MB) is added when the current ones are exhausted
+static int arena_alloc(lpa_graph* g, void** p, size_t bytes) {
+  lpa_graph* o = g->arena_from;
+  if (!o->arena) {
+    o->arena = new (std::nothrow) Arena();
+    if (!o->arena) {
+      set_error("host allocation failed");
+      return LPA_ENOMEM;
+    }
+  }
+  Arena& a = *o->arena;
+  bytes = (bytes + 255) & ~(size_t)255;
+  while (a.cur < a.nblocks && a.off + bytes > a.blocks[a.cur].bytes) {
+    ++a.cur;
+    a.off = 0;
+  }
+  if (a.cur == a.nblocks) {
+    if (a.nblocks == (int)(sizeof(a.blocks) / sizeof(a.blocks[0]))) {
+      set_error("L2 sub-graph arena: too many blocks");
+      return LPA_ENOMEM;
+    }
+    const size_t bb = bytes > ((size_t)256 << 20) ? bytes : ((size_t)256 << 20);
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bb);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("hipMalloc(%zu bytes) for the L2 arena failed: %s", bb, hipGetErrorString(e));
+      return LPA_ENOMEM;
+    }
+    a.blocks[a.nblocks++] = {static_cast<char*>(q), bb};
+    o->device_bytes += (int64_t)bb;
+    a.off = 0;
+  }
+  *p = a.blocks[a.cur].p + a.off;
+  a.off += bytes;
+  return LPA_OK;
+}
+
+void arena_reset(lpa_graph* owner) {
+  if (owner->arena) {
+    owner->arena->cur = 0;
+    owner->arena->off = 0;
+  }
+}
+
 int dev_alloc(lpa_graph* g, void** p, size_t bytes) {
   if (bytes == 0) bytes = 1;
+  if (g->arena_from) {
+    LPA_TRY(arena_alloc(g, p, bytes));
+    g->device_bytes += (int64_t)bytes;
+    return LPA_OK;
+  }
   if (g->pooled) {
     LPA_TRY(tmp_alloc(p, bytes, g->stream));
     g->device_bytes += (int64_t)bytes;
@@ -42,12 +93,13 @@ int dev_alloc(lpa_graph* g, void** p, size_t bytes) {
 }
 
 void dev_free(lpa_graph* g, void* p) {
-  if (!p) return;
+  if (!p || g->arena_from) return;   // arena memory goes back with the next reset
   if (g->pooled) tmp_free(p, g->stream);
   else (void)hipFree(p);
 }
 
 int scratch_alloc(lpa_graph* g, void** p, size_t bytes) {
+  if (g->arena_from) return arena_alloc(g, p, bytes > 0 ? bytes : 1);
   if (g->pooled) return tmp_alloc(p, bytes > 0 ? bytes : 1, g->stream);
   hipError_t e = hipMalloc(p, bytes > 0 ? bytes : 1);
   if (e != hipSuccess) {
@@ -60,7 +112,7 @@ int scratch_alloc(lpa_graph* g, void** p, size_t bytes) {
 }
 
 void scratch_free(lpa_graph* g, void* p) {
-  if (!p) return;
+  if (!p || g->arena_from) return;
   if (g->pooled) tmp_free(p, g->stream);
   else (void)hipFree(p);
 }
@@ -90,8 +142,14 @@ void destroy(lpa_graph* g) {
                   g->blk_pieces, g->gbits, g->ugc, g->umx, g->ulist2, g->gdec, g->gword, g->al0, g->abits,
                   g->glist, g->code2, g->al2};
   for (void* p : bufs) dev_free(g, p);
-  if (g->h_flag) (void)hipHostFree(g->h_flag);
-  if (g->h_err) (void)hipHostFree(g->h_err);
+  if (!g->borrowed) {   // a borrowing L2 sub-graph uses its parent's pinned words
+    if (g->h_flag) (void)hipHostFree(g->h_flag);
+    if (g->h_err) (void)hipHostFree(g->h_err);
+  }
+  if (g->arena) {
+    for (int i = 0; i < g->arena->nblocks; ++i) (void)hipFree(g->arena->blocks[i].p);
+    delete g->arena;
+  }
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : g->bin_ev)
@@ -207,6 +265,8 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
     g->ev_fork2 = borrow->ev_fork2;
     for (int i = 0; i < 3; ++i) g->ev_join2[i] = borrow->ev_join2[i];
     g->borrowed = true;
+    g->h_flag = borrow->h_flag;   // pinned words (hipHostFree costs ~1 ms per call)
+    g->h_err = borrow->h_err;
   } else {
     hipError_t e = hipSuccess;
     for (auto& st : g->aux_stream)
@@ -236,6 +296,10 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
       destroy(g);
       return LPA_ERCCL;
     }
+  }
+  if (l2_parent) {   // every array of the sub-graph from the parent's arena (reset here)
+    g->arena_from = const_cast<lpa_graph*>(l2_parent);
+    arena_reset(g->arena_from);
   }
   int rc = l2_parent ? build_graph_l2(g, l2_parent, l2_labels, l2_marks) : build_graph(g, src, dst, m, V, flags);
   if (rc == LPA_OK) rc = exchange_alloc(g);

@@ -116,6 +116,22 @@ struct DevBuf {
 
 struct Loopback;  // in-process collective over P handles on one device (lpa_comm.cpp)
 
+// Bump arena a handle keeps for the outlier stage's L2 sub-graph (round 6): every device
+// array of that per-call handle, scratch included, is carved from blocks the parent
+// keeps from call to call, so a call issues no hipMallocAsync / hipFreeAsync for them
+// (126 hipFreeAsync per L2 call at C3 blocked the host for 12.6 ms, one of them 4 ms).
+// Reset by each L2 build; released with the parent.
+struct Arena {
+  struct Block {
+    char* p;
+    size_t bytes;
+  };
+  Block blocks[32] = {};
+  int nblocks = 0;
+  int cur = 0;       // block being carved
+  size_t off = 0;    // offset in it
+};
+
 }  // namespace lpa
 
 struct lpa_graph {
@@ -346,6 +362,8 @@ struct lpa_graph {
 
   int64_t device_bytes = 0;
   bool pooled = false;                      // kFlagPooled: arrays from the stream-ordered pool
+  lpa::Arena* arena = nullptr;              // this handle's arena for its L2 sub-graphs (lazy)
+  lpa_graph* arena_from = nullptr;          // a pooled L2 sub-graph: allocate from this parent's arena
   bool no_scatter = false;                  // no CSC position index: every refresh rebuilds al[]
                                             //   (the outlier stage's 5-superstep L2 sub-graph)
   bool borrowed = false;                    // aux streams / fork-join events belong to a parent handle
