@@ -164,6 +164,9 @@ struct lpa_graph {
   int64_t V = 0, m = 0;
   int64_t slice = 0;      // vertex slots per rank (P > 1: a power of two, lpa_build)
   int pow2_slices = 1;    // LPA_POW2_SLICES=0: tight slices (ceil(V / P) rounded to 64)
+  int fused_bins = 1;     // LPA_FUSED_BINS: converged supersteps' bins in one launch per stream
+                          // (0: a launch per bin, 2: the wave bins keep theirs)
+  int conv_streams = 2;   // LPA_CONV_STREAMS: streams of a converged superstep's tally (1-3)
   int64_t vpad = 0;       // nranks * slice
   int64_t own_begin = 0;  // rank * slice
   int64_t n_own = 0;      // real (non-padding) vertices owned

@@ -553,6 +553,26 @@ __device__ __forceinline__ void group_row(const int64_t* __restrict__ rp, const 
   group_tally<G>(lab, Ln, v, live, lane, tab);
 }
 
+// (the bin bodies below take their block index and block count as arguments: a kernel
+// of its own passes blockIdx / gridDim, k_bins_fused its share of one launch)
+template <int G, bool kG = false>
+__device__ __forceinline__ void group_bin(int64_t bid, int64_t nblk, const int64_t* __restrict__ rp,
+                                          const int32_t* __restrict__ al, int32_t* __restrict__ Ln,
+                                          int64_t vbeg, int64_t vend, const int32_t* __restrict__ flist,
+                                          const int32_t* __restrict__ fcnt_b, const int32_t* __restrict__ fr_all,
+                                          const int32_t* __restrict__ Lg) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
+  // 64 / G rows per wave; grid-stride by waves (the grid is sized to the range: one pass)
+  constexpr int64_t kRows = 64 / G;
+  for (int64_t wb = (bid * 4 + w) * kRows; wb < br.n; wb += nblk * 4 * kRows) {
+    const int64_t i = wb + lane / G;
+    const bool live = i < br.n;
+    group_row<G, kG>(rp, al, Ln, live ? br.row(i) : 0, live, lane, nullptr, Lg);
+  }
+}
+
 template <int G, bool kG = false>
 __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ rp,
                                                    const int32_t* __restrict__ al,
@@ -561,16 +581,7 @@ __global__ __launch_bounds__(256) void k_lpa_group(const int64_t* __restrict__ r
                                                    const int32_t* __restrict__ fcnt_b,
                                                    const int32_t* __restrict__ fr_all,
                                                    const int32_t* __restrict__ Lg) {
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
-  // 64 / G rows per wave; grid-stride by waves (the grid is sized to the range: one pass)
-  constexpr int64_t kRows = 64 / G;
-  for (int64_t wb = ((int64_t)blockIdx.x * 4 + w) * kRows; wb < br.n; wb += (int64_t)gridDim.x * 4 * kRows) {
-    const int64_t i = wb + lane / G;
-    const bool live = i < br.n;
-    group_row<G, kG>(rp, al, Ln, live ? br.row(i) : 0, live, lane, nullptr, Lg);
-  }
+  group_bin<G, kG>(blockIdx.x, gridDim.x, rp, al, Ln, vbeg, vend, flist, fcnt_b, fr_all, Lg);
 }
 
 // ---------------------------------------------------------------------------
@@ -715,29 +726,27 @@ constexpr int wave_ring_depth() { return NC <= 2 ? 6 : NC <= 4 ? 4 : 3; }
 // bins w2 / w4 / w8 / w16 (64 < deg <= 64 * NC): one wave per row, grid-stride; D
 // label register sets in an unrolled ring (labels D - 1 rows ahead), row bounds by
 // 64-row batches one batch ahead (span_batch).
+// (tab_all / lst_all: the block's LDS, 4 waves x 2 * 64 * NC table slots / 64 * NC
+// list entries)
 template <int NC, bool kG = false>
-__global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp,
-                                                  const int32_t* __restrict__ al,
-                                                  int32_t* __restrict__ Ln, int64_t vbeg,
-                                                  int64_t vend, const int32_t* __restrict__ flist,
-                                                  const int32_t* __restrict__ fcnt_b,
-                                                  const int32_t* __restrict__ fr_all, int pmax,
-                                                  const int32_t* __restrict__ gsel,
-                                                  const int32_t* __restrict__ Lg) {
+__device__ __forceinline__ void wave_bin(int64_t bid, int64_t nblk, u64* tab_all, uint16_t* lst_all,
+                                         const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
+                                         int32_t* __restrict__ Ln, int64_t vbeg, int64_t vend,
+                                         const int32_t* __restrict__ flist, const int32_t* __restrict__ fcnt_b,
+                                         const int32_t* __restrict__ fr_all, int pmax,
+                                         const int32_t* __restrict__ gsel, const int32_t* __restrict__ Lg) {
   constexpr int kCap = 2 * 64 * NC;
   constexpr int D = wave_ring_depth<NC>();
   static_assert(D >= 2 && D <= 64, "ring depth");
-  __shared__ u64 tab_all[4][kCap];
-  __shared__ uint16_t lst_all[4][64 * NC];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  u64* tab = tab_all[w];
-  uint16_t* lst = lst_all[w];
+  u64* tab = tab_all + w * kCap;
+  uint16_t* lst = lst_all + w * 64 * NC;
   const u64 lt = (1ull << lane) - 1ull;
-  const int64_t stride = (int64_t)gridDim.x * 4;
+  const int64_t stride = nblk * 4;
   const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
-  int64_t ib = (int64_t)blockIdx.x * 4 + w;   // work item of the current batch's lane 0
-  if (ib >= br.n) return;  // no block-level barriers in this kernel
+  int64_t ib = bid * 4 + w;   // work item of the current batch's lane 0
+  if (ib >= br.n) return;  // no block-level barriers in this body
   for (int k = lane; k < kCap; k += 64) tab[k] = 0ull;  // only waves with rows clear
   // gsel (label-dense supersteps): the giant-label word of the labels this superstep
   // reads (k_giant_pick: label, worth trying)
@@ -768,6 +777,21 @@ __global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp
       }
     }
   }
+}
+
+template <int NC, bool kG = false>
+__global__ __launch_bounds__(256) void k_lpa_wave(const int64_t* __restrict__ rp,
+                                                  const int32_t* __restrict__ al,
+                                                  int32_t* __restrict__ Ln, int64_t vbeg,
+                                                  int64_t vend, const int32_t* __restrict__ flist,
+                                                  const int32_t* __restrict__ fcnt_b,
+                                                  const int32_t* __restrict__ fr_all, int pmax,
+                                                  const int32_t* __restrict__ gsel,
+                                                  const int32_t* __restrict__ Lg) {
+  __shared__ u64 tab_all[4 * 2 * 64 * NC];
+  __shared__ uint16_t lst_all[4 * 64 * NC];
+  wave_bin<NC, kG>(blockIdx.x, gridDim.x, tab_all, lst_all, rp, al, Ln, vbeg, vend, flist, fcnt_b, fr_all, pmax,
+                   gsel, Lg);
 }
 
 // ---------------------------------------------------------------------------
@@ -972,31 +996,31 @@ __device__ __forceinline__ void rows_labels_nb(u32 (&lab)[kChunks], u32& vbits, 
   asm volatile("" : "+v"(vbits));  // computed here: not sunk to the tally (64-bit bounds would stay live)
 }
 
+constexpr int kRowsGB = 16;  // giant-label histogram buckets per row (group) of k_lpa_rows
+
+// (htab_all / ghist_all: the block's LDS, 4 waves x kRowsHashSlots table slots /
+// 64 / G * kRowsGB histogram buckets)
 template <int G, bool kG = false>
-__global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp,
-                                                  const int32_t* __restrict__ al,
-                                                  int32_t* __restrict__ Ln, int64_t vbeg,
-                                                  int64_t vend, const int32_t* __restrict__ flist,
-                                                  const int32_t* __restrict__ fcnt_b,
-                                                  const int32_t* __restrict__ fr_all, int sort_after,
-                                                  const int32_t* __restrict__ gsel,
-                                                  const int32_t* __restrict__ Lg) {
+__device__ __forceinline__ void rows_bin(int64_t bid, int64_t nblk, u64* htab_all, u32* ghist_all,
+                                         const int64_t* __restrict__ rp, const int32_t* __restrict__ al,
+                                         int32_t* __restrict__ Ln, int64_t vbeg, int64_t vend,
+                                         const int32_t* __restrict__ flist, const int32_t* __restrict__ fcnt_b,
+                                         const int32_t* __restrict__ fr_all, int sort_after,
+                                         const int32_t* __restrict__ gsel, const int32_t* __restrict__ Lg) {
   static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "lane width");
   constexpr int RB = 512 / G;  // rows per batch
-  constexpr int kGB = 16;      // giant-label histogram buckets per row (group)
-  __shared__ u32 ghist_all[4][64 / G * kGB];
-  __shared__ u64 htab_all[4][kRowsHashSlots];
+  constexpr int kGB = kRowsGB;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  u64* htab = htab_all[w];
+  u64* htab = htab_all + w * kRowsHashSlots;
 #pragma unroll
   for (int k = 0; k < kRowsHashSlots / 64; ++k) htab[k * 64 + lane] = 0ull;
   if (!*fr_all) {
     // frontier: the listed dirty rows, G lanes each (rows are not consecutive, so
     // no batched offsets); every lane of a wave runs every trip (ballot peel)
     const BinRows br = bin_rows(vbeg, vend, flist, fcnt_b, fr_all);
-    const int64_t per = 64 / G, nw = (int64_t)gridDim.x * 4;
-    for (int64_t i0 = ((int64_t)blockIdx.x * 4 + w) * per; i0 < br.n; i0 += nw * per) {
+    const int64_t per = 64 / G, nw = nblk * 4;
+    for (int64_t i0 = (bid * 4 + w) * per; i0 < br.n; i0 += nw * per) {
       const int64_t i = i0 + lane / G;
       const bool live = i < br.n;
       group_row<G, kG>(rp, al, Ln, live ? br.row(i) : 0, live, lane, htab, Lg);
@@ -1004,15 +1028,15 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
     return;
   }
   const int64_t nb = (vend - vbeg + RB - 1) / RB;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  int64_t bi = (int64_t)blockIdx.x * 4 + w;
-  if (bi >= nb) return;  // no block-level barriers in this kernel
+  const int64_t stride = nblk * 4;
+  int64_t bi = bid * 4 + w;
+  if (bi >= nb) return;  // no block-level barriers in this body
   // gsel (superstep 2, rows of > 8 arcs): a chunk whose every row is decided for the
   // giant label (its exact count above each of the row's kGB label-hash buckets of
   // other votes, as giant_decide) skips the peel / hash
   const bool giant = G >= 16 && gsel != nullptr && gsel[1] != 0;
   const u32 Gl = giant ? (u32)gsel[0] : 0u;
-  u32* hg = &ghist_all[w][(lane / G) * kGB];
+  u32* hg = ghist_all + w * (64 / G * kGB) + (lane / G) * kGB;
   const int gj = lane & (G - 1);   // G >= kGB when giant: lane gj < kGB owns bucket gj
   if (gj < kGB) hg[gj] = 0u;
   if constexpr (G == 64 && !kG) {
@@ -1191,6 +1215,75 @@ __global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp
     }
   }
   }
+  }
+}
+
+template <int G, bool kG = false>
+__global__ __launch_bounds__(256) void k_lpa_rows(const int64_t* __restrict__ rp,
+                                                  const int32_t* __restrict__ al,
+                                                  int32_t* __restrict__ Ln, int64_t vbeg,
+                                                  int64_t vend, const int32_t* __restrict__ flist,
+                                                  const int32_t* __restrict__ fcnt_b,
+                                                  const int32_t* __restrict__ fr_all, int sort_after,
+                                                  const int32_t* __restrict__ gsel,
+                                                  const int32_t* __restrict__ Lg) {
+  __shared__ u32 ghist_all[4 * (64 / G) * kRowsGB];
+  __shared__ u64 htab_all[4 * kRowsHashSlots];
+  rows_bin<G, kG>(blockIdx.x, gridDim.x, htab_all, ghist_all, rp, al, Ln, vbeg, vend, flist, fcnt_b, fr_all,
+                  sort_after, gsel, Lg);
+}
+
+// ---------------------------------------------------------------------------
+// The converged supersteps' bins in one launch per stream (round 6): blocks
+// [off[k], off[k + 1]) run sub-launch k's bin body with that share as their grid --
+// the same blocks, lists and ranges as the kernels of their own, minus the launch
+// and drain of every kernel boundary in the stream's chain (a converged superstep's
+// bins tally ~0.2 % of the rows: each of their launches was mostly fixed cost).
+// kWide: 1 = the wave bins w16 / w8 / w4 (aux0), 0 = w2 and the row / group bins
+// (aux1).
+// ---------------------------------------------------------------------------
+#ifndef LPA_FUSED_WAVES
+#define LPA_FUSED_WAVES 5  // waves per SIMD the register budget is set for
+#endif
+constexpr int kFusedMax = 8;
+struct FusedBins {
+  int n;
+  int bin[kFusedMax];
+  int32_t off[kFusedMax + 1];
+  int64_t vb[kFusedMax], ve[kFusedMax];
+};
+
+template <int kWide>
+__global__ __launch_bounds__(256, LPA_FUSED_WAVES) void k_bins_fused(const FusedBins fb, const int64_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ al, int32_t* __restrict__ Ln,
+                                                    const int32_t* __restrict__ flist,
+                                                    const int32_t* __restrict__ fcnt,
+                                                    const int32_t* __restrict__ fr_all, int pmax, int sort_after) {
+  constexpr int kNC = kWide ? 16 : 2;  // the widest wave bin of the launch
+  __shared__ u64 tab[4 * (2 * 64 * kNC > kRowsHashSlots ? 2 * 64 * kNC : kRowsHashSlots)];
+  __shared__ uint16_t lst[4 * 64 * kNC];
+  __shared__ u32 gh[kWide ? 1 : 4 * (64 / 8) * kRowsGB];
+  int k = 0;
+  while (k + 1 < fb.n && (int32_t)blockIdx.x >= fb.off[k + 1]) ++k;  // uniform
+  const int64_t bid = (int64_t)blockIdx.x - fb.off[k], nblk = fb.off[k + 1] - fb.off[k];
+  const int b = fb.bin[k];
+  const int64_t v0 = fb.vb[k], v1 = fb.ve[k];
+  const int32_t* fc = fcnt + b;
+  if constexpr (kWide) {
+    if (b == BIN_W16) wave_bin<16>(bid, nblk, tab, lst, rp, al, Ln, v0, v1, flist, fc, fr_all, pmax, nullptr, nullptr);
+    else if (b == BIN_W8) wave_bin<8>(bid, nblk, tab, lst, rp, al, Ln, v0, v1, flist, fc, fr_all, pmax, nullptr, nullptr);
+    else wave_bin<4>(bid, nblk, tab, lst, rp, al, Ln, v0, v1, flist, fc, fr_all, pmax, nullptr, nullptr);
+  } else {
+    switch (b) {
+      case BIN_W2: wave_bin<2>(bid, nblk, tab, lst, rp, al, Ln, v0, v1, flist, fc, fr_all, pmax, nullptr, nullptr); break;
+      case BIN_G64: rows_bin<64>(bid, nblk, tab, gh, rp, al, Ln, v0, v1, flist, fc, fr_all, sort_after, nullptr, nullptr); break;
+      case BIN_G32: rows_bin<32>(bid, nblk, tab, gh, rp, al, Ln, v0, v1, flist, fc, fr_all, sort_after, nullptr, nullptr); break;
+      case BIN_G16: rows_bin<16>(bid, nblk, tab, gh, rp, al, Ln, v0, v1, flist, fc, fr_all, sort_after, nullptr, nullptr); break;
+      case BIN_G8: rows_bin<8>(bid, nblk, tab, gh, rp, al, Ln, v0, v1, flist, fc, fr_all, sort_after, nullptr, nullptr); break;
+      case BIN_G4: group_bin<4>(bid, nblk, rp, al, Ln, v0, v1, flist, fc, fr_all, nullptr); break;
+      case BIN_G2: group_bin<2>(bid, nblk, rp, al, Ln, v0, v1, flist, fc, fr_all, nullptr); break;
+      default: group_bin<1>(bid, nblk, rp, al, Ln, v0, v1, flist, fc, fr_all, nullptr); break;
+    }
   }
 }
 
@@ -3554,7 +3647,12 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // kernel trace shows each kernel's standalone duration
   // (three streams in every superstep, the converged ones too: 2 or 1 measured slower,
   // the bin chains' overlap is worth more than the fork / join dependencies)
-  const int nstr = g->serial ? 1 : 3;
+  // (converged supersteps with the frontier on: g->conv_streams, LPA_CONV_STREAMS --
+  // their captured graphs pay a cross-queue dependency per node, ~3.5 us, where a
+  // one-queue chain pays ~1.9: tools/microbench/mb_launch.hip.  With the frontier off
+  // every superstep tallies every row, and the bins' overlap on three streams pays)
+  const bool conv = g->since_reset >= kDenseSupersteps + 2 && g->frontier;
+  const int nstr = g->serial ? 1 : conv ? g->conv_streams : 3;
   hipStream_t sb = nstr >= 2 ? g->aux_stream[0] : s;
   hipStream_t sc = nstr >= 3 ? g->aux_stream[1] : sb;
   const int64_t* bb = g->bin_begin;
@@ -3850,6 +3948,64 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // row/group bins (round 4: superstep 2's tail bins g16 .. g1 on the main stream, ahead
   // of the hub combine, measured slower -- 2.08 -> 2.11 ms)
   hipStream_t st_tail = sc;
+  // converged supersteps (captured graphs, frontier lists): each bin stream's chain as
+  // one k_bins_fused launch -- the same blocks per bin as the kernels of their own
+  // (group bins capped like the others: their bodies grid-stride).  Not with the
+  // frontier off: every superstep is then in range mode, where the fused launch's
+  // register / LDS budget (the largest bin's) costs the narrow bins occupancy
+  const bool fused = g->fused_bins && conv && !gnow && !settle4 && !code_tally_now(g) && !code_tally3_now(g) &&
+                     gsel == nullptr;
+  auto launch_fused = [&](int wide, hipStream_t st) -> int {
+    const int b0 = wide ? BIN_W16 : BIN_W2, b1 = wide ? BIN_W2 : BIN_ISO;
+    FusedBins fb{};
+    int32_t tot = 0;
+    for (int b = b0; b < b1; ++b) {
+      const int64_t n = bb[b + 1] - bb[b];
+      if (n <= 0) continue;
+      int64_t want;
+      if (b <= BIN_W2) {
+        want = (n + 3) / 4;
+      } else if (b <= BIN_G8) {
+        const int64_t rb = 512 / (64 >> (b - BIN_G64));
+        want = ((n + rb - 1) / rb + 3) / 4;
+      } else {
+        want = (n * (4 >> (b - BIN_G4)) + 255) / 256;
+      }
+      fb.bin[fb.n] = b;
+      fb.vb[fb.n] = bb[b];
+      fb.ve[fb.n] = bb[b + 1];
+      fb.off[fb.n] = tot;
+      tot += (int32_t)cap_grid(want, 2048);
+      ++fb.n;
+    }
+    fb.off[fb.n] = tot;
+    LPA_TRY(mark(2 * (b0 + 1), st));
+    if (fb.n > 0) {
+      if (wide)
+        hipLaunchKernelGGL(k_bins_fused<1>, dim3((unsigned)tot), dim3(256), 0, st, fb, g->rp, g->al, Lown, g->flist,
+                           fcnt, fr_bins, pmax, sort_after);
+      else
+        hipLaunchKernelGGL(k_bins_fused<0>, dim3((unsigned)tot), dim3(256), 0, st, fb, g->rp, g->al, Lown, g->flist,
+                           fcnt, fr_bins, pmax, sort_after);
+      LPA_HIP(hipGetLastError());
+    }
+    LPA_TRY(mark(2 * (b0 + 1) + 1, st));
+    for (int b = b0 + 1; b < b1; ++b) {  // (serialized stats: the launch counts under its first bin)
+      LPA_TRY(mark(2 * (b + 1), st));
+      LPA_TRY(mark(2 * (b + 1) + 1, st));
+    }
+    return LPA_OK;
+  };
+  if (fused) {
+    if (g->fused_bins == 2) {  // the wave bins keep their own launches
+      LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_wave)
+      LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_wave)
+      LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_wave)
+    } else {
+      LPA_TRY(launch_fused(1, sb));
+    }
+    LPA_TRY(launch_fused(0, sc));
+  } else {
   LPA_WAVE_LAUNCH(BIN_W16, 16, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W8, 8, sb, fr_wave)
   LPA_WAVE_LAUNCH(BIN_W4, 4, sb, fr_wave)
@@ -3874,6 +4030,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     LPA_GROUP_LAUNCH(BIN_G2, 2, st_tail)
     LPA_GROUP_LAUNCH(BIN_G1, 1, st_tail)
   }
+  }
 #undef LPA_ROWS_LAUNCH
 #undef LPA_GROUP_LAUNCH
 #undef LPA_WAVE_LAUNCH
@@ -3897,10 +4054,14 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     const int dm = dense_refresh(g) ? 1 : 0;
     // (the split between the two bin streams follows where w2 ran)
     const int bw = code_tally_now(g) ? BIN_G64 : BIN_W2;
+    if (nstr == 1 && !g->serial) {  // one stream: one diff over every bin
+      LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_ISO], false, g->par, BIN_SEG, BIN_ISO, dm));
+    } else {
     LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[bw], false, g->par, BIN_W16, bw, dm));
     // isolated slots (and the padding) never change: the diff stops at the isolated bin
     LPA_TRY(launch_diff(g, sc, Lc, Ln, bb[bw], bb[BIN_ISO], false, g->par, bw, BIN_ISO, dm));
     LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par, BIN_SEG, BIN_W16, dm));
+    }
   }
   if (sb != s) {
     LPA_HIP(hipEventRecord(g->ev_join[0], sb));
