@@ -1352,14 +1352,20 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join, bool g
     LPA_HIP(hipStreamWaitEvent(sd, g->ev_fork2, 0));
     LPA_TRY(bucket_path());
   }
-  if (hl < n && !block_mode_now(g)) {  // block mode: k_lpa_block tallied these rows
+  // converged supersteps with the frontier on (a few listed rows): k_hub_small takes the
+  // lane-path rows too, one dependent launch fewer on the main stream's chain (same box:
+  // C3 converged supersteps -4 us each, C4 -15 us; a range-mode one -- C5's superstep 5
+  // -- +0.09 ms, its many small hub rows a wave each)
+  const bool all_small = !fork && fused_now(g);
+  const int64_t hd = all_small ? n : hc;
+  if (hl < n && !block_mode_now(g) && !all_small) {  // block mode: k_lpa_block tallied these rows
     hipLaunchKernelGGL(k_hub_lanes, dim3(grid_cap((n - hl + 255) / 256, 2048)), dim3(256), 0, s, hl, n,
                        g->rp, g->hub_uoff, g->ucnt, g->stage, Lown, lists, n, g->hub_wcount, lcnt,
                        g->flist, g->fcnt + 16 * g->par, g->fr_all + g->par);
     LPA_HIP(hipGetLastError());
   }
   // direct rows [0, nd) when not forked: in block mode only those above the block tiers
-  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, fork ? (int64_t)0 : hc, n, g->rp,
+  hipLaunchKernelGGL(k_hub_small, dim3(2048), dim3(256), 0, s, fork ? (int64_t)0 : hd, n, g->rp,
                      g->hub_uoff, g->ucnt, g->stage, g->hub_wcount, Lown, lists, lcnt, g->items_cb,
                      g->items_cc, g->flist, g->fcnt + 16 * g->par, g->fr_all + g->par);
   LPA_HIP(hipGetLastError());

@@ -418,6 +418,7 @@ int launch_hub_combine(lpa_graph* g, int32_t* Lown, bool fork, bool join = true,
                        bool giant = false);  // lpa_hub.hip
 int launch_hub_decide(lpa_graph* g, int32_t* Lown, int64_t h_end, const int32_t* gsel);  // lpa_hub.hip
 bool block_mode_now(const lpa_graph* g);  // lpa_iter.hip
+bool fused_now(const lpa_graph* g);       // lpa_iter.hip
 int64_t block_rows_begin(const lpa_graph* g);  // first row of the block tiers (lpa_iter.hip)
 int rebuild_arc_labels(lpa_graph* g);  // al[i] = lab[cur][col[i]]
 // the caller-driven full exchange (lpa_exchange_put) completes the superstep just run:

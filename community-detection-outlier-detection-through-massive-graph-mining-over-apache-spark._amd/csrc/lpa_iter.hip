@@ -3953,8 +3953,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
   // (group bins capped like the others: their bodies grid-stride).  Not with the
   // frontier off: every superstep is then in range mode, where the fused launch's
   // register / LDS budget (the largest bin's) costs the narrow bins occupancy
-  const bool fused = g->fused_bins && conv && !gnow && !settle4 && !code_tally_now(g) && !code_tally3_now(g) &&
-                     gsel == nullptr;
+  const bool fused = fused_now(g);
   auto launch_fused = [&](int wide, hipStream_t st) -> int {
     const int b0 = wide ? BIN_W16 : BIN_W2, b1 = wide ? BIN_W2 : BIN_ISO;
     FusedBins fb{};
@@ -3989,11 +3988,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
                            fcnt, fr_bins, pmax, sort_after);
       LPA_HIP(hipGetLastError());
     }
-    LPA_TRY(mark(2 * (b0 + 1) + 1, st));
-    for (int b = b0 + 1; b < b1; ++b) {  // (serialized stats: the launch counts under its first bin)
-      LPA_TRY(mark(2 * (b + 1), st));
-      LPA_TRY(mark(2 * (b + 1) + 1, st));
-    }
+    LPA_TRY(mark(2 * (b0 + 1) + 1, st));  // (serialized stats: the launch counts under its first bin)
     return LPA_OK;
   };
   if (fused) {
@@ -4056,6 +4051,9 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     const int bw = code_tally_now(g) ? BIN_G64 : BIN_W2;
     if (nstr == 1 && !g->serial) {  // one stream: one diff over every bin
       LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_ISO], false, g->par, BIN_SEG, BIN_ISO, dm));
+    } else if (nstr == 2) {  // the bins' stream: one diff over its bins
+      LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[BIN_ISO], false, g->par, BIN_W16, BIN_ISO, dm));
+      LPA_TRY(launch_diff(g, s, Lc, Ln, 0, bb[BIN_W16], false, g->par, BIN_SEG, BIN_W16, dm));
     } else {
     LPA_TRY(launch_diff(g, sb, Lc, Ln, bb[BIN_W16], bb[bw], false, g->par, BIN_W16, bw, dm));
     // isolated slots (and the padding) never change: the diff stops at the isolated bin
@@ -4286,6 +4284,11 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
 
 }  // namespace
 
+// the converged supersteps' bins as one k_bins_fused launch per stream (launch_tally)
+bool fused_now(const lpa_graph* g) {
+  return g->fused_bins && g->frontier && g->since_reset >= kDenseSupersteps + 2 && !gather_now(g);
+}
+
 // (the caller-driven delta exchange, lpa_exchange_put_delta: the refresh of the superstep
 // lpa_step just ran, which since_reset already counts -- it is seen as the in-library
 // refresh of that superstep sees it: dense / code-settled supersteps, code refresh allowed)
@@ -4336,8 +4339,10 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
   // k (k < kTallyKernels), then kTallyEv after the join, +1 after the exchange, +2
   // after the diff + scatter, +3 after the rebuild, +4 / +5 around the frontier lists
   bool blk_ran[LPA_STATS_MAX_ITERS] = {};  // serialized stats: k_lpa_block ran in superstep t
+  bool fus_ran[LPA_STATS_MAX_ITERS] = {};  // ... the fused bins (no marks of the other bins)
   for (int32_t t = 0; t < n; ++t) {
     if (t < nt) blk_ran[t] = block_mode_now(g);
+    if (t < nt) fus_ran[t] = fused_now(g);
     const int32_t* Lc = g->lab[g->cur];
     int32_t* Ln = g->lab[g->cur ^ 1];
     int32_t* Lown = Ln + g->own_begin;
@@ -4491,6 +4496,8 @@ int run_supersteps(lpa_graph* g, int32_t n, lpa_stats* st, bool last_refresh) {
       hipEvent_t* bev = &g->bin_ev[t * kBinEvents];
       float ms;
       for (int k = 0; k < kTallyKernels; ++k) {
+        if (fus_ran[t] && (k > BIN_W2 + 1 || (g->fused_bins != 2 && (k == BIN_W8 + 1 || k == BIN_W4 + 1))))
+          continue;  // a bin inside a fused launch (no marks of its own)
         LPA_HIP(hipEventElapsedTime(&ms, bev[2 * k], bev[2 * k + 1]));
         st->kernel_ms[k] += ms;
       }
