@@ -71,19 +71,21 @@ MAX_ITER = 10
 
 def superstep_traffic(kernel, superstep, config_id):
     """HBM bytes of `kernel`'s launch(es) in superstep `superstep` of a labelPropagation(10)
-    call from the round-5 per-config PMC summary (tools/pmc_r05.sh ->
-    profiles/r05/traffic/pmc_traffic_<config>.json), or (None, None)."""
-    path = os.path.join(ROOT, "profiles", "r05", "traffic", f"pmc_traffic_{config_id}.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)
-        per = t["per_superstep"]
-        # keys carry template arguments ("k_al_rebuild_hot<true, false>"): match the base name
-        key = next(k for k in per if k.split("<")[0] == kernel)
-        e = per[key][f"superstep_{superstep}"]
-    except (OSError, ValueError, KeyError, StopIteration):
-        return None, None
-    return e["traffic_bytes"], os.path.relpath(path, ROOT)
+    call from the newest per-config PMC summary (tools/pmc_r05.sh ->
+    profiles/r06/traffic/ or profiles/r05/traffic/pmc_traffic_<config>.json), or (None, None)."""
+    for rnd in ("r06", "r05"):
+        path = os.path.join(ROOT, "profiles", rnd, "traffic", f"pmc_traffic_{config_id}.json")
+        try:
+            with open(path) as f:
+                t = json.load(f)
+            per = t["per_superstep"]
+            # keys carry template arguments ("k_al_rebuild_hot<true, false>"): match the base name
+            key = next(k for k in per if k.split("<")[0] == kernel)
+            e = per[key][f"superstep_{superstep}"]
+        except (OSError, ValueError, KeyError, StopIteration):
+            continue
+        return e["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def measured_traffic(kernel, config_id):
