@@ -464,6 +464,7 @@ int init_labels(lpa_graph* g) {
   LPA_HIP(hipMemsetAsync(g->counters, 0, sizeof(unsigned long long) * 8, g->stream));
   if (g->gword) {
     LPA_HIP(hipMemsetAsync(g->gword + 2, 0, sizeof(int32_t), g->stream));  // abits stale
+    LPA_HIP(hipMemsetAsync(g->gword + 9, 0, sizeof(int32_t), g->stream));  // no abits pass ran
     LPA_HIP(hipMemsetAsync(g->gword + 5, 0, sizeof(int32_t), g->stream));  // no giant-code refresh pending
   }
   g->cur = 0;
@@ -645,8 +646,8 @@ int finish_build(lpa_graph* g, int32_t* deg_own, int64_t m) {
 
   // ---- labels (replicated, ping-pong) ----
   LPA_TRY(dev_alloc(g, (void**)&g->gbits, sizeof(uint32_t) * ((g->vpad + 63) / 64 * 2)));
-  LPA_TRY(dev_alloc(g, (void**)&g->gword, sizeof(int32_t) * 8));
-  LPA_HIP(hipMemsetAsync(g->gword, 0, sizeof(int32_t) * 8, s));
+  LPA_TRY(dev_alloc(g, (void**)&g->gword, sizeof(int32_t) * 16));
+  LPA_HIP(hipMemsetAsync(g->gword, 0, sizeof(int32_t) * 16, s));
   LPA_TRY(dev_alloc(g, (void**)&g->abits, sizeof(unsigned long long) * ((g->arcs + 63) / 64 + 1)));
   LPA_TRY(dev_alloc(g, (void**)&g->lab[0], sizeof(int32_t) * g->vpad));
   LPA_TRY(dev_alloc(g, (void**)&g->lab[1], sizeof(int32_t) * g->vpad));

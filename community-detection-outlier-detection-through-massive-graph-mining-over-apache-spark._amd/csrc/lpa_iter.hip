@@ -1888,7 +1888,7 @@ __global__ __launch_bounds__(256) void k_frontier_lists(uint8_t* __restrict__ rd
 // block before k_settle_commit changes fr_all.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool settle_on(const int32_t* fr_all, const int32_t* gword) {
-  return *fr_all != 0 && gword[1] != 0 && gword[2] != 0;
+  return *fr_all != 0 && gword[1] != 0 && (gword[2] != 0 || gword[9] != 0);
 }
 
 __device__ __forceinline__ unsigned long long range_mask(int64_t x, int64_t w0, int64_t w1, int64_t a, int64_t b) {
@@ -1950,12 +1950,16 @@ __global__ __launch_bounds__(256) void k_settle_rows(const int64_t* __restrict__
 // 3 (after superstep 3 nearly every row's strict majority is G: R-MAT 100 % of the arcs).
 // One streaming pass over 4 B/arc (the bins' giant decision cost ~2.5x that: LDS
 // histogram atomics, scalar-issue bound row batches); the next batch's loads are in
-// flight while a batch is packed.  gword[2] = 1: abits valid (G worth trying only).
+// flight while a batch is packed.  Round 6: only when superstep 3's scatter did not keep
+// the bits (gword[2] != 0: the bits of the bits-mode rebuild, the arcs whose column left
+// G cleared by that scatter -- a lower bound of each row's G votes, which the settle's
+// strict-majority test only needs).  gword[9] = 1: the bits are valid (G worth trying).
 __global__ __launch_bounds__(256) void k_abits_pass(const int32_t* __restrict__ al, int64_t p0, int64_t arcs,
                                                     int32_t* __restrict__ gword,
                                                     unsigned long long* __restrict__ abits) {
-  if (gword[1] == 0) return;  // uniform: no settle this superstep (gword[2] stays 0)
-  if (blockIdx.x == 0 && threadIdx.x == 0) gword[2] = 1;
+  if (gword[1] == 0) return;  // uniform: no settle this superstep
+  if (gword[2] != 0) return;  // uniform: the kept bits serve (no block writes gword[2] here)
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[9] = 1;
   const u32 G = (u32)gword[0];
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -2033,9 +2037,11 @@ static_assert(kSegArcs == 512, "unit of a position: (p - rp[row]) >> 9");
 // lanes (lane -> piece by a binary search over the inclusive piece prefix), so a
 // wave whose lanes hold runs of 17..256 positions writes them in parallel instead of
 // run after run with the whole wave.  Every lane of the wave must call it.
-__device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, const uint32_t* __restrict__ cpos,
+// clr (this lane's run): also clear the arc giant bits of its positions (a column that
+// left G, superstep 3's scatter keeping the bits of the bits-mode rebuild: k_al_scatter)
+__device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, bool clr, const uint32_t* __restrict__ cpos,
                                              int32_t* __restrict__ al, bool all, const FrontierMarks& fm,
-                                             int lane) {
+                                             unsigned long long* __restrict__ abits, int lane) {
   if (al == nullptr && all) return;  // gather mode without marks: nothing to write (uniform)
   const int k = (n + 15) >> 4;
   int incl = k;
@@ -2058,6 +2064,7 @@ __device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, cons
     const int64_t bo = __shfl(b, o, 64);
     const int no = __shfl(n, o, 64);
     const int32_t lv = __shfl(lab, o, 64);
+    const bool cl = __shfl((int)clr, o, 64) != 0;
     if (t < S) {
       const int p0 = (t - excl) * 16;
       const int cnt = min(16, no - p0);
@@ -2070,6 +2077,7 @@ __device__ __forceinline__ void scatter_runs(int64_t b, int n, int32_t lab, cons
         for (int u = 0; u < 4; ++u)
           if (q + u < cnt) {
             if (al) al[p[u]] = lv;   // gather mode: marks only
+            if (cl) atomicAnd(&abits[p[u] >> 6], ~(1ull << (p[u] & 63u)));
             if (!all) fm.mark(p[u]);
           }
       }
@@ -2122,16 +2130,27 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
                                                     int frontier, int64_t fr_thr,
                                                     int32_t* __restrict__ Lold,
                                                     const int32_t* __restrict__ col_fold, int64_t arcs,
-                                                    int32_t* __restrict__ gword) {
+                                                    int32_t* __restrict__ gword, int keep_bits,
+                                                    const uint32_t* __restrict__ gbits,
+                                                    unsigned long long* __restrict__ abits) {
   // the next superstep's counters (the other parity; no memset launch)
   if (blockIdx.x == 0 && threadIdx.x < 3) counters_next[threadIdx.x] = 0ull;
   const bool rebuild = rebuild_wanted(counters, thr);
   // al changes here (scatter, or the plain folded rebuild), so the arc giant bits go
-  // stale: gword[2] = 0.  (Keeping them in step with 64-bit atomics in the scatter cost
-  // 0.25 ms in superstep 3, more than a settled superstep 4 saves; superstep 4
-  // re-derives them with k_abits_pass instead.)  A wanted, non-folded rebuild follows
-  // this kernel and sets gword[2] itself.
-  if (blockIdx.x == 0 && threadIdx.x == 0 && (!rebuild || col_fold)) gword[2] = 0;
+  // stale: gword[2] = 0 -- except in superstep 3's scatter (keep_bits, host-set), right
+  // after the bits-mode rebuild whose bits they are: a column that LEFT G (its gbits
+  // bit, the rebuild's bitmap of the same vector and G) clears its positions' bits, one
+  // atomic each (rare: R-MAT superstep 3 moves labels onto G); a column that joined G
+  // leaves its bits clear.  The bits then hold a lower bound of every row's G votes, all
+  // superstep 4's settle needs, and its k_abits_pass is skipped (round 6; exact upkeep
+  // with an atomic per written position cost superstep 3 0.25 ms, round 3).  A wanted,
+  // non-folded rebuild follows this kernel and sets gword[2] itself.
+  const bool keep = keep_bits != 0 && !rebuild;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (!rebuild || col_fold) && !keep) gword[2] = 0;
+  const int32_t Gk = gword[0];
+  auto left_g = [&](int64_t u, int32_t lab) -> bool {
+    return keep && lab != Gk && ((gbits[u >> 5] >> (u & 31)) & 1u);
+  };
   // The next superstep tallies every row after a rebuild, with the frontier off, or
   // when more than fr_thr arcs changed: then nearly every row has a changed neighbour
   // anyway (R-MAT superstep 3 -> 4: 1.5 % of arcs dirty, 88 % of the arcs in dirty
@@ -2153,14 +2172,16 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
       int64_t b = 0;
       int n = 0;
       int32_t lab = 0;
+      bool clr = false;
       if (c < nl) {
         const int64_t u = chlist[c];
         b = cptr[u];
         n = (int)(cptr[u + 1] - b);  // <= kChunkPos
         lab = Ln[u];
         Lold[u] = lab;  // frontier sync (after the join)
+        clr = left_g(u, lab);
       }
-      scatter_runs(b, n, lab, cpos, al, all, fm, lane);
+      scatter_runs(b, n, lab, clr, cpos, al, all, fm, abits, lane);
     }
   }
   uint4* __restrict__ flw = const_cast<uint4*>(chflag16);
@@ -2186,6 +2207,7 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
       int64_t b = 0;
       int n = 0;
       int32_t lab = 0;
+      bool clr = false;
       if (bits) {
         const int t = __ffs(bits) - 1;
         bits &= bits - 1u;
@@ -2198,8 +2220,9 @@ __global__ __launch_bounds__(256) void k_al_scatter(const int32_t* __restrict__ 
         // frontier sync of a changed label into the next superstep's output vector
         // (after the join; every changed vertex with local arcs has a chunk 0)
         if (kk == 0) Lold[u] = lab;
+        clr = left_g(u, lab);
       }
-      scatter_runs(b, n, lab, cpos, al, all, fm, lane);
+      scatter_runs(b, n, lab, clr, cpos, al, all, fm, abits, lane);
     }
   }
 }
@@ -2275,6 +2298,7 @@ __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__
     gword[0] = G;
     gword[3] = 0;  // k_giant_bits counts the set bits of the hot slots here
     gword[5] = 0;  // no giant-code refresh unless k_code_mode takes it below
+    gword[9] = 0;  // no k_abits_pass since this refresh
     gword[1] = n > 0 && 5 * (int64_t)(m >> 32) >= n ? 1 : 0;
   }
 }
@@ -4254,6 +4278,10 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
   // gather mode (lpa_build): no al[] to keep -- the scatter only marks the rows the next
   // superstep re-tallies (and syncs the changed labels into Lc), no rebuild
   const bool gnow = gather_now(g);
+  // superstep 3's refresh keeps the arc giant bits of superstep 2's bits-mode rebuild
+  // (k_al_scatter; superstep 4's row settle reads them)
+  const bool keep_bits = g->since_reset == 2 && g->abits != nullptr && g->gbits != nullptr && !gnow &&
+                         g->keep_bits;
   if (g->al_pending && !gnow) {  // the column-run superstep after a lazy reset (al holds nothing)
     hipLaunchKernelGGL(k_al_fill_unless_rebuild, dim3(cap_grid((g->arcs / 4 + 255) / 256, 8192)), dim3(256), 0, s,
                        ctr, thr, (const v4i*)g->al0, (v4i*)g->al, g->arcs);
@@ -4265,7 +4293,8 @@ int launch_refresh(lpa_graph* g, const int32_t* Lc, const int32_t* Ln, bool diff
                      g->counters + 4 * (par ^ 1), g->cptr,
                      g->cpos, Ln, gnow ? (int32_t*)nullptr : g->al, thr, fm, g->fr_all + (par ^ 1),
                      g->frontier, (int64_t)(kFrontierFrac * (double)g->arcs), const_cast<int32_t*>(Lc),
-                     (fold_rebuild && !gnow) ? g->col : (const int32_t*)nullptr, g->arcs, g->gword);
+                     (fold_rebuild && !gnow) ? g->col : (const int32_t*)nullptr, g->arcs, g->gword,
+                     keep_bits ? 1 : 0, g->gbits, g->abits);
   LPA_HIP(hipGetLastError());
   LPA_TRACE_POINT("scatter");
   if (ev_scatter) LPA_HIP(hipEventRecord(ev_scatter, s));  // profiling: scatter | rebuild
