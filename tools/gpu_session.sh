@@ -3,6 +3,7 @@
 # STEPS (space-separated, in order; default "tests c3"):
 #   tests     pytest -m gpu (FILES, PER_TEST as tools/gpu_tests.sh)
 #   c3        bench.py default (C3, CPU baseline, outlier, quality)
+#   drv       the driver's command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   c3q       bench.py C3 without the CPU baseline, outlier and quality
 #   c2 / c4 / c5   bench.py --config C2 / C4 / C5 (no CPU baseline, outlier or quality)
 #   prof      rocprofv3 kernel trace + stats of the C3 bench (no CPU baseline)
@@ -35,6 +36,7 @@ for st in $STEPS; do
   case $st in
     tests) TAG=$TAG LIMIT=${LIMIT:-600} PER_TEST=${PER_TEST:-300} bash tools/gpu_tests.sh || exit 1 ;;
     c3) bench c3 400 ;;
+    drv) bench drv 500 --gpus 1 --steps 20 --warmup 5 ;;   # the driver's command
     c3q) bench c3q 300 --no-cpu-baseline --no-outlier --no-quality ;;
     c2) bench c2 300 --config C2 --no-cpu-baseline --no-outlier --no-quality ;;
     c4) bench c4 400 --config C4 --no-cpu-baseline --no-outlier --no-quality --steps 3 ;;
