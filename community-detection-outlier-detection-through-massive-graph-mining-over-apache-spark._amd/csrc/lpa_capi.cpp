@@ -235,6 +235,7 @@ int create_common(int32_t device, hipStream_t stream, const int32_t* src, const 
   if (const char* f = getenv("LPA_POW2_SLICES")) g->pow2_slices = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_GIANT_CODES")) g->codes_env = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_FUSED_BINS")) g->fused_bins = atoi(f) < 0 ? 0 : atoi(f) > 2 ? 2 : atoi(f);
+  if (const char* f = getenv("LPA_UNITS_PURE")) g->units_pure = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_KEEP_BITS")) g->keep_bits = atoi(f) ? 1 : 0;
   if (const char* f = getenv("LPA_CONV_STREAMS")) g->conv_streams = atoi(f) < 1 ? 1 : atoi(f) > 3 ? 3 : atoi(f);
   // internal builds (the outlier stage's L2 sub-graph): the locality order is a

@@ -166,6 +166,7 @@ struct lpa_graph {
   int pow2_slices = 1;    // LPA_POW2_SLICES=0: tight slices (ceil(V / P) rounded to 64)
   int fused_bins = 1;     // LPA_FUSED_BINS: converged supersteps' bins in one launch per stream
                           // (0: a launch per bin, 2: the wave bins keep theirs)
+  int units_pure = 1;     // LPA_UNITS_PURE=0: superstep 4 re-tallies every hub unit
   int keep_bits = 1;      // LPA_KEEP_BITS=0: superstep 3's scatter drops the arc giant bits
   int conv_streams = 2;   // LPA_CONV_STREAMS: streams of a converged superstep's tally (1-3)
   int64_t vpad = 0;       // nranks * slice
@@ -266,8 +267,9 @@ struct lpa_graph {
                                 //     [5] giant-code refresh taken (superstep 2 settles from al2),
                                 //     [6] superstep 2's wave bins: 0 = lists of the unsettled rows,
                                 //     [7] superstep 3's row bins (code refresh), [9] superstep 4's
-                                //     k_abits_pass ran (its bits valid for the rows below the hubs);
-                                //     16 words
+                                //     k_abits_pass ran (its bits valid for the rows below the hubs),
+                                //     [10] / [11] superstep 4's impure-unit list mode / count
+                                //     (k_units_pure); 16 words
   // giant codes (round 5, lpa_iter.hip "Giant codes"): the refresh after superstep 1 (or
   // 2), when one label G carries the hubs but not half the hot slots (R-MAT), writes a
   // 2-bit code per arc instead of al[] (code 0 = G, else 1 + a label hash mod 3; 16 arcs

@@ -1565,6 +1565,82 @@ __global__ __launch_bounds__(256) void k_lpa_units_giant(const T* __restrict__ a
   }
 }
 
+// Superstep 4 (the settle schedule, main stream, ahead of k_lpa_units): every hub unit is
+// re-tallied there so that the frontier supersteps find each unit's words staged.  A unit
+// whose every arc votes G stages its one word (len, G) here without a tally: an arc votes G
+// when its giant bit is set, or -- the bits kept through superstep 3's scatter are a lower
+// bound, its joiners' bits clear -- when its al[] entry is G.  A lane per 64-arc chunk, eight
+// units per wave; a lane reads its chunk's bit words and only the al[] entries of the clear
+// bits, stopping at the first non-G vote.  The other units are listed (ulist, count
+// gword[11], zeroed by k_giant_pick; a block's ids gathered in LDS first) for k_lpa_units in list mode (gword[10] = 0, its
+// "fr_all").  Only with the kept bits (gword[2]: nothing writes them during superstep 4);
+// otherwise gword[10] = 1 and k_lpa_units takes every unit.
+constexpr int kPureIds = 8192;  // units per k_units_pure block (its LDS list)
+__global__ __launch_bounds__(256) void k_units_pure(const int32_t* __restrict__ al,
+                                                    const unsigned long long* __restrict__ abits, int64_t arcs,
+                                                    const Segment* __restrict__ units, int64_t nunits,
+                                                    int32_t* __restrict__ gword, u64* __restrict__ stage,
+                                                    int32_t* __restrict__ ucnt, int32_t* __restrict__ ulist) {
+  __shared__ int32_t lids[kPureIds];
+  __shared__ int ln, lbase;
+  const bool on = gword[2] != 0 && gword[1] != 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) gword[10] = on ? 0 : 1;
+  if (!on) return;  // uniform
+  const int32_t G = gword[0];
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 7;
+  const int64_t nwords = (arcs + 63) >> 6;
+  // this block's units: a contiguous range of <= kPureIds (the host sizes the grid)
+  const int64_t per = (nunits + gridDim.x - 1) / gridDim.x;
+  const int64_t ub = (int64_t)blockIdx.x * per, ue = min(nunits, ub + per);
+  if (threadIdx.x == 0) ln = 0;
+  __syncthreads();
+  for (int64_t u0 = ub + (threadIdx.x >> 6) * 8; u0 < ue; u0 += 32) {
+    const int64_t u = u0 + (lane >> 3);
+    bool ok = true;
+    int64_t begin = 0;
+    int len = 0;
+    if (u < ue) {
+      const Segment d = units[u];
+      begin = d.begin;
+      len = d.len & 1023;
+      const int lo = c * 64, n = min(len - lo, 64);
+      if (n > 0) {
+        const int64_t a = begin + lo;
+        const int64_t wq = a >> 6;
+        const int off = (int)(a & 63);
+        u64 bits = abits[wq] >> off;
+        if (off && off + n > 64 && wq + 1 < nwords) bits |= abits[wq + 1] << (64 - off);
+        u64 clear = ~bits & (n == 64 ? ~0ull : ((1ull << n) - 1ull));
+        while (clear) {
+          const int k = __ffsll((unsigned long long)clear) - 1;
+          clear &= clear - 1ull;
+          if (al[a + k] != G) {
+            ok = false;
+            break;
+          }
+        }
+      }
+    }
+    const u64 bad = __ballot(!ok);
+    const bool pure = ((bad >> (lane & ~7)) & 0xFFull) == 0ull;
+    const bool head = u < ue && c == 0;
+    if (head && pure) {
+      stage[begin] = ((u64)(u32)len << 32) | (u64)(u32)(~(u32)G);
+      ucnt[u] = 1;
+    }
+    if (head && !pure) lids[atomicAdd(&ln, 1)] = (int32_t)u;
+  }
+  // the block's impure units into the list: one global atomic per block (returning
+  // atomics on one address serialise: a list atomic per wave cost C5 ~3 ms)
+  __syncthreads();
+  const int n = ln;
+  if (n == 0) return;  // uniform
+  if (threadIdx.x == 0) lbase = atomicAdd(&gword[11], n);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256) ulist[lbase + i] = lids[i];
+}
+
 // ---------------------------------------------------------------------------
 // refresh of the replicated neighbour labels al[]
 // ---------------------------------------------------------------------------
@@ -2299,6 +2375,7 @@ __global__ __launch_bounds__(1024) void k_giant_pick(const int32_t* __restrict__
     gword[3] = 0;  // k_giant_bits counts the set bits of the hot slots here
     gword[5] = 0;  // no giant-code refresh unless k_code_mode takes it below
     gword[9] = 0;  // no k_abits_pass since this refresh
+    gword[11] = 0;  // superstep 4's impure-unit list (k_units_pure)
     gword[1] = n > 0 && 5 * (int64_t)(m >> 32) >= n ? 1 : 0;
   }
 }
@@ -3904,6 +3981,16 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     if (n_units > 0 && giant_units) {
       hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
                          g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist2, g->gdec, g->gdec + 3, pmax);
+      LPA_HIP(hipGetLastError());
+    } else if (n_units > 0 && settle4 && g->units_pure) {
+      // superstep 4: the pure-G units staged without a tally, the others listed
+      const int64_t npb = std::max<int64_t>((n_units + 2047) / 2048, 32);  // units per block
+      hipLaunchKernelGGL(k_units_pure, dim3((unsigned)((n_units + std::min<int64_t>(npb, kPureIds) - 1) /
+                                                       std::min<int64_t>(npb, kPureIds))), dim3(256), 0, s, g->al,
+                         g->abits, g->arcs, g->segs, n_units, g->gword, g->stage, g->ucnt, g->ulist2);
+      LPA_HIP(hipGetLastError());
+      hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,
+                         g->al, g->segs, n_units, g->stage, g->ucnt, g->ulist2, g->gword + 11, g->gword + 10, pmax);
       LPA_HIP(hipGetLastError());
     } else if (n_units > 0) {
       hipLaunchKernelGGL(k_lpa_units, dim3(cap_grid((n_units + 3) / 4, 2048)), dim3(256), 0, s,

@@ -265,7 +265,7 @@ def test_schedules_identical(gfa, graph):
 @pytest.mark.parametrize("env", [{"LPA_SERIAL": "1"}, {"LPA_FIRST_RUNS": "0"}, {"LPA_GRAPHS": "0"},
                                  {"LPA_REBUILD_HOT": "0"}, {"LPA_FRONTIER": "0"}, {"LPA_LOCALITY": "0"},
                                  {"LPA_FUSED_BINS": "0"}, {"LPA_FUSED_BINS": "2", "LPA_CONV_STREAMS": "3"},
-                                 {"LPA_CONV_STREAMS": "1"}, {"LPA_KEEP_BITS": "0"}])
+                                 {"LPA_CONV_STREAMS": "1"}, {"LPA_KEEP_BITS": "0"}, {"LPA_UNITS_PURE": "0"}])
 def test_schedule_options_bit_exact(gfa, oracle, monkeypatch, env):
     """The switches read at graph creation (the serialized profiling
     schedule, superstep 1 by hash tallies, no captured graphs, the plain rebuild, no
