@@ -29,9 +29,34 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/lpa.h"
 
 
+def _bundle_targets(data):
+    """Target ids of the library's offload bundles: plain bundles carry them in the clear;
+    compressed ones (csrc/Makefile builds with --offload-compress: a "CCOB" header, version,
+    method, then the bundle's total size) are listed by clang-offload-bundler."""
+    import shutil
+    import struct
+    import subprocess
+    import tempfile
+
+    if b"__CLANG_OFFLOAD_BUNDLE__" in data:
+        return data.decode("latin-1")
+    i = data.find(b"CCOB")
+    assert i >= 0, "no offload bundle in the library"
+    total = struct.unpack_from("<Q", data, i + 8)[0]
+    tool = shutil.which("clang-offload-bundler") or "/opt/rocm/lib/llvm/bin/clang-offload-bundler"
+    with tempfile.NamedTemporaryFile(suffix=".ccob") as f:
+        f.write(data[i:i + total])
+        f.flush()
+        out = subprocess.run([tool, "--list", "--type=o", f"--input={f.name}"], capture_output=True, text=True,
+                             check=True)
+    return out.stdout
+
+
 def test_library_is_hip_gfx950():
     data = open(_lib.LIB_PATH, "rb").read()
-    assert b"gfx950" in data and b"k_lpa_wave" in data and b"k_lpa_group" in data
+    # the kernels' host-side registration names, and a gfx950 device code object
+    assert b"k_lpa_wave" in data and b"k_lpa_group" in data
+    assert "gfx950" in _bundle_targets(data)
 
 
 def test_no_device_fails_loudly():
