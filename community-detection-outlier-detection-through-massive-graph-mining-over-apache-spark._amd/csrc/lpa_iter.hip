@@ -1612,13 +1612,21 @@ __global__ __launch_bounds__(256) void k_units_pure(const int32_t* __restrict__ 
         u64 bits = abits[wq] >> off;
         if (off && off + n > 64 && wq + 1 < nwords) bits |= abits[wq + 1] << (64 - off);
         u64 clear = ~bits & (n == 64 ? ~0ull : ((1ull << n) - 1ull));
-        while (clear) {
-          const int k = __ffsll((unsigned long long)clear) - 1;
-          clear &= clear - 1ull;
-          if (al[a + k] != G) {
-            ok = false;
-            break;
+        // the clear bits' al[] entries eight at a time, every load issued before the first
+        // compare (unused slots re-read the chunk's first entry): a chunk of a hub row holds
+        // several joiners, and one dependent load after another cost ~5x
+        while (clear && ok) {
+          int pos[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            pos[k] = clear ? __ffsll((unsigned long long)clear) - 1 : 0;
+            clear &= clear - 1ull;
           }
+          int32_t v[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = al[a + pos[k]];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) ok = ok && v[k] == G;  // (a padding slot's arc is the chunk's too)
         }
       }
     }
