@@ -2401,6 +2401,11 @@ __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __
                                                     unsigned long long* __restrict__ abits, int64_t nzero,
                                                     uint64_t hmask, int64_t hlim) {
   if (kIfWanted && !rebuild_wanted(counters, thr)) return;
+  // the hot-bit count: summed per block in LDS, one global atomic per block (a returning
+  // atomic per wave on the one word serialised: ~2,500 of them, ~30 us at C3)
+  __shared__ u32 bcnt;
+  if (threadIdx.x == 0) bcnt = 0u;
+  __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += (int64_t)gridDim.x * blockDim.x)
     abits[i] = 0ull;
   const int32_t G = gword[0];
@@ -2426,9 +2431,11 @@ __global__ __launch_bounds__(256) void k_giant_bits(const unsigned long long* __
     const bool hot = lane < 8 && wi < n && (int64_t)((uint64_t)wi & hmask) < hlim;
     if (__ballot(hot)) {
       const u32 c = wave_sum_u32(hot ? (u32)__popcll(mine) : 0u);
-      if (lane == 0 && c) atomicAdd(&gword[3], (int32_t)c);
+      if (lane == 0 && c) atomicAdd(&bcnt, c);
     }
   }
+  __syncthreads();
+  if (threadIdx.x == 0 && bcnt) atomicAdd(&gword[3], (int32_t)bcnt);
 }
 
 // al[i] = lab(col[i]) over every arc by the calling grid (one wave per 512-arc batch,
