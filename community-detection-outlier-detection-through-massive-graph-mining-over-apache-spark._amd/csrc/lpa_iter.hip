@@ -1727,15 +1727,25 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
       }
       c += (unsigned long long)__popc(chg);
     }
+    // (the counts summed per block first: one atomic per block on the counter, not one
+    // per wave -- the same-address atomics of ~8 K waves queue at the counter's channel)
+    __shared__ unsigned long long csum;
+    if (threadIdx.x == 0) csum = 0ull;
+    __syncthreads();
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&counters[2], c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&csum, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && csum) atomicAdd(&counters[2], csum);
     return;
   }
   __shared__ int32_t q_col[kDiffQuads * 4];
   __shared__ int qn;
-  __shared__ unsigned long long base_s;
+  __shared__ unsigned long long base_s, dsum;
   const int lane = threadIdx.x & 63;
-  if (threadIdx.x == 0) qn = 0;
+  if (threadIdx.x == 0) {
+    qn = 0;
+    dsum = 0ull;
+  }
   __syncthreads();
   unsigned long long dirty = 0;
   auto emit = [&](int64_t u, int32_t nb) {
@@ -1780,8 +1790,9 @@ __global__ __launch_bounds__(256) void k_diff(const int4* __restrict__ Lc4,
     }
   }
   for (int off = 32; off > 0; off >>= 1) dirty += __shfl_xor(dirty, off, 64);
-  if (lane == 0 && dirty) atomicAdd(&counters[1], dirty);
+  if (lane == 0 && dirty) atomicAdd(&dsum, dirty);
   __syncthreads();
+  if (threadIdx.x == 0 && dsum) atomicAdd(&counters[1], dsum);
   const int n = qn;
   if (n == 0) return;  // uniform
   if (threadIdx.x == 0) base_s = atomicAdd(&counters[0], (unsigned long long)n);
