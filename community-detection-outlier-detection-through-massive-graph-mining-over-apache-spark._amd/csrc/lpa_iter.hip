@@ -2734,7 +2734,11 @@ __device__ __forceinline__ void rebuild_pieces(P1 p1, P2 p2, int32_t G, bool bit
 // r's slice are its first slots (degree rank k lives at slot (k mod P) S + k / P),
 // so the global top set is the first H slots of every slice: slot c is hot iff
 // (c mod S) < H, at LDS index (c / S) H + c mod S (H = 2^hot_lg labels or 2^hb_lg bits).
-template <bool kIfWanted, bool kRanked>
+// kPieces (P = 1, a class-blocked handle: its labels-mode rebuild goes through the pieces):
+// its own instantiation, so that the plain one's registers are allocated without the
+// pieces' descriptor ring (one form for both spilled 16 VGPRs to scratch at the 128 of
+// four waves per SIMD)
+template <bool kIfWanted, bool kRanked, bool kPieces = false>
 __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long long* __restrict__ counters,
                                                          int64_t thr, const int32_t* __restrict__ col,
                                                          int64_t arcs, const int32_t* __restrict__ Ln,
@@ -2809,11 +2813,15 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
     // index, the gbits word / the label at a fixed address where it is not needed (the
     // wave's lanes then share one line)
     const u32 nhbu = (u32)nhb;
+    // (the slots' labels through a buffer descriptor: launch_rebuild takes this kernel at
+    // P = 1 only up to kHotMaxSlots = 2^29 slots, so every byte offset fits the voffset)
+    const auto ln_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Ln, 0, (int)(nbits * 4), 0x00020000);
+    constexpr int kPast = (int)0x80000000u;  // past every record count: no request
     auto run = [&](auto p1, auto p2, bool wbits) {
       // uniform: labels / hybrid mode of a blocked handle (the bits mode through the
       // pieces measured slower, round 6: C5 superstep 3 13.4 -> 17.4 ms, C4 superstep 2
       // 8.9 -> 12.8 ms -- its lookups hit LDS / L2 anyway, the split arc ranges cost)
-      if (!bits && pieces) {
+      if (kPieces && !bits) {
         const int grp = blockIdx.x & 7;
         const int64_t nwv = (int64_t)(gridDim.x >> 3) * (blockDim.x >> 6);
         const int64_t wi = (int64_t)(blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -2836,24 +2844,32 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
       }
     };
     if (bits) {
+      // the gbits words and the labels through buffer descriptors (base + 32-bit offset:
+      // two VGPRs fewer per address under the 128 of four waves per SIMD, where the 64-bit
+      // form spilled 14), and a lane that needs no word or label takes an offset past the
+      // records: the range check drops its request instead of re-reading a fixed line
+      const auto gb_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)gbits, 0, (int)(((nbits + 31) >> 5) * 4), 0x00020000);
       run(
           [&](int c) -> u32 {
             const bool h = (u32)c < nhbu;
             const u32 hw = hot[(h ? (u32)c : nhbu - 1u) >> 5];
-            const u32 gw = gbits[h ? 0u : (u32)c >> 5];
+            const u32 gw = __builtin_amdgcn_raw_buffer_load_b32(gb_rsrc, h ? kPast : (int)(((u32)c >> 5) << 2), 0, 0);
             return h ? hw : gw;
           },
           [&](int c, u32 w) -> int32_t {
             const bool g = (w >> ((u32)c & 31u)) & 1u;
-            const int32_t x = Ln[g ? 0 : c];
+            const int32_t x = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ln_rsrc, g ? kPast : (int)((u32)c << 2), 0, 0);
             return g ? G : x;
           },
           true);
     } else {
+#ifdef LPA_DIAG_BITS_ONLY
+      return;
+#endif
       run([&](int c) -> u32 { return hot[(u32)c < nh ? (u32)c : nh - 1u]; },
           [&](int c, u32 w) -> int32_t {
             const bool h = (u32)c < nh;
-            const int32_t x = Ln[h ? 0 : c];
+            const int32_t x = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ln_rsrc, h ? kPast : (int)((u32)c << 2), 0, 0);
             return h ? (int32_t)w : x;
           },
           hyb);
@@ -4211,6 +4227,7 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
 
 // al[] rebuild: the LDS hot-label kernel on a single-GPU handle (hub slots are
 // [0, kHotLabels) there), the plain one otherwise
+constexpr int64_t kHotMaxSlots = int64_t(1) << 29;  // k_al_rebuild_hot's 32-bit label offsets (P = 1)
 int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
                    const unsigned long long* ctr) {
   hipStream_t s = g->stream;
@@ -4242,7 +4259,7 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
       hipLaunchKernelGGL(k_al_rebuild_small<false>, dim3(gr), dim3(256), 0, s, ctr, thr, g->col, g->arcs, L, g->al,
                          g->gbits, g->vpad, g->gword, g->abits);
     }
-  } else if (g->rebuild_hot && (g->nranks == 1 || ranked)) {
+  } else if (g->rebuild_hot && ((g->nranks == 1 && g->vpad <= kHotMaxSlots) || ranked)) {
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
     int slice_lg = 0, hot_lg = 0, hb_lg = 0;
@@ -4276,8 +4293,8 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
     for (int x = 0; x <= kMaxBlkClasses; ++x) binfo.off[x] = g->blk_off[x];
     binfo.a0 = blk ? g->blk_a0 : 0;
     binfo.phases = g->blk_classes / 8;
-#define LPA_HOT_LAUNCH(W, R)                                                                     \
-  hipLaunchKernelGGL((k_al_rebuild_hot<W, R>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
+#define LPA_HOT_LAUNCH(W, R, B)                                                                  \
+  hipLaunchKernelGGL((k_al_rebuild_hot<W, R, B>), dim3(dev_cus), dim3(1024), 0, s, ctr, thr, g->col, \
                      g->arcs, L, nhot, g->al, slice_lg, hot_lg, hb_lg, g->gbits, nbits, g->gword, g->abits, \
                      blk ? g->blk_pieces : nullptr, binfo, code ? g->gword + 5 : nullptr)
     if (code) {
@@ -4285,9 +4302,13 @@ int launch_rebuild(lpa_graph* g, bool if_wanted, int64_t thr, const int32_t* L,
       LPA_HIP(hipGetLastError());
     }
     if (if_wanted) {
-      if (ranked) LPA_HOT_LAUNCH(true, true); else LPA_HOT_LAUNCH(true, false);
+      if (ranked) LPA_HOT_LAUNCH(true, true, false);
+      else if (blk) LPA_HOT_LAUNCH(true, false, true);
+      else LPA_HOT_LAUNCH(true, false, false);
     } else {
-      if (ranked) LPA_HOT_LAUNCH(false, true); else LPA_HOT_LAUNCH(false, false);
+      if (ranked) LPA_HOT_LAUNCH(false, true, false);
+      else if (blk) LPA_HOT_LAUNCH(false, false, true);
+      else LPA_HOT_LAUNCH(false, false, false);
     }
 #undef LPA_HOT_LAUNCH
     if (code) {
