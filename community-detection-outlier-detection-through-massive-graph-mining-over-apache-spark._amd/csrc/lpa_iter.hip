@@ -2863,9 +2863,6 @@ __global__ __launch_bounds__(1024) void k_al_rebuild_hot(const unsigned long lon
           },
           true);
     } else {
-#ifdef LPA_DIAG_BITS_ONLY
-      return;
-#endif
       run([&](int c) -> u32 { return hot[(u32)c < nh ? (u32)c : nh - 1u]; },
           [&](int c, u32 w) -> int32_t {
             const bool h = (u32)c < nh;
