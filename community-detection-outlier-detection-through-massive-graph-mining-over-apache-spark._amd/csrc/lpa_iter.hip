@@ -3264,18 +3264,22 @@ __device__ __forceinline__ void code_settle_wave(const int64_t* __restrict__ rp,
   }
 }
 
+// W words per row: 5 for the row bins (<= 64 arcs), 9 for w2 (<= 128), 17 for w4 (<= 256)
+// -- a lane per row issues all its words at once, so a wave has 64 rows' loads in flight
+// where a wave per row had three (the w2 / w4 rows in code_settle_wave: latency-bound)
+template <int W>
 __device__ __forceinline__ void code_settle_rows(const int64_t* __restrict__ rp, const uint32_t* __restrict__ al2,
                                                  int64_t vbeg, int64_t vend, int32_t G, int32_t* __restrict__ Ln,
                                                  uint8_t* __restrict__ rdirty, int64_t bx, int64_t nbx) {
   for (int64_t v = vbeg + bx * 256 + threadIdx.x; v < vend; v += nbx * 256) {
     const int64_t b = rp[v], e = rp[v + 1];
     const int64_t w0 = b >> 4, wl = e > b ? (e - 1) >> 4 : w0;
-    u32 wd[5];
+    u32 wd[W];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) wd[k] = al2[w0 + k <= wl ? w0 + k : wl];
+    for (int k = 0; k < W; ++k) wd[k] = al2[w0 + k <= wl ? w0 + k : wl];
     u32 x = 0, y = 0;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) code2_counts(wd[k], code2_fmask(w0 + k, b, e), x, y);
+    for (int k = 0; k < W; ++k) code2_counts(wd[k], code2_fmask(w0 + k, b, e), x, y);
     const bool settled = code2_decided(x, y);
     if (settled) Ln[v] = G;
     rdirty[v] = settled ? 0 : 1;
@@ -3304,9 +3308,9 @@ __global__ __launch_bounds__(256) void k_code_settle(const int64_t* __restrict__
   switch (t) {
     case 0: code_settle_wave<16>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
     case 1: code_settle_wave<8>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
-    case 2: code_settle_wave<4>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
-    case 3: code_settle_wave<2>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
-    default: code_settle_rows(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
+    case 2: code_settle_rows<17>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
+    case 3: code_settle_rows<9>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
+    default: code_settle_rows<5>(rp, al2, vb, ve, G, Ln, rdirty, bx, nbx); break;
   }
 }
 
@@ -3755,7 +3759,7 @@ bool code_tally3_now(const lpa_graph* g) { return g->code_ok && g->since_reset =
 int launch_code_settle(lpa_graph* g, hipStream_t st, int32_t* Lown) {
   const int64_t* bb = g->bin_begin;
   const int bins[7] = {BIN_W16, BIN_W8, BIN_W4, BIN_W2, BIN_G64, BIN_G32, BIN_G16};
-  const int lanes[7] = {64, 64, 64, 64, 4, 4, 4};   // work per row: a wave; a lane's <= 5 loads
+  const int lanes[7] = {64, 64, 16, 8, 4, 4, 4};   // work per row: a wave; a lane's W loads
   CodeTasks ct;
   int64_t work[7], tot = 0;
   for (int t = 0; t < 7; ++t) {
@@ -3764,12 +3768,15 @@ int launch_code_settle(lpa_graph* g, hipStream_t st, int32_t* Lown) {
     work[t] = (ct.vend[t] - ct.vbeg[t]) * lanes[t];
     tot += work[t];
   }
-  const int64_t kBlocks = 4096;   // 16 waves per CU
+#ifndef LPA_CODE_SETTLE_BLOCKS
+#define LPA_CODE_SETTLE_BLOCKS 4096
+#endif
+  const int64_t kBlocks = LPA_CODE_SETTLE_BLOCKS;   // 16 waves per CU
   ct.first[0] = 0;
   for (int t = 0; t < 7; ++t) {
     int64_t nb = tot > 0 ? (work[t] * kBlocks + tot - 1) / tot : 0;
     const int64_t rows = ct.vend[t] - ct.vbeg[t];
-    const int64_t need = t < 4 ? (rows + 3) / 4 : (rows + 255) / 256;
+    const int64_t need = t < 2 ? (rows + 3) / 4 : (rows + 255) / 256;
     if (nb > need) nb = need;
     if (work[t] > 0 && nb < 1) nb = 1;
     ct.first[t + 1] = ct.first[t] + (int32_t)nb;
