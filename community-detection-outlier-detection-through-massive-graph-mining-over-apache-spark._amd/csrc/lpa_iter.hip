@@ -3849,17 +3849,29 @@ int launch_tally(lpa_graph* g, int32_t* Lown, hipEvent_t* bev, const int32_t* Lc
     // kernel returns at once unless they are valid): the others' dirty flags, then the
     // lists of this superstep are built from them in list mode
     if (g->since_reset == 2 && g->abits && !block_mode_now(g) && !code_tally3_now(g)) {
+      const int64_t r0 = g->n_hub, r1 = g->bin_begin[BIN_ISO];
+      // the hub rows (main) and the rows below them (aux0) settle side by side: disjoint
+      // rows, both read only abits; joined before the commit
+      const bool fork_settle = sb != s && g->n_hub > 0 && r1 > r0;
+      if (fork_settle) {
+        LPA_HIP(hipEventRecord(g->ev_fork, s));
+        LPA_HIP(hipStreamWaitEvent(sb, g->ev_fork, 0));
+      }
       if (g->n_hub > 0) {
         hipLaunchKernelGGL(k_settle_big, dim3(cap_grid((g->n_hub + 3) / 4, 2048)), dim3(256), 0, s, g->rp,
                            g->abits, g->n_hub, fr_all, g->gword, Lown, g->rdirty[g->par], g->udirty[g->par],
                            g->hub_uoff);
         LPA_HIP(hipGetLastError());
       }
-      const int64_t r0 = g->n_hub, r1 = g->bin_begin[BIN_ISO];
       if (r1 > r0) {
-        hipLaunchKernelGGL(k_settle_rows, dim3(cap_grid((r1 - r0 + 255) / 256, 8192)), dim3(256), 0, s, g->rp,
-                           g->abits, r0, r1, fr_all, g->gword, Lown, g->rdirty[g->par]);
+        hipLaunchKernelGGL(k_settle_rows, dim3(cap_grid((r1 - r0 + 255) / 256, 8192)), dim3(256), 0,
+                           fork_settle ? sb : s, g->rp, g->abits, r0, r1, fr_all, g->gword, Lown,
+                           g->rdirty[g->par]);
         LPA_HIP(hipGetLastError());
+      }
+      if (fork_settle) {
+        LPA_HIP(hipEventRecord(g->ev_join2[2], sb));
+        LPA_HIP(hipStreamWaitEvent(s, g->ev_join2[2], 0));
       }
       hipLaunchKernelGGL(k_settle_commit, dim3(1), dim3(1), 0, s, const_cast<int32_t*>(fr_all), g->gword, fcnt);
       LPA_HIP(hipGetLastError());
